@@ -1,0 +1,146 @@
+/*
+ * qldpc_hip.h — C ABI of the MI355X (gfx950) Monte Carlo BP decoding engine.
+ *
+ * The reference's hot path is Python calling the third-party `ldpc`
+ * bp_decoder once per shot.  Each entry point below replaces
+ * one reference interface; the Python host layer (qldpc_fault_tolerance_amd/)
+ * binds them with ctypes exactly as INTEGRATION.md shows.
+ *
+ * Conventions: every function returns 0 on success or a negative error code
+ * (see QLDPC_E*), and qldpc_last_error() returns a thread-local message.
+ * Device pointers (d_*) are plain device addresses (e.g. torch
+ * Tensor.data_ptr()); `stream` is a hipStream_t passed as void* (NULL = the
+ * legacy default stream).  Handles are not thread-safe: one host thread per
+ * handle; distinct handles may be used concurrently.
+ */
+#ifndef QLDPC_HIP_H
+#define QLDPC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QLDPC_ABI_VERSION 1
+
+#define QLDPC_OK 0
+#define QLDPC_EINVAL -1   /* bad argument (shape, range, NULL)            */
+#define QLDPC_EHIP -2     /* HIP runtime error (message has hipGetErrorString) */
+#define QLDPC_ENOMEM -3   /* allocation failed                            */
+#define QLDPC_ENOTSUP -4  /* graph/method combination not supported       */
+
+/* bp_method, as the strings the reference passes (src/Decoders.py:80-84) */
+#define QLDPC_PRODUCT_SUM 0
+#define QLDPC_MIN_SUM 1
+
+/* logical_mode = eval_logical_type of CodeSimulator_DataError (src/Simulators.py:162-168) */
+#define QLDPC_LOGICAL_X 0
+#define QLDPC_LOGICAL_Z 1
+#define QLDPC_LOGICAL_TOTAL 2
+
+#define QLDPC_HIST_BINS 1025 /* iteration histogram bins (iter 0..1024; last bin = >=1024) */
+
+typedef struct qldpc_graph qldpc_graph;
+typedef struct qldpc_bp qldpc_bp;
+typedef struct qldpc_mc qldpc_mc;
+
+/* Counters of one fused Monte Carlo run (summed over calls if not reset). */
+typedef struct {
+  int64_t shots;               /* shots simulated                                */
+  int64_t failures;            /* shots whose eval_logical_type outcome failed   */
+  int64_t sector_decodes[2];   /* [0] = X errors on hz, [1] = Z errors on hx      */
+  int64_t sector_iters[2];     /* sum of BP iterations                            */
+  int64_t sector_nonconv[2];   /* decodes that hit max_iter without H x == s      */
+  int64_t sector_fail[2];      /* sector failures (syndrome mismatch or logical)  */
+  int64_t iter_hist[2][QLDPC_HIST_BINS];
+} qldpc_counters;
+
+int qldpc_abi_version(void);
+const char *qldpc_last_error(void);
+int qldpc_device_count(int *out);
+
+/*
+ * Tanner graph of a parity-check matrix H (m x n), CSR with columns ascending
+ * inside each row (the `mod2sparse` order `ldpc` builds from the ndarray it is
+ * given: src/Decoders.py:80, `bp_decoder(parity_check_matrix=h, ...)`).
+ * Copied to the device; the caller's arrays may be freed after the call.
+ */
+int qldpc_graph_create(int device, int32_t m, int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
+                       qldpc_graph **out);
+int qldpc_graph_destroy(qldpc_graph *g);
+int qldpc_graph_info(const qldpc_graph *g, int32_t *m, int32_t *n, int32_t *nnz, int32_t *max_row_deg,
+                     int32_t *max_col_deg);
+
+/*
+ * BP decoder on a graph: replaces `ldpc.bp_decoder(parity_check_matrix=h,
+ * channel_probs=..., max_iter=..., bp_method=..., ms_scaling_factor=...)`
+ * (src/Decoders.py:80-84, :52-56; src/Decoders_SpaceTime.py:207-213).
+ *   channel_probs : host array of n doubles (priors log((1-p)/p) computed on
+ *                   the host with libm, as the Cython does);
+ *   max_iter      : <= 0 means n (ldpc's default);
+ *   ms_scaling_factor : alpha; 0 selects alpha = 1 - 2^-iter;
+ *   precision     : 64 = float64 messages (reference arithmetic, bit-exact
+ *                   with the oracle), 32 = float32 fast mode (same op order).
+ *   vars_per_thread : 0 = automatic; else variables per thread (tuning knob).
+ *   min_col_slots : 0 = automatic; else edge slots per variable are at least
+ *                   this (4 or 8) — lets the two sectors of one MC run share a
+ *                   kernel variant when hx and hz have different column degrees.
+ */
+int qldpc_bp_create(qldpc_graph *g, const double *channel_probs, int32_t max_iter, int32_t bp_method,
+                    double ms_scaling_factor, int32_t precision, int32_t vars_per_thread, int32_t min_col_slots,
+                    qldpc_bp **out);
+int qldpc_bp_destroy(qldpc_bp *bp);
+int qldpc_bp_set_channel_probs(qldpc_bp *bp, const double *channel_probs);
+
+/*
+ * Decode B syndromes: the batched form of `bp_decoder.decode(synd)` (and
+ * BPDecoder.decode, src/Decoders.py:88-90).
+ *   d_synd  : uint8 [B][m] 0/1          d_corr : uint8 [B][n] 0/1 (output)
+ *   d_iters : int32 [B] or NULL         d_conv : uint8 [B] or NULL
+ */
+int qldpc_bp_decode_batch(qldpc_bp *bp, const uint8_t *d_synd, uint8_t *d_corr, int32_t *d_iters,
+                          uint8_t *d_conv, int64_t B, void *stream);
+
+/*
+ * Fused Monte Carlo shot loop = CodeSimulator_DataError._single_run
+ * (src/Simulators.py:117-168) for many shots in one launch: per shot sample
+ * the Pauli error (3-way split of u, :99-113), syndrome H e, BP decode,
+ * residual, failure = (H r != 0) or (L r != 0).
+ *   dec_x, logical_x : decoder on hz and the lz logicals (sector X);
+ *   dec_z, logical_z : decoder on hx and the lx logicals (sector Z); either
+ *                      sector may be NULL if logical_mode does not need it.
+ * Shots are keyed by their global index: shot s, qubit j draws
+ * u = Philox4x32-10(key = seed, ctr = (j, s_lo, s_hi, stream)) as a 53-bit
+ * double, so any shot range sharded over devices reproduces the same counts.
+ */
+int qldpc_mc_create(qldpc_bp *dec_x, const qldpc_graph *logical_x, qldpc_bp *dec_z,
+                    const qldpc_graph *logical_z, qldpc_mc **out);
+int qldpc_mc_destroy(qldpc_mc *mc);
+
+/* Async launch: counters accumulate in device memory (d_counters, a
+ * qldpc_counters-sized device buffer, zeroed by the caller).  uniforms: NULL
+ * => Philox, else device doubles [shot_count][n] (bit-exact replays of an
+ * external u stream, e.g. CPython random()).  Optional per-shot outputs
+ * (device, NULL to skip): d_fail uint8 [S] (bit0 X-sector fail, bit1 Z),
+ * d_err uint8 [S][n] (bit0 x, bit1 z), d_corr uint8 [S][2][n], d_iters
+ * int32 [S][2].  grid_blocks <= 0 selects a persistent grid sized to the device.
+ */
+int qldpc_mc_launch(qldpc_mc *mc, double px, double py, double pz, uint64_t seed, uint64_t shot_begin,
+                    int64_t shot_count, int32_t logical_mode, const double *d_uniforms, void *d_counters,
+                    uint8_t *d_fail, uint8_t *d_err, uint8_t *d_corr, int32_t *d_iters, int32_t grid_blocks,
+                    void *stream);
+
+/* Synchronous convenience: launch + copy counters to host (accumulating into *out). */
+int qldpc_mc_run(qldpc_mc *mc, double px, double py, double pz, uint64_t seed, uint64_t shot_begin,
+                 int64_t shot_count, int32_t logical_mode, qldpc_counters *out, void *stream);
+
+/* Launch geometry chosen for a decoder (threads per shot, vars per thread,
+ * LDS bytes, resident blocks per CU) — reported by bench.py / DESIGN.md. */
+int qldpc_bp_geometry(const qldpc_bp *bp, int32_t *threads, int32_t *vars_per_thread, int32_t *lds_bytes,
+                      int32_t *blocks_per_cu);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QLDPC_HIP_H */

@@ -1,0 +1,156 @@
+"""ctypes wrapper of the CPU restatement (oracle/qldpc_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libqldpc_oracle.so")
+
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [("shots", ctypes.c_int64), ("failures", ctypes.c_int64),
+                ("sector_decodes", ctypes.c_int64 * 2), ("sector_iters", ctypes.c_int64 * 2),
+                ("sector_nonconv", ctypes.c_int64 * 2), ("sector_fail", ctypes.c_int64 * 2)]
+
+    def as_dict(self):
+        return {"shots": self.shots, "failures": self.failures,
+                "sector_decodes": list(self.sector_decodes), "sector_iters": list(self.sector_iters),
+                "sector_nonconv": list(self.sector_nonconv), "sector_fail": list(self.sector_fail)}
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.oracle_bp_decode_batch.restype = ctypes.c_int
+        L.oracle_bp_decode_batch.argtypes = [
+            ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+            ctypes.c_int, _u8p, _u8p, _i32p, _u8p, ctypes.c_int64, ctypes.c_int]
+        L.oracle_philox4x32_10.restype = None
+        L.oracle_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
+        L.oracle_uniform.restype = ctypes.c_double
+        L.oracle_uniform.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_mc_run.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+STREAM_DATA = 0x51D50001
+METHODS = {"product_sum": 0, "minimum_sum": 1}
+
+
+def _csr(H):
+    from qldpc_fault_tolerance_amd.codes import CSR
+
+    c = H if isinstance(H, CSR) else CSR.from_dense(H)
+    return c.m, c.n, np.ascontiguousarray(c.row_ptr, np.int32), np.ascontiguousarray(c.col_idx, np.int32)
+
+
+def bp_decode_batch(H, channel_probs, max_iter, bp_method="minimum_sum", ms_scaling_factor=0.625,
+                    synd=None, precision=64, nthreads=0):
+    m, n, rp, ci = _csr(H)
+    synd = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.uint8) & 1)
+    B = synd.shape[0]
+    assert synd.shape[1] == m
+    corr = np.zeros((B, n), np.uint8)
+    iters = np.zeros(B, np.int32)
+    conv = np.zeros(B, np.uint8)
+    probs = np.ascontiguousarray(np.broadcast_to(np.asarray(channel_probs, np.float64), (n,)))
+    rc = lib().oracle_bp_decode_batch(m, n, rp, ci, probs, int(max_iter), METHODS[bp_method],
+                                      float(ms_scaling_factor), int(precision), synd, corr, iters, conv,
+                                      B, int(nthreads))
+    if rc:
+        raise RuntimeError("oracle_bp_decode_batch failed")
+    return corr, iters, conv.astype(bool)
+
+
+def philox4x32_10(ctr, key):
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().oracle_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def uniform(seed, shot, qubit, stream=STREAM_DATA):
+    return lib().oracle_uniform(seed, shot, qubit, stream)
+
+
+def mc_run(code, px, py, pz, seed, shot_begin, shot_count, logical_mode="X", max_iter=None,
+           bp_method="minimum_sum", ms_scaling_factor=0.625, precision=64, probs_x=None, probs_z=None,
+           uniforms=None, per_shot=False, nthreads=0):
+    """Fused data-error shot loop on the CPU (oracle / CPU baseline)."""
+    n = code.N
+    hz, lz, hx, lx = code.csr("hz"), code.csr("lz"), code.csr("hx"), code.csr("lx")
+    if probs_x is None:
+        probs_x = (px + py)
+    if probs_z is None:
+        probs_z = (pz + py)
+    px_arr = np.ascontiguousarray(np.broadcast_to(np.asarray(probs_x, np.float64), (n,)))
+    pz_arr = np.ascontiguousarray(np.broadcast_to(np.asarray(probs_z, np.float64), (n,)))
+    if max_iter is None:
+        max_iter = int(n / 10)
+    mode = {"X": 0, "Z": 1, "Total": 2}[logical_mode]
+    S = int(shot_count)
+    fail = err = corr = iters = None
+    if per_shot:
+        fail = np.zeros(S, np.uint8)
+        err = np.zeros((S, n), np.uint8)
+        corr = np.zeros((S, 2, n), np.uint8)
+        iters = np.zeros((S, 2), np.int32)
+    if uniforms is not None:
+        uniforms = np.ascontiguousarray(uniforms, np.float64)
+        assert uniforms.shape == (S, n)
+    cnt = Counters()
+
+    def p(a, t):
+        return a.ctypes.data_as(ctypes.POINTER(t)) if a is not None else None
+
+    i32 = ctypes.c_int32
+    keep = [np.ascontiguousarray(a, np.int32) for a in
+            (hz.row_ptr, hz.col_idx, lz.row_ptr, lz.col_idx, hx.row_ptr, hx.col_idx, lx.row_ptr, lx.col_idx)]
+    L = lib()
+    rc = L.oracle_mc_run(
+        ctypes.c_int(n),
+        ctypes.c_int(hz.m), p(keep[0], i32), p(keep[1], i32),
+        ctypes.c_int(lz.m), p(keep[2], i32), p(keep[3], i32),
+        p(px_arr, ctypes.c_double),
+        ctypes.c_int(hx.m), p(keep[4], i32), p(keep[5], i32),
+        ctypes.c_int(lx.m), p(keep[6], i32), p(keep[7], i32),
+        p(pz_arr, ctypes.c_double),
+        ctypes.c_int(int(max_iter)), ctypes.c_int(int(max_iter)), ctypes.c_int(METHODS[bp_method]),
+        ctypes.c_double(ms_scaling_factor), ctypes.c_int(precision),
+        ctypes.c_double(px), ctypes.c_double(py), ctypes.c_double(pz), ctypes.c_uint64(seed),
+        ctypes.c_uint64(shot_begin), ctypes.c_int64(S), ctypes.c_int(mode),
+        p(uniforms, ctypes.c_double), ctypes.byref(cnt),
+        p(fail, ctypes.c_uint8), p(err, ctypes.c_uint8), p(corr, ctypes.c_uint8), p(iters, ctypes.c_int32),
+        ctypes.c_int(int(nthreads)))
+    del keep
+    if rc:
+        raise RuntimeError("oracle_mc_run failed")
+    out = cnt.as_dict()
+    if per_shot:
+        out.update(fail=fail, err=err, corr=corr, iters=iters)
+    return out

@@ -1,0 +1,422 @@
+/*
+ * qldpc_oracle.c — CPU restatement of the reference hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product package links, loads or
+ * calls this file: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg use it, as the checker / the CPU baseline.
+ *
+ * What it restates (file:line under /root/reference):
+ *  - BP decoding: the reference calls the third-party `ldpc` package
+ *    (`from ldpc import bp_decoder`, src/Decoders.py:47; constructed at
+ *    src/Decoders.py:52,80-84 and src/Decoders_SpaceTime.py:207-213).  `ldpc` is
+ *    not vendored and not installed; this is a restatement of the published
+ *    ldpc 0.1.x `bp_decoder` Cython (bp_decoder.pyx: `bp_decode_log_prob_ratios`
+ *    = "minimum_sum", `bp_decode_prob_ratios` = "product_sum") over Neal's
+ *    `mod2sparse` lists: rows visited in ascending column order, columns in
+ *    ascending row order, flooding schedule, stop when H·x == syndrome or at
+ *    max_iter.  Parity of this part is UNPINNED by the reference (it has no
+ *    tests or fixtures for BP); see DESIGN.md §Oracle.
+ *  - Error sampling / syndromes / failure check: CodeSimulator_DataError
+ *    (src/Simulators.py:89-168): per-qubit uniform u, 3-way split
+ *    Z if u<pz, X if pz<=u<pz+px, Y if pz+px<=u<pz+px+py; s = H e mod 2;
+ *    failure = any(H r) or any(L r) with r = e + decoding.
+ *  - Shot RNG: the reference uses Python's MT19937 (`random.random()`),
+ *    reseeded per forked worker and therefore not reproducible.  The engine's
+ *    fused path draws u from Philox4x32-10 keyed by (seed, shot, qubit) with
+ *    the same 53-bit construction as CPython's random.random()
+ *    ((a>>5)*2^26 + (b>>6)) / 2^53; the "external uniforms" entry points take u
+ *    from the caller (e.g. CPython's own random()) for bit-exact replays.
+ *
+ * T = double is the reference arithmetic; T = float is the engine's fast mode
+ * in the same operation order (so the fp32 GPU kernel is checked bit-exactly
+ * too).  Float mode replaces the 1e308 min-sum sentinel by FLT_MAX.
+ */
+#include <math.h>
+#include <float.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORACLE_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------ graph */
+typedef struct {
+    int m, n, E;
+    const int32_t *row_ptr, *col_idx; /* CSR, columns ascending in a row      */
+    int32_t *col_ptr, *col_edge;      /* CSC: edge ids (row-major), rows asc. */
+    int32_t *edge_row;                /* row of each edge                     */
+} graph_t;
+
+static int graph_init(graph_t *g, int m, int n, const int32_t *row_ptr, const int32_t *col_idx) {
+    g->m = m; g->n = n; g->E = row_ptr[m];
+    g->row_ptr = row_ptr; g->col_idx = col_idx;
+    g->col_ptr = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+    g->col_edge = (int32_t *)malloc(sizeof(int32_t) * (size_t)(g->E ? g->E : 1));
+    g->edge_row = (int32_t *)malloc(sizeof(int32_t) * (size_t)(g->E ? g->E : 1));
+    if (!g->col_ptr || !g->col_edge || !g->edge_row) return -1;
+    for (int e = 0; e < g->E; e++) g->col_ptr[col_idx[e] + 1]++;
+    for (int j = 0; j < n; j++) g->col_ptr[j + 1] += g->col_ptr[j];
+    int32_t *fill = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n ? n : 1));
+    memcpy(fill, g->col_ptr, sizeof(int32_t) * (size_t)n);
+    for (int i = 0; i < m; i++)
+        for (int e = row_ptr[i]; e < row_ptr[i + 1]; e++) {
+            g->edge_row[e] = i;
+            g->col_edge[fill[col_idx[e]]++] = e; /* rows visited ascending */
+        }
+    free(fill);
+    return 0;
+}
+
+static void graph_free(graph_t *g) {
+    free(g->col_ptr); free(g->col_edge); free(g->edge_row);
+}
+
+/* ------------------------------------------------------------- BP decoders */
+typedef struct {
+    int max_iter;
+    int method;     /* 0 = product_sum, 1 = minimum_sum */
+    double alpha;   /* ms_scaling_factor; 0 => 1 - 2^-iter   */
+} bp_params_t;
+
+#define DEFINE_BP(T, SUFFIX, SENTINEL)                                                          \
+typedef struct {                                                                                \
+    T *b2c, *c2b; int *sgn; T *prior; T *ratio; uint8_t *dec, *dsyn;                          \
+} ws_##SUFFIX;                                                                                  \
+                                                                                                \
+static int ws_alloc_##SUFFIX(ws_##SUFFIX *w, const graph_t *g) {                                \
+    size_t E = g->E ? g->E : 1;                                                                 \
+    w->b2c = (T *)malloc(sizeof(T) * E); w->c2b = (T *)malloc(sizeof(T) * E);                  \
+    w->sgn = (int *)malloc(sizeof(int) * E);                                                    \
+    w->prior = (T *)malloc(sizeof(T) * (size_t)(g->n + 1));                                     \
+    w->ratio = (T *)malloc(sizeof(T) * (size_t)(g->n + 1));                                     \
+    w->dec = (uint8_t *)malloc((size_t)g->n + 1); w->dsyn = (uint8_t *)malloc((size_t)g->m + 1);\
+    return (w->b2c && w->c2b && w->sgn && w->prior && w->ratio && w->dec && w->dsyn) ? 0 : -1;\
+}                                                                                               \
+static void ws_free_##SUFFIX(ws_##SUFFIX *w) {                                                  \
+    free(w->b2c); free(w->c2b); free(w->sgn); free(w->prior); free(w->ratio);                  \
+    free(w->dec); free(w->dsyn);                                                                \
+}                                                                                               \
+/* channel priors, computed in double with libm like the Cython code */                         \
+static void ws_priors_##SUFFIX(ws_##SUFFIX *w, const graph_t *g, const double *p) {             \
+    for (int j = 0; j < g->n; j++) {                                                            \
+        w->prior[j] = (T)log((1.0 - p[j]) / p[j]);                                              \
+        w->ratio[j] = (T)(p[j] / (1.0 - p[j]));                                                 \
+    }                                                                                           \
+}                                                                                               \
+/* H x == synd ?  (mod2sparse_mulvec + compare) */                                             \
+static int synd_equal_##SUFFIX(const graph_t *g, const uint8_t *x, const uint8_t *s, uint8_t *d) {\
+    for (int i = 0; i < g->m; i++) {                                                            \
+        uint8_t a = 0;                                                                          \
+        for (int e = g->row_ptr[i]; e < g->row_ptr[i + 1]; e++) a ^= x[g->col_idx[e]];         \
+        d[i] = a;                                                                               \
+    }                                                                                           \
+    for (int i = 0; i < g->m; i++) if (d[i] != (s[i] & 1)) return 0;                            \
+    return 1;                                                                                   \
+}                                                                                               \
+/* ldpc bp_decode_log_prob_ratios (minimum_sum) */                                              \
+static int bp_ms_##SUFFIX(const graph_t *g, const bp_params_t *P, ws_##SUFFIX *w,              \
+                          const uint8_t *synd, int *iters_out) {                               \
+    const int m = g->m, n = g->n;                                                               \
+    for (int j = 0; j < n; j++)                                                                 \
+        for (int k = g->col_ptr[j]; k < g->col_ptr[j + 1]; k++) w->b2c[g->col_edge[k]] = w->prior[j];\
+    int it;                                                                                     \
+    for (it = 1; it <= P->max_iter; it++) {                                                     \
+        T alpha = (P->alpha == 0.0) ? (T)(1.0 - ldexp(1.0, -it)) : (T)P->alpha;                \
+        for (int i = 0; i < m; i++) {                                                           \
+            const int e0 = g->row_ptr[i], e1 = g->row_ptr[i + 1];                               \
+            T temp = (T)(SENTINEL);                                                             \
+            int sgn = (synd[i] & 1) ? 1 : 0;                                                    \
+            for (int e = e0; e < e1; e++) {                                                     \
+                w->c2b[e] = temp; w->sgn[e] = sgn;                                              \
+                T a = fabs(w->b2c[e]);                                                          \
+                if (a < temp) temp = a;                                                         \
+                if (w->b2c[e] <= 0) sgn += 1;                                                   \
+            }                                                                                   \
+            temp = (T)(SENTINEL); sgn = 0;                                                      \
+            for (int e = e1 - 1; e >= e0; e--) {                                                \
+                if (temp < w->c2b[e]) w->c2b[e] = temp;                                         \
+                w->sgn[e] += sgn;                                                               \
+                w->c2b[e] *= ((w->sgn[e] & 1) ? -alpha : alpha);                                \
+                T a = fabs(w->b2c[e]);                                                          \
+                if (a < temp) temp = a;                                                         \
+                if (w->b2c[e] <= 0) sgn += 1;                                                   \
+            }                                                                                   \
+        }                                                                                       \
+        for (int j = 0; j < n; j++) {                                                           \
+            const int k0 = g->col_ptr[j], k1 = g->col_ptr[j + 1];                               \
+            T temp = w->prior[j];                                                               \
+            for (int k = k0; k < k1; k++) {                                                     \
+                int e = g->col_edge[k];                                                         \
+                w->b2c[e] = temp; temp += w->c2b[e];                                            \
+            }                                                                                   \
+            w->dec[j] = (temp <= 0) ? 1 : 0;                                                    \
+            temp = (T)0;                                                                        \
+            for (int k = k1 - 1; k >= k0; k--) {                                                \
+                int e = g->col_edge[k];                                                         \
+                w->b2c[e] += temp; temp += w->c2b[e];                                           \
+            }                                                                                   \
+        }                                                                                       \
+        if (synd_equal_##SUFFIX(g, w->dec, synd, w->dsyn)) { *iters_out = it; return 1; }       \
+    }                                                                                           \
+    *iters_out = P->max_iter;                                                                   \
+    return 0;                                                                                   \
+}                                                                                               \
+/* ldpc bp_decode_prob_ratios (product_sum) */                                                  \
+static int bp_ps_##SUFFIX(const graph_t *g, const bp_params_t *P, ws_##SUFFIX *w,              \
+                          const uint8_t *synd, int *iters_out) {                               \
+    const int m = g->m, n = g->n;                                                               \
+    for (int j = 0; j < n; j++)                                                                 \
+        for (int k = g->col_ptr[j]; k < g->col_ptr[j + 1]; k++) w->b2c[g->col_edge[k]] = w->ratio[j];\
+    int it;                                                                                     \
+    for (it = 1; it <= P->max_iter; it++) {                                                     \
+        for (int i = 0; i < m; i++) {                                                           \
+            const int e0 = g->row_ptr[i], e1 = g->row_ptr[i + 1];                               \
+            T temp = (synd[i] & 1) ? (T)-1 : (T)1;                                              \
+            for (int e = e0; e < e1; e++) {                                                     \
+                w->c2b[e] = temp;                                                               \
+                temp *= (T)2 / ((T)1 + w->b2c[e]) - (T)1;                                       \
+            }                                                                                   \
+            temp = (T)1;                                                                        \
+            for (int e = e1 - 1; e >= e0; e--) {                                                \
+                w->c2b[e] *= temp;                                                              \
+                w->c2b[e] = ((T)1 - w->c2b[e]) / ((T)1 + w->c2b[e]);                            \
+                temp *= (T)2 / ((T)1 + w->b2c[e]) - (T)1;                                       \
+            }                                                                                   \
+        }                                                                                       \
+        for (int j = 0; j < n; j++) {                                                           \
+            const int k0 = g->col_ptr[j], k1 = g->col_ptr[j + 1];                               \
+            T temp = w->ratio[j];                                                               \
+            for (int k = k0; k < k1; k++) {                                                     \
+                int e = g->col_edge[k];                                                         \
+                w->b2c[e] = temp; temp *= w->c2b[e];                                            \
+                if (isnan(temp)) temp = (T)1;                                                   \
+            }                                                                                   \
+            w->dec[j] = (temp >= (T)1) ? 1 : 0;                                                 \
+            temp = (T)1;                                                                        \
+            for (int k = k1 - 1; k >= k0; k--) {                                                \
+                int e = g->col_edge[k];                                                         \
+                w->b2c[e] *= temp; temp *= w->c2b[e];                                           \
+                if (isnan(temp)) temp = (T)1;                                                   \
+            }                                                                                   \
+        }                                                                                       \
+        if (synd_equal_##SUFFIX(g, w->dec, synd, w->dsyn)) { *iters_out = it; return 1; }       \
+    }                                                                                           \
+    *iters_out = P->max_iter;                                                                   \
+    return 0;                                                                                   \
+}                                                                                               \
+static int bp_run_##SUFFIX(const graph_t *g, const bp_params_t *P, ws_##SUFFIX *w,             \
+                           const uint8_t *synd, int *iters) {                                   \
+    return P->method == 0 ? bp_ps_##SUFFIX(g, P, w, synd, iters) : bp_ms_##SUFFIX(g, P, w, synd, iters);\
+}
+
+DEFINE_BP(double, f64, 1e308)
+DEFINE_BP(float, f32, FLT_MAX)
+
+static int norm_max_iter(int max_iter, int n) { return max_iter > 0 ? max_iter : n; }
+
+/*
+ * Batch decode of external syndromes (the `bp_decoder.decode(synd)` contract,
+ * src/Decoders.py:88-90).  synd: [B][m] 0/1 bytes; corr: [B][n] 0/1 bytes.
+ * precision: 64 or 32.  Returns 0 on success.
+ */
+ORACLE_API int oracle_bp_decode_batch(int m, int n, const int32_t *row_ptr, const int32_t *col_idx,
+                                      const double *channel_probs, int max_iter, int method, double alpha,
+                                      int precision, const uint8_t *synd, uint8_t *corr, int32_t *iters,
+                                      uint8_t *conv, int64_t B, int nthreads) {
+    graph_t g;
+    if (graph_init(&g, m, n, row_ptr, col_idx)) return -1;
+    bp_params_t P = {norm_max_iter(max_iter, n), method, alpha};
+    int rc = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads) reduction(| : rc)
+#endif
+    {
+        int tid = 0, nth = 1;
+#ifdef _OPENMP
+        tid = omp_get_thread_num(); nth = omp_get_num_threads();
+#endif
+        if (precision == 32) {
+            ws_f32 w; if (ws_alloc_f32(&w, &g)) rc |= 1; else {
+                ws_priors_f32(&w, &g, channel_probs);
+                for (int64_t b = tid; b < B; b += nth) {
+                    int it; int c = bp_run_f32(&g, &P, &w, synd + b * m, &it);
+                    memcpy(corr + b * n, w.dec, (size_t)n);
+                    if (iters) iters[b] = it;
+                    if (conv) conv[b] = (uint8_t)c;
+                }
+                ws_free_f32(&w);
+            }
+        } else {
+            ws_f64 w; if (ws_alloc_f64(&w, &g)) rc |= 1; else {
+                ws_priors_f64(&w, &g, channel_probs);
+                for (int64_t b = tid; b < B; b += nth) {
+                    int it; int c = bp_run_f64(&g, &P, &w, synd + b * m, &it);
+                    memcpy(corr + b * n, w.dec, (size_t)n);
+                    if (iters) iters[b] = it;
+                    if (conv) conv[b] = (uint8_t)c;
+                }
+                ws_free_f64(&w);
+            }
+        }
+    }
+    graph_free(&g);
+    return rc ? -1 : 0;
+}
+
+/* ------------------------------------------------------------- Philox4x32 */
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+ORACLE_API void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)PHILOX_M0 * c0, p1 = (uint64_t)PHILOX_M1 * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += PHILOX_W0; k1 += PHILOX_W1;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Domain tag in counter word 3 for the data-error stream. */
+#define QLDPC_STREAM_DATA 0x51D50001u
+
+/* u for (seed, shot, qubit, stream): CPython random() 53-bit construction */
+ORACLE_API double oracle_uniform(uint64_t seed, uint64_t shot, uint32_t qubit, uint32_t stream) {
+    uint32_t ctr[4] = {qubit, (uint32_t)shot, (uint32_t)(shot >> 32), stream};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t o[4];
+    oracle_philox4x32_10(ctr, key, o);
+    return ((double)(o[0] >> 5) * 67108864.0 + (double)(o[1] >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+/* src/Simulators.py:99-113 three-way split; returns bit0 = x, bit1 = z */
+static inline int classify(double u, double t1, double t2, double t3) {
+    if (u < t1) return 2;                 /* Z */
+    if (t1 <= u && u < t2) return 1;      /* X */
+    if (t2 <= u && u < t3) return 3;      /* Y */
+    return 0;
+}
+
+/* ------------------------------------------------------------ MC shot loop */
+typedef struct {
+    int64_t shots, failures;
+    int64_t sector_decodes[2], sector_iters[2], sector_nonconv[2], sector_fail[2];
+} oracle_counters_t;
+
+/*
+ * Fused data-error shot loop (CodeSimulator_DataError._single_run,
+ * src/Simulators.py:117-168).  Sector 0 = X errors decoded on hz (logical lz),
+ * sector 1 = Z errors decoded on hx (logical lx).  logical_mode: 0 = 'X',
+ * 1 = 'Z', 2 = 'Total'; sectors not needed by the mode are skipped (their
+ * outcome cannot change the returned failure).  uniforms: NULL => Philox
+ * stream, else [shot_count][n] doubles.  per-shot outputs optional.
+ */
+ORACLE_API int oracle_mc_run(int n,
+                             int mx, const int32_t *hz_row_ptr, const int32_t *hz_col_idx,
+                             int kx, const int32_t *lz_row_ptr, const int32_t *lz_col_idx,
+                             const double *probs_x,
+                             int mz, const int32_t *hx_row_ptr, const int32_t *hx_col_idx,
+                             int kz, const int32_t *lx_row_ptr, const int32_t *lx_col_idx,
+                             const double *probs_z,
+                             int max_iter_x, int max_iter_z, int method, double alpha, int precision,
+                             double px, double py, double pz, uint64_t seed, uint64_t shot_begin,
+                             int64_t shot_count, int logical_mode, const double *uniforms,
+                             oracle_counters_t *out, uint8_t *fail_out, uint8_t *err_out /*[S][n] bit0 x bit1 z*/,
+                             uint8_t *corr_out /*[S][2][n]*/, int32_t *iters_out /*[S][2]*/,
+                             int nthreads) {
+    graph_t G[2];
+    if (graph_init(&G[0], mx, n, hz_row_ptr, hz_col_idx)) return -1;
+    if (graph_init(&G[1], mz, n, hx_row_ptr, hx_col_idx)) return -1;
+    const int32_t *lrp[2] = {lz_row_ptr, lx_row_ptr}, *lci[2] = {lz_col_idx, lx_col_idx};
+    const int kk[2] = {kx, kz};
+    const double *pr[2] = {probs_x, probs_z};
+    bp_params_t P[2] = {{norm_max_iter(max_iter_x, n), method, alpha}, {norm_max_iter(max_iter_z, n), method, alpha}};
+    const int need[2] = {logical_mode != 1, logical_mode != 0};
+    const double t1 = pz, t2 = pz + px, t3 = (pz + px) + py;
+    oracle_counters_t tot;
+    memset(&tot, 0, sizeof(tot));
+    int rc = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads) reduction(| : rc)
+#endif
+    {
+        int tid = 0, nth = 1;
+#ifdef _OPENMP
+        tid = omp_get_thread_num(); nth = omp_get_num_threads();
+#endif
+        oracle_counters_t loc; memset(&loc, 0, sizeof(loc));
+        ws_f64 w64[2]; ws_f32 w32[2];
+        uint8_t *e = (uint8_t *)malloc((size_t)n), *s = (uint8_t *)malloc((size_t)(mx > mz ? mx : mz) + 1);
+        uint8_t *r = (uint8_t *)malloc((size_t)n);
+        for (int q = 0; q < 2; q++) {
+            if (precision == 32) { if (ws_alloc_f32(&w32[q], &G[q])) rc |= 1; else ws_priors_f32(&w32[q], &G[q], pr[q]); }
+            else { if (ws_alloc_f64(&w64[q], &G[q])) rc |= 1; else ws_priors_f64(&w64[q], &G[q], pr[q]); }
+        }
+        /* static contiguous partition of the shot range */
+        int64_t lo = shot_count * tid / nth, hi = shot_count * (tid + 1) / nth;
+        for (int64_t b = lo; b < hi && !rc; b++) {
+            uint64_t shot = shot_begin + (uint64_t)b;
+            uint8_t cls[1]; (void)cls;
+            int fail_sec[2] = {0, 0};
+            for (int q = 0; q < 2; q++) {
+                if (!need[q]) continue;
+                for (int j = 0; j < n; j++) {
+                    double u = uniforms ? uniforms[b * n + j] : oracle_uniform(seed, shot, (uint32_t)j, QLDPC_STREAM_DATA);
+                    int c = classify(u, t1, t2, t3);
+                    e[j] = (uint8_t)((q == 0) ? (c & 1) : (c >> 1));
+                    if (err_out) err_out[b * n + j] = (uint8_t)c;
+                }
+                const graph_t *g = &G[q];
+                for (int i = 0; i < g->m; i++) {
+                    uint8_t a = 0;
+                    for (int k = g->row_ptr[i]; k < g->row_ptr[i + 1]; k++) a ^= e[g->col_idx[k]];
+                    s[i] = a;
+                }
+                int it, conv;
+                const uint8_t *dec;
+                if (precision == 32) { conv = bp_run_f32(g, &P[q], &w32[q], s, &it); dec = w32[q].dec; }
+                else { conv = bp_run_f64(g, &P[q], &w64[q], s, &it); dec = w64[q].dec; }
+                for (int j = 0; j < n; j++) r[j] = e[j] ^ dec[j];
+                int lf = 0;
+                for (int l = 0; l < kk[q] && !lf; l++) {
+                    uint8_t a = 0;
+                    for (int k = lrp[q][l]; k < lrp[q][l + 1]; k++) a ^= r[lci[q][k]];
+                    lf = a;
+                }
+                fail_sec[q] = (!conv) || lf;
+                loc.sector_decodes[q]++; loc.sector_iters[q] += it; loc.sector_nonconv[q] += !conv;
+                loc.sector_fail[q] += fail_sec[q];
+                if (corr_out) memcpy(corr_out + (b * 2 + q) * n, dec, (size_t)n);
+                if (iters_out) iters_out[b * 2 + q] = it;
+            }
+            int f = logical_mode == 0 ? fail_sec[0] : logical_mode == 1 ? fail_sec[1] : (fail_sec[0] || fail_sec[1]);
+            loc.shots++; loc.failures += f;
+            if (fail_out) fail_out[b] = (uint8_t)(fail_sec[0] | (fail_sec[1] << 1));
+        }
+        for (int q = 0; q < 2; q++) { if (precision == 32) ws_free_f32(&w32[q]); else ws_free_f64(&w64[q]); }
+        free(e); free(s); free(r);
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        {
+            tot.shots += loc.shots; tot.failures += loc.failures;
+            for (int q = 0; q < 2; q++) {
+                tot.sector_decodes[q] += loc.sector_decodes[q]; tot.sector_iters[q] += loc.sector_iters[q];
+                tot.sector_nonconv[q] += loc.sector_nonconv[q]; tot.sector_fail[q] += loc.sector_fail[q];
+            }
+        }
+    }
+    graph_free(&G[0]); graph_free(&G[1]);
+    if (out) *out = tot;
+    return rc ? -1 : 0;
+}

@@ -1,0 +1,129 @@
+"""ctypes binding of ``libqldpc_hip.so`` (C ABI in ``include/qldpc_hip.h``).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU
+is visible, every entry point raises :class:`NativeUnavailable` naming the
+cause.  Build the library in-tree with ``python -c "import __graft_entry__ as g;
+g.build()"`` (or :func:`qldpc_fault_tolerance_amd.build.build_native`).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libqldpc_hip.so")
+HIST_BINS = 1025
+
+# Every symbol include/qldpc_hip.h declares (tests check the .so exports them).
+EXPORTED = [
+    "qldpc_abi_version", "qldpc_last_error", "qldpc_device_count", "qldpc_graph_create", "qldpc_graph_destroy",
+    "qldpc_graph_info", "qldpc_bp_create", "qldpc_bp_destroy", "qldpc_bp_set_channel_probs",
+    "qldpc_bp_decode_batch", "qldpc_mc_create", "qldpc_mc_destroy", "qldpc_mc_launch", "qldpc_mc_run",
+    "qldpc_bp_geometry",
+]
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class QldpcError(RuntimeError):
+    pass
+
+
+class Counters(ctypes.Structure):
+    """Mirror of ``qldpc_counters``."""
+
+    _fields_ = [
+        ("shots", ctypes.c_int64),
+        ("failures", ctypes.c_int64),
+        ("sector_decodes", ctypes.c_int64 * 2),
+        ("sector_iters", ctypes.c_int64 * 2),
+        ("sector_nonconv", ctypes.c_int64 * 2),
+        ("sector_fail", ctypes.c_int64 * 2),
+        ("iter_hist", (ctypes.c_int64 * HIST_BINS) * 2),
+    ]
+
+
+COUNTER_WORDS = ctypes.sizeof(Counters) // 8
+
+_lib = None
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_u64 = ctypes.c_uint64
+_dbl = ctypes.c_double
+_pp = ctypes.POINTER(ctypes.c_void_p)
+
+
+def _declare(L):
+    L.qldpc_abi_version.restype = ctypes.c_int
+    L.qldpc_abi_version.argtypes = []
+    L.qldpc_last_error.restype = ctypes.c_char_p
+    L.qldpc_last_error.argtypes = []
+    L.qldpc_device_count.restype = ctypes.c_int
+    L.qldpc_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    L.qldpc_graph_create.restype = ctypes.c_int
+    L.qldpc_graph_create.argtypes = [ctypes.c_int, _i32, _i32, _vp, _vp, _pp]
+    L.qldpc_graph_destroy.restype = ctypes.c_int
+    L.qldpc_graph_destroy.argtypes = [_vp]
+    L.qldpc_graph_info.restype = ctypes.c_int
+    L.qldpc_graph_info.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 5
+    L.qldpc_bp_create.restype = ctypes.c_int
+    L.qldpc_bp_create.argtypes = [_vp, _vp, _i32, _i32, _dbl, _i32, _i32, _i32, _pp]
+    L.qldpc_bp_destroy.restype = ctypes.c_int
+    L.qldpc_bp_destroy.argtypes = [_vp]
+    L.qldpc_bp_set_channel_probs.restype = ctypes.c_int
+    L.qldpc_bp_set_channel_probs.argtypes = [_vp, _vp]
+    L.qldpc_bp_decode_batch.restype = ctypes.c_int
+    L.qldpc_bp_decode_batch.argtypes = [_vp, _vp, _vp, _vp, _vp, _i64, _vp]
+    L.qldpc_mc_create.restype = ctypes.c_int
+    L.qldpc_mc_create.argtypes = [_vp, _vp, _vp, _vp, _pp]
+    L.qldpc_mc_destroy.restype = ctypes.c_int
+    L.qldpc_mc_destroy.argtypes = [_vp]
+    L.qldpc_mc_launch.restype = ctypes.c_int
+    L.qldpc_mc_launch.argtypes = [_vp, _dbl, _dbl, _dbl, _u64, _u64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _i32, _vp]
+    L.qldpc_mc_run.restype = ctypes.c_int
+    L.qldpc_mc_run.argtypes = [_vp, _dbl, _dbl, _dbl, _u64, _u64, _i64, _i32, ctypes.POINTER(Counters), _vp]
+    L.qldpc_bp_geometry.restype = ctypes.c_int
+    L.qldpc_bp_geometry.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 4
+
+
+def lib():
+    """The loaded HIP library (raises NativeUnavailable if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable(
+                f"{LIB_PATH} not found: build the HIP extension first (__graft_entry__.build()); "
+                "the engine has no CPU fallback")
+        # One HIP runtime per process: load PyTorch's libamdhip64 first so this
+        # library binds to it (same SONAME) and shares its device context,
+        # allocations and streams instead of initialising a second runtime.
+        import torch  # noqa: F401
+
+        L = ctypes.CDLL(LIB_PATH)
+        _declare(L)
+        if L.qldpc_abi_version() != 1:
+            raise NativeUnavailable("libqldpc_hip.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().qldpc_last_error().decode(errors="replace")
+        raise QldpcError(f"{what} failed (rc={rc}): {msg}")
+
+
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    rc = lib().qldpc_device_count(ctypes.byref(c))
+    return c.value if rc == 0 else 0
+
+
+def require_gpu() -> None:
+    if device_count() <= 0:
+        raise NativeUnavailable("no HIP device visible: the MI355X engine needs a GPU (no CPU fallback)")

@@ -1,0 +1,498 @@
+// qldpc_hip.hip — host runtime + C ABI (include/qldpc_hip.h) of the MI355X engine.
+//
+// Graph/decoder/MC handles own their device buffers; launches take a caller
+// stream.  Kernel variants (fp32/fp64 × variables-per-thread × max column
+// degree) are instantiated here and selected per graph at create time.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/qldpc_hip.h"
+#include "variants.h"
+
+using namespace qldpc;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define QLDPC_HIP(x)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess) return set_err(QLDPC_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int alloc(size_t b) {
+    bytes = b;
+    if (b == 0) return 0;
+    if (hipMalloc(&p, b) != hipSuccess) {
+      p = nullptr;
+      return set_err(QLDPC_ENOMEM, "hipMalloc failed");
+    }
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+  }
+};
+
+constexpr int kVplMax = 12;
+const int kVplSet[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12};
+
+}  // namespace
+
+struct qldpc_graph {
+  int device = 0;
+  int m = 0, n = 0, nnz = 0, max_row = 0, max_col = 0;
+  std::vector<int32_t> row_ptr, col_idx;
+  std::vector<std::vector<int32_t>> col_rows;  // rows of each column, ascending
+};
+
+struct qldpc_bp {
+  qldpc_graph* g = nullptr;
+  int max_iter = 0, method = 1, precision = 64;
+  double alpha = 0.625;
+  int TB = 64, VPL = 1, DMAX = 4;
+  int lds_bytes = 0, blocks_per_cu = 0, cus = 0;
+  std::vector<double> probs;
+  DevBuf vchk, llr;
+};
+
+struct qldpc_mc {
+  qldpc_bp* dec[2] = {nullptr, nullptr};
+  int kw[2] = {0, 0};
+  DevBuf lmask[2];
+  DevBuf counters;
+  int TB = 0, VPL = 0, DMAX = 0, precision = 64, lds_bytes = 0, blocks_per_cu = 0, cus = 0;
+};
+
+// --------------------------------------------------------------- dispatch
+namespace {
+
+Variant get_variant(int precision, int vpl, int dmax) {
+  if (precision == 32) return dmax == 4 ? get_variant_f32_d4(vpl) : get_variant_f32_d8(vpl);
+  return dmax == 4 ? get_variant_f64_d4(vpl) : get_variant_f64_d8(vpl);
+}
+
+int round_up(int x, int a) { return (x + a - 1) / a * a; }
+
+// Choose threads-per-shot TB (multiple of 64, <= 512) and variables per thread.
+// Largest vars-per-thread whose kernels compile without register spills (gfx950,
+// -Rpass-analysis=kernel-resource-usage).
+int max_spill_free_vpl(int precision, int dmax) {
+  if (precision == 32) return dmax == 4 ? 10 : 5;
+  return dmax == 4 ? 6 : 3;
+}
+
+int choose_geometry(int n, int m, int requested_vpl, int vmax, int& TB, int& VPL) {
+  if (requested_vpl > 0) {
+    bool ok = false;
+    for (int v : kVplSet) ok |= (v == requested_vpl);
+    if (!ok) return set_err(QLDPC_EINVAL, "vars_per_thread must be one of 1-8,10,12");
+    VPL = requested_vpl;
+    TB = round_up((n + VPL - 1) / VPL, 64);
+    if (TB > kMaxThreads) return set_err(QLDPC_EINVAL, "vars_per_thread too small for this graph (>512 threads)");
+  } else {
+    // smallest padding waste with the per-thread work >= 4 variables when possible
+    double best = 1e30;
+    for (int v : kVplSet) {
+      const int tb = round_up((n + v - 1) / v, 64);
+      if (tb > kMaxThreads || v > vmax) continue;
+      const double waste = (double)(tb * v - n) / (double)(tb * v);
+      const double score = waste + (v < 4 ? 0.25 : 0.0) + 0.01 * v;
+      if (score < best) {
+        best = score;
+        TB = tb;
+        VPL = v;
+      }
+    }
+    if (best >= 1e30) return set_err(QLDPC_ENOTSUP, "graph too large for the register-resident kernel");
+  }
+  if ((m + TB - 1) / TB > 32) return set_err(QLDPC_ENOTSUP, "too many checks per thread (m > 32*threads)");
+  return 0;
+}
+
+size_t lds_for(int precision, int mmax) {
+  const size_t pair = precision == 32 ? 8 : 16;
+  return pair * 2 * (size_t)mmax + 4 * 2 * (size_t)mmax + 64;
+}
+
+int device_cus(int dev, int& cus) {
+  hipDeviceProp_t prop;
+  QLDPC_HIP(hipGetDeviceProperties(&prop, dev));
+  cus = prop.multiProcessorCount;
+  return 0;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+int qldpc_abi_version(void) { return QLDPC_ABI_VERSION; }
+
+const char* qldpc_last_error(void) { return g_err.c_str(); }
+
+int qldpc_device_count(int* out) {
+  if (!out) return set_err(QLDPC_EINVAL, "out is NULL");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *out = 0;
+    return set_err(QLDPC_EHIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return 0;
+}
+
+int qldpc_graph_create(int device, int32_t m, int32_t n, const int32_t* row_ptr, const int32_t* col_idx,
+                       qldpc_graph** out) {
+  if (!out || !row_ptr || (m > 0 && !col_idx)) return set_err(QLDPC_EINVAL, "NULL argument");
+  if (m < 0 || n <= 0) return set_err(QLDPC_EINVAL, "bad shape");
+  if (m >= 0xFFFF) return set_err(QLDPC_ENOTSUP, "more than 65534 checks");
+  if (row_ptr[0] != 0) return set_err(QLDPC_EINVAL, "row_ptr[0] != 0");
+  auto* g = new qldpc_graph();
+  g->device = device;
+  g->m = m;
+  g->n = n;
+  g->nnz = row_ptr[m];
+  g->row_ptr.assign(row_ptr, row_ptr + m + 1);
+  g->col_idx.assign(col_idx, col_idx + g->nnz);
+  g->col_rows.assign(n, {});
+  for (int i = 0; i < m; ++i) {
+    if (row_ptr[i + 1] < row_ptr[i]) {
+      delete g;
+      return set_err(QLDPC_EINVAL, "row_ptr not monotone");
+    }
+    g->max_row = std::max(g->max_row, row_ptr[i + 1] - row_ptr[i]);
+    for (int e = row_ptr[i]; e < row_ptr[i + 1]; ++e) {
+      const int c = col_idx[e];
+      if (c < 0 || c >= n || (e > row_ptr[i] && col_idx[e - 1] >= c)) {
+        delete g;
+        return set_err(QLDPC_EINVAL, "col_idx out of range or not strictly ascending within a row");
+      }
+      g->col_rows[c].push_back(i);
+    }
+  }
+  for (int j = 0; j < n; ++j) g->max_col = std::max<int>(g->max_col, (int)g->col_rows[j].size());
+  *out = g;
+  return 0;
+}
+
+int qldpc_graph_destroy(qldpc_graph* g) {
+  delete g;
+  return 0;
+}
+
+int qldpc_graph_info(const qldpc_graph* g, int32_t* m, int32_t* n, int32_t* nnz, int32_t* max_row_deg,
+                     int32_t* max_col_deg) {
+  if (!g) return set_err(QLDPC_EINVAL, "NULL graph");
+  if (m) *m = g->m;
+  if (n) *n = g->n;
+  if (nnz) *nnz = g->nnz;
+  if (max_row_deg) *max_row_deg = g->max_row;
+  if (max_col_deg) *max_col_deg = g->max_col;
+  return 0;
+}
+
+static int upload_llr(qldpc_bp* bp) {
+  const int TB = bp->TB, VPL = bp->VPL, n = bp->g->n;
+  const size_t cnt = (size_t)VPL * TB;
+  std::vector<double> l64(cnt, 1.0);
+  for (int k = 0; k < VPL; ++k)
+    for (int t = 0; t < TB; ++t) {
+      const int j = k * TB + t;
+      if (j < n) l64[(size_t)k * TB + t] = std::log((1.0 - bp->probs[j]) / bp->probs[j]);  // glibc log, as Cython
+    }
+  if (bp->precision == 32) {
+    std::vector<float> l32(cnt);
+    for (size_t i = 0; i < cnt; ++i) l32[i] = (float)l64[i];
+    QLDPC_HIP(hipMemcpy(bp->llr.p, l32.data(), cnt * sizeof(float), hipMemcpyHostToDevice));
+  } else {
+    QLDPC_HIP(hipMemcpy(bp->llr.p, l64.data(), cnt * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_iter, int32_t bp_method,
+                    double ms_scaling_factor, int32_t precision, int32_t vars_per_thread, int32_t min_col_slots,
+                    qldpc_bp** out) {
+  if (!g || !channel_probs || !out) return set_err(QLDPC_EINVAL, "NULL argument");
+  if (precision != 32 && precision != 64) return set_err(QLDPC_EINVAL, "precision must be 32 or 64");
+  if (bp_method != QLDPC_MIN_SUM) return set_err(QLDPC_ENOTSUP, "GPU engine implements minimum_sum only");
+  if (g->max_col > 8 || min_col_slots > 8) return set_err(QLDPC_ENOTSUP, "column degree > 8");
+  QLDPC_HIP(hipSetDevice(g->device));
+  auto* bp = new qldpc_bp();
+  bp->g = g;
+  bp->max_iter = max_iter > 0 ? max_iter : g->n;
+  bp->method = bp_method;
+  bp->alpha = ms_scaling_factor;
+  bp->precision = precision;
+  bp->DMAX = std::max(g->max_col, (int)min_col_slots) <= 4 ? 4 : 8;
+  bp->probs.assign(channel_probs, channel_probs + g->n);
+  int rc = choose_geometry(g->n, g->m, vars_per_thread, max_spill_free_vpl(precision, bp->DMAX), bp->TB, bp->VPL);
+  if (rc) {
+    delete bp;
+    return rc;
+  }
+  const int TB = bp->TB, VPL = bp->VPL, D2 = bp->DMAX / 2;
+  std::vector<uint32_t> vchk((size_t)VPL * D2 * TB, 0xFFFFFFFFu);
+  for (int k = 0; k < VPL; ++k)
+    for (int t = 0; t < TB; ++t) {
+      const int j = k * TB + t;
+      if (j >= g->n) continue;
+      const auto& rows = g->col_rows[j];
+      for (int d = 0; d < bp->DMAX; ++d) {
+        const uint32_t v = d < (int)rows.size() ? (uint32_t)rows[d] : 0xFFFFu;
+        uint32_t& w = vchk[((size_t)k * D2 + d / 2) * TB + t];
+        w = (d & 1) ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
+      }
+    }
+  if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)VPL * TB * (precision == 32 ? 4 : 8)))) {
+    delete bp;
+    return rc;
+  }
+  if (hipMemcpy(bp->vchk.p, vchk.data(), vchk.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    delete bp;
+    return set_err(QLDPC_EHIP, "upload vchk");
+  }
+  if ((rc = upload_llr(bp))) {
+    delete bp;
+    return rc;
+  }
+  bp->lds_bytes = (int)lds_for(precision, g->m);
+  Variant v = get_variant(precision, VPL, bp->DMAX);
+  if (!v.dec) {
+    delete bp;
+    return set_err(QLDPC_ENOTSUP, "no kernel variant");
+  }
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, v.dec_k, TB, bp->lds_bytes) != hipSuccess) nb = 1;
+  bp->blocks_per_cu = std::max(1, nb);
+  if ((rc = device_cus(g->device, bp->cus))) {
+    delete bp;
+    return rc;
+  }
+  *out = bp;
+  return 0;
+}
+
+int qldpc_bp_destroy(qldpc_bp* bp) {
+  if (!bp) return 0;
+  bp->vchk.release();
+  bp->llr.release();
+  delete bp;
+  return 0;
+}
+
+int qldpc_bp_set_channel_probs(qldpc_bp* bp, const double* channel_probs) {
+  if (!bp || !channel_probs) return set_err(QLDPC_EINVAL, "NULL argument");
+  bp->probs.assign(channel_probs, channel_probs + bp->g->n);
+  return upload_llr(bp);
+}
+
+int qldpc_bp_geometry(const qldpc_bp* bp, int32_t* threads, int32_t* vpl, int32_t* lds_bytes,
+                      int32_t* blocks_per_cu) {
+  if (!bp) return set_err(QLDPC_EINVAL, "NULL decoder");
+  if (threads) *threads = bp->TB;
+  if (vpl) *vpl = bp->VPL;
+  if (lds_bytes) *lds_bytes = bp->lds_bytes;
+  if (blocks_per_cu) *blocks_per_cu = bp->blocks_per_cu;
+  return 0;
+}
+
+static SectorDev sector_of(const qldpc_bp* bp, const unsigned long long* lmask, int kw) {
+  SectorDev s;
+  s.vchk = static_cast<const uint32_t*>(bp->vchk.p);
+  s.llr = bp->llr.p;
+  s.lmask = lmask;
+  s.m = bp->g->m;
+  s.n = bp->g->n;
+  s.kw = kw;
+  s.max_iter = bp->max_iter;
+  s.alpha = bp->alpha;
+  return s;
+}
+
+int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, int32_t* d_iters, uint8_t* d_conv,
+                          int64_t B, void* stream) {
+  if (!bp || (B > 0 && (!d_synd || !d_corr))) return set_err(QLDPC_EINVAL, "NULL argument");
+  if (B == 0) return 0;
+  QLDPC_HIP(hipSetDevice(bp->g->device));
+  DecArgs a;
+  a.sec = sector_of(bp, nullptr, 0);
+  a.synd = d_synd;
+  a.corr = d_corr;
+  a.iters = d_iters;
+  a.conv = d_conv;
+  a.B = B;
+  Variant v = get_variant(bp->precision, bp->VPL, bp->DMAX);
+  const long long cap = (long long)bp->blocks_per_cu * bp->cus;
+  const int grid = (int)std::max<long long>(1, std::min<long long>(B, cap));
+  QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
+  return 0;
+}
+
+static int build_lmask(const qldpc_graph* L, int n, DevBuf& buf, int& kw) {
+  if (!L) {
+    kw = 0;
+    return 0;
+  }
+  if (L->n != n) return set_err(QLDPC_EINVAL, "logical operator width != code length");
+  kw = (L->m + 63) / 64;
+  if (kw > 4) return set_err(QLDPC_ENOTSUP, "more than 256 logical operators");
+  if (kw == 0) kw = 1;
+  std::vector<unsigned long long> mask((size_t)n * kw, 0ull);
+  for (int r = 0; r < L->m; ++r)
+    for (int e = L->row_ptr[r]; e < L->row_ptr[r + 1]; ++e)
+      mask[(size_t)L->col_idx[e] * kw + r / 64] |= 1ull << (r % 64);
+  int rc = buf.alloc(mask.size() * 8);
+  if (rc) return rc;
+  QLDPC_HIP(hipMemcpy(buf.p, mask.data(), mask.size() * 8, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec_z, const qldpc_graph* logical_z,
+                    qldpc_mc** out) {
+  if (!out || (!dec_x && !dec_z)) return set_err(QLDPC_EINVAL, "need at least one sector decoder");
+  qldpc_bp* d0 = dec_x ? dec_x : dec_z;
+  if (dec_x && dec_z) {
+    if (dec_x->g->n != dec_z->g->n) return set_err(QLDPC_EINVAL, "sector code lengths differ");
+    if (dec_x->TB != dec_z->TB || dec_x->VPL != dec_z->VPL || dec_x->DMAX != dec_z->DMAX ||
+        dec_x->precision != dec_z->precision)
+      return set_err(QLDPC_EINVAL, "sector decoders need identical geometry/precision (same vars_per_thread)");
+    if (dec_x->g->device != dec_z->g->device) return set_err(QLDPC_EINVAL, "sector decoders on different devices");
+  }
+  QLDPC_HIP(hipSetDevice(d0->g->device));
+  auto* mc = new qldpc_mc();
+  mc->dec[0] = dec_x;
+  mc->dec[1] = dec_z;
+  int rc = 0;
+  if (dec_x && (rc = build_lmask(logical_x, dec_x->g->n, mc->lmask[0], mc->kw[0]))) {
+    delete mc;
+    return rc;
+  }
+  if (dec_z && (rc = build_lmask(logical_z, dec_z->g->n, mc->lmask[1], mc->kw[1]))) {
+    mc->lmask[0].release();
+    delete mc;
+    return rc;
+  }
+  mc->TB = d0->TB;
+  mc->VPL = d0->VPL;
+  mc->DMAX = d0->DMAX;
+  mc->precision = d0->precision;
+  int mmax = std::max(dec_x ? dec_x->g->m : 0, dec_z ? dec_z->g->m : 0);
+  mc->lds_bytes = (int)lds_for(mc->precision, mmax);
+  Variant v = get_variant(mc->precision, mc->VPL, mc->DMAX);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, v.mc_k, mc->TB, mc->lds_bytes) != hipSuccess) nb = 1;
+  mc->blocks_per_cu = std::max(1, nb);
+  mc->cus = d0->cus;
+  if ((rc = mc->counters.alloc(sizeof(qldpc_counters)))) {
+    delete mc;
+    return rc;
+  }
+  *out = mc;
+  return 0;
+}
+
+int qldpc_mc_destroy(qldpc_mc* mc) {
+  if (!mc) return 0;
+  mc->lmask[0].release();
+  mc->lmask[1].release();
+  mc->counters.release();
+  delete mc;
+  return 0;
+}
+
+static unsigned long long ceil_2p53(double t) {
+  if (!(t > 0.0)) return 0ull;
+  if (t >= 1.0) return 1ull << 53;
+  return (unsigned long long)std::ceil(std::ldexp(t, 53));
+}
+
+int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed, uint64_t shot_begin,
+                    int64_t shot_count, int32_t logical_mode, const double* d_uniforms, void* d_counters,
+                    uint8_t* d_fail, uint8_t* d_err, uint8_t* d_corr, int32_t* d_iters, int32_t grid_blocks,
+                    void* stream) {
+  if (!mc || !d_counters) return set_err(QLDPC_EINVAL, "NULL argument");
+  if (logical_mode < 0 || logical_mode > 2) return set_err(QLDPC_EINVAL, "logical_mode must be 0 (X), 1 (Z), 2 (Total)");
+  if (!(px >= 0 && py >= 0 && pz >= 0)) return set_err(QLDPC_EINVAL, "negative Pauli probability");
+  if (shot_count <= 0) return 0;
+  McArgs a;
+  std::memset(&a, 0, sizeof(a));
+  const bool need[2] = {logical_mode != 1, logical_mode != 0};
+  a.nsec = 0;
+  for (int q = 0; q < 2; ++q) {
+    if (!need[q]) continue;
+    if (!mc->dec[q]) return set_err(QLDPC_EINVAL, q == 0 ? "logical_mode needs the X sector (hz decoder)"
+                                                          : "logical_mode needs the Z sector (hx decoder)");
+    if (!mc->lmask[q].p) return set_err(QLDPC_EINVAL, "sector has no logical operators");
+    a.sec[a.nsec] = sector_of(mc->dec[q], static_cast<const unsigned long long*>(mc->lmask[q].p), mc->kw[q]);
+    a.sec_id[a.nsec] = q;
+    a.nsec++;
+  }
+  a.logical_mode = logical_mode;
+  a.mmax = std::max(mc->dec[0] ? mc->dec[0]->g->m : 0, mc->dec[1] ? mc->dec[1]->g->m : 0);
+  a.t1 = pz;
+  a.t2 = pz + px;
+  a.t3 = (pz + px) + py;  // evaluation order of src/Simulators.py:108
+  a.K1 = ceil_2p53(a.t1);
+  a.K2 = ceil_2p53(a.t2);
+  a.K3 = ceil_2p53(a.t3);
+  a.seed = seed;
+  a.shot_begin = shot_begin;
+  a.shot_count = shot_count;
+  a.uniforms = d_uniforms;
+  a.counters = static_cast<unsigned long long*>(d_counters);
+  a.fail = d_fail;
+  a.err = d_err;
+  a.corr = d_corr;
+  a.iters = d_iters;
+  QLDPC_HIP(hipSetDevice((mc->dec[0] ? mc->dec[0] : mc->dec[1])->g->device));
+  Variant v = get_variant(mc->precision, mc->VPL, mc->DMAX);
+  const long long cap = (long long)mc->blocks_per_cu * mc->cus;
+  long long grid = grid_blocks > 0 ? grid_blocks : cap;
+  grid = std::max<long long>(1, std::min<long long>(grid, shot_count));
+  QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
+  return 0;
+}
+
+int qldpc_mc_run(qldpc_mc* mc, double px, double py, double pz, uint64_t seed, uint64_t shot_begin,
+                 int64_t shot_count, int32_t logical_mode, qldpc_counters* out, void* stream) {
+  if (!mc || !out) return set_err(QLDPC_EINVAL, "NULL argument");
+  hipStream_t s = (hipStream_t)stream;
+  QLDPC_HIP(hipMemsetAsync(mc->counters.p, 0, sizeof(qldpc_counters), s));
+  int rc = qldpc_mc_launch(mc, px, py, pz, seed, shot_begin, shot_count, logical_mode, nullptr, mc->counters.p,
+                           nullptr, nullptr, nullptr, nullptr, 0, stream);
+  if (rc) return rc;
+  qldpc_counters c;
+  QLDPC_HIP(hipMemcpyAsync(&c, mc->counters.p, sizeof(c), hipMemcpyDeviceToHost, s));
+  QLDPC_HIP(hipStreamSynchronize(s));
+  out->shots += c.shots;
+  out->failures += c.failures;
+  for (int q = 0; q < 2; ++q) {
+    out->sector_decodes[q] += c.sector_decodes[q];
+    out->sector_iters[q] += c.sector_iters[q];
+    out->sector_nonconv[q] += c.sector_nonconv[q];
+    out->sector_fail[q] += c.sector_fail[q];
+    for (int b = 0; b < QLDPC_HIST_BINS; ++b) out->iter_hist[q][b] += c.iter_hist[q][b];
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,59 @@
+// variants.h — launchable kernel variants (fp32/fp64 × vars-per-thread × max column degree).
+// Each kern_*.hip translation unit instantiates one (T, DMAX) family so the
+// build compiles them in parallel.
+#pragma once
+#include "bp_kernels.h"
+
+namespace qldpc {
+
+using DecLaunch = hipError_t (*)(dim3, dim3, size_t, hipStream_t, const DecArgs&);
+using McLaunch = hipError_t (*)(dim3, dim3, size_t, hipStream_t, const McArgs&);
+
+struct Variant {
+  DecLaunch dec;
+  McLaunch mc;
+  const void* dec_k;
+  const void* mc_k;
+};
+
+Variant get_variant_f32_d4(int vpl);
+Variant get_variant_f32_d8(int vpl);
+Variant get_variant_f64_d4(int vpl);
+Variant get_variant_f64_d8(int vpl);
+
+#ifdef QLDPC_VARIANT_TU
+template <typename T, int VPL, int DMAX>
+hipError_t launch_dec(dim3 g, dim3 b, size_t lds, hipStream_t s, const DecArgs& a) {
+  hipLaunchKernelGGL((bp_decode_kernel<T, VPL, DMAX>), g, b, lds, s, a);
+  return hipGetLastError();
+}
+template <typename T, int VPL, int DMAX>
+hipError_t launch_mc(dim3 g, dim3 b, size_t lds, hipStream_t s, const McArgs& a) {
+  hipLaunchKernelGGL((mc_kernel<T, VPL, DMAX>), g, b, lds, s, a);
+  return hipGetLastError();
+}
+template <typename T, int VPL, int DMAX>
+Variant make_variant() {
+  return Variant{&launch_dec<T, VPL, DMAX>, &launch_mc<T, VPL, DMAX>,
+                 reinterpret_cast<const void*>(&bp_decode_kernel<T, VPL, DMAX>),
+                 reinterpret_cast<const void*>(&mc_kernel<T, VPL, DMAX>)};
+}
+template <typename T, int DMAX>
+Variant pick_vpl(int vpl) {
+  switch (vpl) {
+    case 1: return make_variant<T, 1, DMAX>();
+    case 2: return make_variant<T, 2, DMAX>();
+    case 3: return make_variant<T, 3, DMAX>();
+    case 4: return make_variant<T, 4, DMAX>();
+    case 5: return make_variant<T, 5, DMAX>();
+    case 6: return make_variant<T, 6, DMAX>();
+    case 7: return make_variant<T, 7, DMAX>();
+    case 8: return make_variant<T, 8, DMAX>();
+    case 10: return make_variant<T, 10, DMAX>();
+    case 12: return make_variant<T, 12, DMAX>();
+    default: return Variant{nullptr, nullptr, nullptr, nullptr};
+  }
+}
+#endif
+
+}  // namespace qldpc

@@ -1,0 +1,234 @@
+"""Drop-in decoder classes with the reference's names and signatures.
+
+Mirrors ``src/Decoders.py`` and the space-time part of
+``src/Decoders_SpaceTime.py``.  Where the reference wraps the third-party
+``ldpc.bp_decoder`` (``src/Decoders.py:77-90``), these classes wrap the MI355X
+BP engine (:class:`engine.DeviceBP`): same constructor arguments, same
+``decode(synd) -> ndarray[int]`` contract, plus ``decode_batch`` for many
+syndromes per launch.  ``DecoderClass.GetDecoder(params)`` keeps the reference's
+dict keys and assertions (``:94-172``; ``src/Decoders_SpaceTime.py:227-257``).
+
+BP+OSD (``BPOSD_Decoder``) is outside this engine's scope:
+the class exists so code written against the reference imports cleanly, and
+raises ``NotImplementedError`` when constructed.
+"""
+from __future__ import annotations
+
+from abc import ABC, abstractmethod
+
+import numpy as np
+
+from .codes import CSR, space_time_csr
+
+
+def _int_max_iter(max_iter, n):
+    # ldpc stores max_iter in a C int: the float n/max_iter_ratio the factories
+    # pass (src/Decoders.py:123,162 — quirk Q1) is truncated; 0 means n.
+    mi = int(max_iter)
+    return mi if mi > 0 else n
+
+
+class BPDecoder:
+    """``BPDecoder(h, channel_probs, max_iter, bp_method, ms_scaling_factor)`` (``src/Decoders.py:77-90``)."""
+
+    def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, precision: int = 64,
+                 device: int = 0, vars_per_thread: int = 0):
+        from .engine import DeviceBP
+
+        self.h = h
+        self.max_iter = max_iter
+        self.bp_method = bp_method
+        self.ms_scaling_factor = ms_scaling_factor
+        self.channel_probs = np.asarray(channel_probs, dtype=np.float64)
+        H = h if isinstance(h, CSR) else CSR.from_dense(h)
+        self.num_checks, self.num_qubits = H.m, H.n
+        self.decoder = DeviceBP(H, self.channel_probs, max_iter=_int_max_iter(max_iter, H.n), bp_method=bp_method,
+                                ms_scaling_factor=ms_scaling_factor, precision=precision, device=device,
+                                vars_per_thread=vars_per_thread)
+        self.iter = 0
+        self.converge = 0
+
+    def decode(self, synd):
+        corr, it, conv = self.decoder.decode_batch(np.asarray(synd).reshape(1, -1))
+        self.iter, self.converge = int(it[0]), int(conv[0])
+        return corr[0]
+
+    def decode_batch(self, synd):
+        """[B, m] syndromes -> ([B, n] corrections, iterations [B], converged [B])."""
+        return self.decoder.decode_batch(synd)
+
+
+class FirstMinBPDecoder:
+    """Repeated one-iteration BP while the syndrome weight does not grow (``src/Decoders.py:49-74``)."""
+
+    def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, precision: int = 64,
+                 device: int = 0):
+        self.h = np.asarray(h)
+        self.max_iter = max_iter
+        self._bp = BPDecoder(h, channel_probs, 1, bp_method, ms_scaling_factor, precision=precision, device=device)
+        self._H = CSR.from_dense(self.h)
+
+    def decode(self, synd):
+        return self.decode_batch(np.asarray(synd).reshape(1, -1))[0]
+
+    def decode_batch(self, synd):
+        S = (np.atleast_2d(np.asarray(synd)).astype(np.int64) % 2).astype(np.uint8)
+        B = S.shape[0]
+        correction = np.zeros((B, self._H.n), dtype=np.int64)
+        current = S.copy()
+        active = np.ones(B, dtype=bool)
+        counter = np.zeros(B, dtype=np.int64)
+        new_corr, _, _ = self._bp.decode_batch(current)
+        new_synd = (self._H.matvec(new_corr.astype(np.uint8)) ^ current).astype(np.uint8)
+        while True:
+            ok = active & (new_synd.sum(1) <= current.sum(1)) & (counter < self.max_iter)
+            if not ok.any():
+                break
+            current[ok] = new_synd[ok]
+            correction[ok] = (correction[ok] + new_corr[ok]) % 2
+            counter[ok] += 1
+            active = ok
+            idx = np.flatnonzero(ok)
+            nc, _, _ = self._bp.decode_batch(current[idx])
+            new_corr[idx] = nc
+            new_synd[idx] = (self._H.matvec(nc.astype(np.uint8)) ^ current[idx]).astype(np.uint8)
+        return correction
+
+
+class BPOSD_Decoder:
+    """Placeholder for ``src/Decoders.py:26-41`` (OSD post-processing is out of scope)."""
+
+    def __init__(self, *a, **k):
+        raise NotImplementedError("BP+OSD is not part of the MI355X engine's hot path (SURVEY.md §8f rank 2); "
+                                  "use BPDecoder / BP_Decoder_Class")
+
+
+class DecoderClass(ABC):
+    """``src/Decoders.py:94-97``."""
+
+    @abstractmethod
+    def GetDecoder(self, code_and_noise_channel_params):
+        pass
+
+
+class BP_Decoder_Class(DecoderClass):
+    """``src/Decoders.py:141-172``: factory keyed by ``{'h', 'p_data'[, 'p_syndrome']}``."""
+
+    def __init__(self, max_iter_ratio: int, bp_method: str, ms_scaling_factor: float, precision: int = 64,
+                 device: int = 0):
+        self.decoder_default_params = {"max_iter_ratio": max_iter_ratio, "bp_method": bp_method,
+                                       "ms_scaling_factor": ms_scaling_factor}
+        self.precision = precision
+        self.device = device
+
+    @staticmethod
+    def _probs(params):
+        h = params["h"]
+        if "p_syndrome" in params:
+            num_checks, num_qubits = h.shape[0], h.shape[1] - h.shape[0]
+            probs = np.hstack([params["p_data"] * np.ones(num_qubits), params["p_syndrome"] * np.ones(num_checks)])
+        else:
+            num_checks, num_qubits = h.shape
+            probs = params["p_data"] * np.ones(num_qubits)
+        return num_qubits, probs
+
+    def GetDecoder(self, code_and_noise_channel_params):
+        p = code_and_noise_channel_params
+        assert "h" in p.keys(), "missing the check matrix h"
+        assert "p_data" in p.keys(), "missing the data error prob: p_data"
+        num_qubits, probs = self._probs(p)
+        max_iter = num_qubits / self.decoder_default_params["max_iter_ratio"]
+        return BPDecoder(h=p["h"], channel_probs=probs, max_iter=max_iter,
+                         bp_method=self.decoder_default_params["bp_method"],
+                         ms_scaling_factor=self.decoder_default_params["ms_scaling_factor"],
+                         precision=self.precision, device=self.device)
+
+
+class BPOSD_Decoder_Class(DecoderClass):
+    """``src/Decoders.py:100-138`` (OSD out of scope; constructing a decoder raises)."""
+
+    def __init__(self, max_iter_ratio: int, bp_method: str, ms_scaling_factor: float, osd_method: str,
+                 osd_order: int):
+        self.decoder_default_params = {"max_iter_ratio": max_iter_ratio, "bp_method": bp_method,
+                                       "ms_scaling_factor": ms_scaling_factor, "osd_method": osd_method,
+                                       "osd_order": osd_order}
+
+    def GetDecoder(self, code_and_noise_channel_params):
+        raise NotImplementedError("BP+OSD is not part of the MI355X engine's hot path (SURVEY.md §8f rank 2)")
+
+
+# ------------------------------------------------------------------ space-time
+def GetSpaceTimeCheckMat(h, t0):
+    """Dense ``t0·m × t0·(n+m)`` space-time check matrix (``src/Decoders_SpaceTime.py:179-194``)."""
+    H = np.asarray(h)
+    return space_time_csr(H, int(t0)).to_dense().astype(np.float64)
+
+
+def fold_space_time_correction(error_history, num_qubits: int, num_checks: int, num_rep: int):
+    """Sum of the data slices of a space-time decoding, mod 2 (``src/Decoders_SpaceTime.py:218-223``)."""
+    E = np.asarray(error_history)
+    w = num_qubits + num_checks
+    lead = E.shape[:-1]
+    E = E.reshape(lead + (num_rep, w))
+    return (E[..., :num_qubits].astype(np.int64).sum(axis=-2) % 2)
+
+
+class ST_BP_Decoder_syndrome:
+    """BP on the stacked space-time graph (``src/Decoders_SpaceTime.py:200-223``)."""
+
+    def __init__(self, h, p_data: float, p_synd: float, max_iter: int, bp_method: str, ms_scaling_factor,
+                 num_rep: int, precision: int = 64, device: int = 0):
+        from .engine import DeviceBP
+
+        H = np.asarray(h)
+        self.num_checks, self.num_qubits = H.shape
+        self.h = H
+        self.num_rep = int(num_rep)
+        self.ST_csr = space_time_csr(H, self.num_rep)
+        probs = np.hstack([p_data * np.ones(self.num_qubits), p_synd * np.ones(self.num_checks)] * self.num_rep)
+        self.channel_probs = probs
+        self.max_iter = max_iter
+        self.space_decoder = DeviceBP(self.ST_csr, probs, max_iter=_int_max_iter(max_iter, self.ST_csr.n),
+                                      bp_method=bp_method, ms_scaling_factor=ms_scaling_factor, precision=precision,
+                                      device=device)
+
+    @property
+    def ST_h(self):
+        return self.ST_csr.to_dense().astype(np.float64)
+
+    def decode(self, detector_history):
+        return self.decode_batch(np.asarray(detector_history)[None])[0]
+
+    def decode_batch(self, detector_histories):
+        """[B, num_rep, m] detector histories -> [B, n] corrections."""
+        D = np.asarray(detector_histories)
+        B = D.shape[0]
+        synd = D.reshape(B, D.shape[1] * D.shape[2])
+        err, _, _ = self.space_decoder.decode_batch(synd)
+        return fold_space_time_correction(err, self.num_qubits, self.num_checks, self.num_rep)
+
+
+class ST_BP_Decoder_Class(DecoderClass):
+    """``src/Decoders_SpaceTime.py:227-257`` (keeps quirk Q4: p_synd = p_data when p_syndrome is given)."""
+
+    def __init__(self, max_iter_ratio: int, bp_method: str, ms_scaling_factor: float, precision: int = 64,
+                 device: int = 0):
+        self.decoder_default_params = {"max_iter_ratio": max_iter_ratio, "bp_method": bp_method,
+                                       "ms_scaling_factor": ms_scaling_factor}
+        self.precision = precision
+        self.device = device
+
+    def GetDecoder(self, code_and_noise_channel_params):
+        p = code_and_noise_channel_params
+        assert "h" in p.keys(), "missing the check matrix h"
+        assert "p_data" in p.keys(), "missing the data error prob: p_data"
+        assert "num_rep" in p.keys(), "missing the data error prob: p_data"
+        h = p["h"]
+        p_data = p["p_data"]
+        num_checks, num_qubits = np.asarray(h).shape
+        p_synd = p["p_data"] if "p_syndrome" in p.keys() else 0
+        max_iter = num_qubits / self.decoder_default_params["max_iter_ratio"]
+        return ST_BP_Decoder_syndrome(h=h, p_data=p_data, p_synd=p_synd, max_iter=max_iter,
+                                      bp_method=self.decoder_default_params["bp_method"],
+                                      ms_scaling_factor=self.decoder_default_params["ms_scaling_factor"],
+                                      num_rep=p["num_rep"], precision=self.precision, device=self.device)

@@ -1,0 +1,241 @@
+"""Device-side objects of the engine: Tanner graphs, BP decoders, fused MC runs.
+
+Thin owners of the C-ABI handles in ``libqldpc_hip.so``.  PyTorch-ROCm is used
+only for device buffers and the current HIP stream; every computation runs in
+the hand-written kernels.  No CPU fallback exists (``_native`` raises).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native
+from .codes import CSR, CSSCode
+
+METHODS = {"product_sum": 0, "prod_sum": 0, "ps": 0, "minimum_sum": 1, "min_sum": 1, "ms": 1}
+LOGICAL_MODES = {"X": 0, "Z": 1, "Total": 2}
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        raise _native.NativeUnavailable("torch reports no HIP device; the engine needs an MI355X (no CPU fallback)")
+    return torch
+
+
+def _stream_handle(torch, device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def bp_method_code(bp_method) -> int:
+    if isinstance(bp_method, (int, np.integer)):
+        return int(bp_method)
+    key = str(bp_method).lower()
+    if key not in METHODS:
+        raise ValueError(f"unknown bp_method {bp_method!r}")
+    return METHODS[key]
+
+
+class DeviceGraph:
+    """A parity-check matrix uploaded once (``qldpc_graph_create``)."""
+
+    def __init__(self, H, device: int = 0):
+        c = H if isinstance(H, CSR) else CSR.from_dense(H)
+        self.csr = c
+        self.m, self.n = c.m, c.n
+        self.device = device
+        L = _native.lib()
+        self._rp = np.ascontiguousarray(c.row_ptr, dtype=np.int32)
+        self._ci = np.ascontiguousarray(c.col_idx, dtype=np.int32)
+        h = ctypes.c_void_p()
+        _native.check(L.qldpc_graph_create(device, c.m, c.n, self._rp.ctypes.data_as(ctypes.c_void_p),
+                                           self._ci.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)),
+                      "qldpc_graph_create")
+        self.handle = h
+
+    def info(self):
+        v = [ctypes.c_int32() for _ in range(5)]
+        _native.check(_native.lib().qldpc_graph_info(self.handle, *[ctypes.byref(x) for x in v]), "graph_info")
+        return dict(zip(["m", "n", "nnz", "max_row_deg", "max_col_deg"], [x.value for x in v]))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _native._lib is not None:
+            _native.lib().qldpc_graph_destroy(h)
+            self.handle = None
+
+
+class DeviceBP:
+    """``ldpc.bp_decoder`` equivalent on the GPU (``qldpc_bp_create``)."""
+
+    def __init__(self, H, channel_probs, max_iter: int = 0, bp_method="minimum_sum", ms_scaling_factor=0.625,
+                 precision: int = 64, vars_per_thread: int = 0, device: int = 0, graph: DeviceGraph | None = None,
+                 min_col_slots: int = 0):
+        self.graph = graph if graph is not None else DeviceGraph(H, device=device)
+        n = self.graph.n
+        probs = np.asarray(channel_probs, dtype=np.float64)
+        if probs.ndim == 0:
+            probs = np.full(n, float(probs))
+        if probs.shape != (n,):
+            raise ValueError(f"channel_probs must have length {n}")
+        self.channel_probs = np.ascontiguousarray(probs)
+        self.max_iter = int(max_iter) if int(max_iter) > 0 else n
+        self.bp_method = bp_method_code(bp_method)
+        self.ms_scaling_factor = float(ms_scaling_factor)
+        self.precision = int(precision)
+        h = ctypes.c_void_p()
+        _native.check(_native.lib().qldpc_bp_create(
+            self.graph.handle, self.channel_probs.ctypes.data_as(ctypes.c_void_p), self.max_iter, self.bp_method,
+            self.ms_scaling_factor, self.precision, int(vars_per_thread), int(min_col_slots), ctypes.byref(h)),
+            "qldpc_bp_create")
+        self.handle = h
+
+    @property
+    def m(self):
+        return self.graph.m
+
+    @property
+    def n(self):
+        return self.graph.n
+
+    def geometry(self):
+        v = [ctypes.c_int32() for _ in range(4)]
+        _native.check(_native.lib().qldpc_bp_geometry(self.handle, *[ctypes.byref(x) for x in v]), "bp_geometry")
+        return dict(zip(["threads", "vars_per_thread", "lds_bytes", "blocks_per_cu"], [x.value for x in v]))
+
+    def decode_batch_device(self, synd_dev, corr_dev, iters_dev=None, conv_dev=None, stream=None):
+        """Decode device uint8 syndromes [B, m] into device corrections [B, n] (async)."""
+        torch = _torch()
+        B = int(synd_dev.shape[0])
+        assert synd_dev.dtype == torch.uint8 and synd_dev.is_contiguous() and synd_dev.shape[1] == self.m
+        assert corr_dev.dtype == torch.uint8 and corr_dev.is_contiguous() and tuple(corr_dev.shape) == (B, self.n)
+        s = stream if stream is not None else _stream_handle(torch, synd_dev.device)
+        _native.check(_native.lib().qldpc_bp_decode_batch(
+            self.handle, ctypes.c_void_p(synd_dev.data_ptr()), ctypes.c_void_p(corr_dev.data_ptr()),
+            ctypes.c_void_p(iters_dev.data_ptr()) if iters_dev is not None else None,
+            ctypes.c_void_p(conv_dev.data_ptr()) if conv_dev is not None else None, B, s), "qldpc_bp_decode_batch")
+
+    def decode_batch(self, synd):
+        """Host convenience: ``synd`` [B, m] (0/1) -> (corr [B, n] int, iters [B], converged [B])."""
+        torch = _torch()
+        s = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.int64) % 2, dtype=np.uint8)
+        if s.shape[1] != self.m:
+            raise ValueError(f"syndrome length {s.shape[1]} != number of checks {self.m}")
+        dev = torch.device("cuda", self.graph.device)
+        sd = torch.from_numpy(s).to(dev)
+        corr = torch.empty((s.shape[0], self.n), dtype=torch.uint8, device=dev)
+        iters = torch.empty(s.shape[0], dtype=torch.int32, device=dev)
+        conv = torch.empty(s.shape[0], dtype=torch.uint8, device=dev)
+        self.decode_batch_device(sd, corr, iters, conv)
+        torch.cuda.synchronize(dev)
+        return corr.cpu().numpy().astype(np.int64), iters.cpu().numpy(), conv.cpu().numpy().astype(bool)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _native._lib is not None:
+            _native.lib().qldpc_bp_destroy(h)
+            self.handle = None
+
+
+@dataclass
+class MCResult:
+    shots: int
+    failures: int
+    sector_decodes: list
+    sector_iters: list
+    sector_nonconv: list
+    sector_fail: list
+    iter_hist: np.ndarray  # [2, HIST_BINS]
+    fail: np.ndarray | None = None
+    err: np.ndarray | None = None
+    corr: np.ndarray | None = None
+    iters: np.ndarray | None = None
+
+    @staticmethod
+    def from_words(w: np.ndarray) -> "MCResult":
+        w = np.asarray(w, dtype=np.int64)
+        hb = _native.HIST_BINS
+        return MCResult(int(w[0]), int(w[1]), w[2:4].tolist(), w[4:6].tolist(), w[6:8].tolist(), w[8:10].tolist(),
+                        w[10:10 + 2 * hb].reshape(2, hb).copy())
+
+    def merge(self, o: "MCResult") -> "MCResult":
+        return MCResult(self.shots + o.shots, self.failures + o.failures,
+                        [a + b for a, b in zip(self.sector_decodes, o.sector_decodes)],
+                        [a + b for a, b in zip(self.sector_iters, o.sector_iters)],
+                        [a + b for a, b in zip(self.sector_nonconv, o.sector_nonconv)],
+                        [a + b for a, b in zip(self.sector_fail, o.sector_fail)], self.iter_hist + o.iter_hist)
+
+
+class DeviceMC:
+    """Fused shot loop of ``CodeSimulator_DataError`` on one GPU (``qldpc_mc_*``).
+
+    Sector X decodes X errors with the hz decoder and checks lz; sector Z
+    decodes Z errors with the hx decoder and checks lx.
+    """
+
+    def __init__(self, code: CSSCode, dec_x: DeviceBP | None, dec_z: DeviceBP | None):
+        self.code = code
+        self.dec_x, self.dec_z = dec_x, dec_z
+        dev = (dec_x or dec_z).graph.device
+        self.device = dev
+        self.lz = DeviceGraph(code.csr("lz"), device=dev) if dec_x is not None else None
+        self.lx = DeviceGraph(code.csr("lx"), device=dev) if dec_z is not None else None
+        h = ctypes.c_void_p()
+        _native.check(_native.lib().qldpc_mc_create(
+            dec_x.handle if dec_x else None, self.lz.handle if self.lz else None,
+            dec_z.handle if dec_z else None, self.lx.handle if self.lx else None, ctypes.byref(h)),
+            "qldpc_mc_create")
+        self.handle = h
+
+    def new_counters(self):
+        torch = _torch()
+        return torch.zeros(_native.COUNTER_WORDS, dtype=torch.int64, device=torch.device("cuda", self.device))
+
+    def launch(self, px, py, pz, seed, shot_begin, shot_count, logical_mode="X", counters=None, uniforms=None,
+               fail=None, err=None, corr=None, iters=None, grid_blocks=0, stream=None):
+        """Asynchronous launch on the current stream; counters accumulate in ``counters`` (device int64)."""
+        torch = _torch()
+        if counters is None:
+            raise ValueError("counters buffer required")
+        mode = LOGICAL_MODES[logical_mode] if isinstance(logical_mode, str) else int(logical_mode)
+        s = stream if stream is not None else _stream_handle(torch, counters.device)
+
+        def ptr(t):
+            return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+        _native.check(_native.lib().qldpc_mc_launch(
+            self.handle, float(px), float(py), float(pz), int(seed) & (2**64 - 1), int(shot_begin), int(shot_count),
+            mode, ptr(uniforms), ptr(counters), ptr(fail), ptr(err), ptr(corr), ptr(iters), int(grid_blocks), s),
+            "qldpc_mc_launch")
+
+    def run(self, px, py, pz, seed, shot_begin, shot_count, logical_mode="X", uniforms=None, per_shot=False,
+            grid_blocks=0) -> MCResult:
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        n = self.code.N
+        S = int(shot_count)
+        cnt = self.new_counters()
+        u = torch.from_numpy(np.ascontiguousarray(uniforms, dtype=np.float64)).to(dev) if uniforms is not None else None
+        if u is not None and tuple(u.shape) != (S, n):
+            raise ValueError(f"uniforms must be [{S}, {n}]")
+        f = e = c = it = None
+        if per_shot:
+            f = torch.zeros(S, dtype=torch.uint8, device=dev)
+            e = torch.zeros((S, n), dtype=torch.uint8, device=dev)
+            c = torch.zeros((S, 2, n), dtype=torch.uint8, device=dev)
+            it = torch.zeros((S, 2), dtype=torch.int32, device=dev)
+        self.launch(px, py, pz, seed, shot_begin, S, logical_mode, cnt, u, f, e, c, it, grid_blocks)
+        torch.cuda.synchronize(dev)
+        res = MCResult.from_words(cnt.cpu().numpy())
+        if per_shot:
+            res.fail, res.err, res.corr, res.iters = f.cpu().numpy(), e.cpu().numpy(), c.cpu().numpy(), it.cpu().numpy()
+        return res
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _native._lib is not None:
+            _native.lib().qldpc_mc_destroy(h)
+            self.handle = None

@@ -1,0 +1,233 @@
+"""Generate golden vectors from the reference's own Python harness.
+
+Run in the build container only (``/root/reference`` is not on the GPU box):
+
+    python tests/golden/make_golden.py
+
+The reference modules import third-party packages that are absent here
+(``graph_tools``, ``ldpc``, ``bposd``, ``stim``, …), so empty stub
+modules are registered under those names before importing
+``Decoders``/``Simulators``/``Decoders_SpaceTime``/``Simulators_SpaceTime`` from
+``/root/reference/src``.  The reference's own code then runs unchanged for
+everything that does not live in those packages: error sampling
+(``_generate_error``), syndromes, failure checks (``_single_run``), the WER
+formulas (``WordErrorRate``), ``GetSpaceTimeCheckMat`` and the space-time
+detector histories.  The one stubbed class that is exercised, ``ldpc.bp_decoder``,
+is backed by this repository's CPU oracle — so BP outputs in these fixtures are
+oracle outputs (the reference pins no BP results), while
+everything around BP is the reference's own behaviour.
+
+No pickle from the reference is loaded: the n225 code comes from the bundled
+``.npz`` (converted by the non-executing reader in ``safepickle.py``).
+Outputs: ``tests/golden/*.npz`` (data only).
+"""
+from __future__ import annotations
+
+import os
+import random
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+REF_SRC = "/root/reference/src"
+
+import oracle  # noqa: E402  (CPU restatement, used only as the stubbed BP)
+from qldpc_fault_tolerance_amd import codes  # noqa: E402
+
+
+class OracleBP:
+    """Stand-in for ``ldpc.bp_decoder`` recording how the reference constructs it."""
+
+    log = []
+
+    def __init__(self, parity_check_matrix=None, channel_probs=None, max_iter=0, bp_method="minimum_sum",
+                 ms_scaling_factor=1.0, **kw):
+        if parity_check_matrix is None:
+            parity_check_matrix = kw.pop("H")
+        self.H = np.asarray(parity_check_matrix)
+        self.channel_probs = np.asarray(channel_probs, dtype=np.float64)
+        self.max_iter_arg = max_iter
+        self.max_iter = int(max_iter)  # Cython int conversion truncates (quirk Q1)
+        self.bp_method = bp_method
+        self.alpha = ms_scaling_factor
+        OracleBP.log.append(dict(shape=self.H.shape, max_iter_arg=float(max_iter), bp_method=bp_method,
+                                 alpha=float(ms_scaling_factor), probs=self.channel_probs.copy()))
+
+    def decode(self, synd):
+        corr, _, _ = oracle.bp_decode_batch(self.H, self.channel_probs, self.max_iter, self.bp_method, self.alpha,
+                                            np.asarray(synd).reshape(1, -1), 64)
+        return corr[0].astype(int)
+
+
+def install_stubs():
+    def mod(name, **attrs):
+        m = types.ModuleType(name)
+        m.__dict__.update(attrs)
+        sys.modules[name] = m
+        return m
+
+    class _Anything:
+        def __init__(self, *a, **k):
+            raise RuntimeError("stubbed third-party class used")
+
+    mod("graph_tools", Graph=_Anything)
+    ldpc = mod("ldpc", bp_decoder=OracleBP)
+    ldpc.codes = mod("ldpc.codes")
+    ldpc.code_util = mod("ldpc.code_util", compute_code_distance=lambda H: 0)
+    ldpc.mod2 = mod("ldpc.mod2")
+    bposd = mod("bposd", bposd_decoder=_Anything)
+    bposd.css_decode_sim = mod("bposd.css_decode_sim", css_decode_sim=_Anything)
+    bposd.hgp = mod("bposd.hgp", hgp=_Anything)
+    bposd.css = mod("bposd.css", css_code=_Anything)
+    for name in ("stim", "pymatching", "sinter"):
+        m = mod(name)
+        m.__getattr__ = lambda attr: type(attr, (), {})  # annotation-only names (stim.Circuit, ...)
+    import matplotlib
+
+    matplotlib.use("Agg")
+    sys.path.insert(0, REF_SRC)
+
+
+def main():
+    install_stubs()
+    import Decoders  # noqa: F401
+    import Decoders_SpaceTime
+    import Simulators
+    import Simulators_SpaceTime
+
+    # serial parmap: same semantics, no fork (src/Simulators.py:45-61)
+    Simulators.parmap = lambda f, X, nprocs=1: [f(x) for x in X]
+    Simulators_SpaceTime.parmap = Simulators.parmap
+
+    code = codes.get_code("hgp_34_n225")
+    n = code.N
+    out = {}
+
+    # ---- A5: _generate_error on seeded CPython random, with the raw uniforms
+    for tag, probs in [("dep05", [0.05 / 2] * 3), ("dep10", [0.10 / 2] * 3), ("asym", [0.03, 0.01, 0.07])]:
+        sim = Simulators.CodeSimulator_DataError(code=code, decoder_x=None, decoder_z=None,
+                                                 pauli_error_probs=probs, eval_logical_type="Total")
+        E_x, E_z, U = [], [], []
+        for s in range(20):
+            random.seed(1000 + s)
+            ex, ez = sim._generate_error()
+            random.seed(1000 + s)
+            U.append([random.random() for _ in range(n)])
+            E_x.append(ex.copy())
+            E_z.append(ez.copy())
+        out[f"gen_{tag}_probs"] = np.array(probs)
+        out[f"gen_{tag}_u"] = np.array(U)
+        out[f"gen_{tag}_ex"] = np.array(E_x, dtype=np.uint8)
+        out[f"gen_{tag}_ez"] = np.array(E_z, dtype=np.uint8)
+
+    # ---- A1-A3, A6-A8: _single_run through the reference decoder factory
+    for p in (0.03, 0.06):
+        cls = Decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+        OracleBP.log.clear()
+        dx = cls.GetDecoder({"h": code.hz, "p_data": p})
+        dz = cls.GetDecoder({"h": code.hx, "p_data": p})
+        out[f"factory_p{int(p*100)}_max_iter_arg"] = np.array([d["max_iter_arg"] for d in OracleBP.log])
+        out[f"factory_p{int(p*100)}_probs"] = np.array([d["probs"] for d in OracleBP.log])
+        probs = [p / 2] * 3  # EvalWER data branch (src/Simulators.py:763-764)
+        for mode in ("X", "Z", "Total"):
+            sim = Simulators.CodeSimulator_DataError(code=code, decoder_x=dx, decoder_z=dz,
+                                                     pauli_error_probs=probs, eval_logical_type=mode)
+            flags = []
+            for s in range(60):
+                random.seed(5000 + s)
+                flags.append(int(sim._single_run()))
+            out[f"run_p{int(p*100)}_{mode}_fail"] = np.array(flags, dtype=np.uint8)
+        # the uniforms of those shots (same seeds), for replay through the engine
+        U = []
+        for s in range(60):
+            random.seed(5000 + s)
+            U.append([random.random() for _ in range(n)])
+        out[f"run_p{int(p*100)}_u"] = np.array(U)
+
+    # ---- A8: WordErrorRate formula incl. quirk Q2, with injected failure lists
+    class _K:
+        N, K = n, code.K
+        hx, hz, lx, lz = code.hx, code.hz, code.lx, code.lz
+
+    wer_cases = []
+    for num_run, nfail in [(1000, 0), (1000, 17), (5000, 1234), (200, 199), (10, 10)]:
+        sim = Simulators.CodeSimulator_DataError(code=_K, decoder_x=None, decoder_z=None)
+        flags = [1] * nfail + [0] * (num_run - nfail)
+        sim._single_run = (lambda it=iter(flags): next(it))
+        wer, eb = sim.WordErrorRate(num_run)
+        wer_cases.append([num_run, nfail, wer, eb])
+    out["wer_cases"] = np.array(wer_cases, dtype=np.float64)
+
+    # ---- A10: GetSpaceTimeCheckMat
+    for t0 in (1, 2, 3):
+        ST = Decoders_SpaceTime.GetSpaceTimeCheckMat(code.hx.astype(float), t0)
+        c = codes.CSR.from_dense(ST)
+        out[f"st_t{t0}_shape"] = np.array(ST.shape)
+        out[f"st_t{t0}_row_ptr"] = c.row_ptr
+        out[f"st_t{t0}_col_idx"] = c.col_idx
+
+    # ---- A11/A12: ST decoder factory + decode fold on random detector histories
+    stc = Decoders_SpaceTime.ST_BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    OracleBP.log.clear()
+    st_dec = stc.GetDecoder({"h": code.hz, "p_data": 0.02, "p_syndrome": 0.02, "num_rep": 3})
+    out["stfactory_max_iter_arg"] = np.array([OracleBP.log[0]["max_iter_arg"]])
+    out["stfactory_probs"] = OracleBP.log[0]["probs"]
+    rng = np.random.default_rng(3)
+    hist = (rng.random((10, 3, code.hz.shape[0])) < 0.03).astype(np.float64)
+    out["stdec_hist"] = hist.astype(np.uint8)
+    out["stdec_corr"] = np.array([st_dec.decode(h) for h in hist], dtype=np.uint8)
+
+    # ---- A13: CodeSimulator_Phenon_SpaceTime detector histories (quirk Q3) and failures
+    class Capture:
+        def __init__(self, inner):
+            self.inner, self.seen = inner, []
+
+        def decode(self, x):
+            self.seen.append(np.array(x, dtype=np.uint8))
+            return self.inner.decode(x)
+
+    p = 0.02
+    d1x = Capture(stc.GetDecoder({"h": code.hz, "p_data": p, "p_syndrome": p, "num_rep": 3}))
+    d1z = Capture(stc.GetDecoder({"h": code.hx, "p_data": p, "p_syndrome": p, "num_rep": 3}))
+    cls = Decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    d2x = Capture(cls.GetDecoder({"h": code.hz, "p_data": p}))
+    d2z = Capture(cls.GetDecoder({"h": code.hx, "p_data": p}))
+    sim = Simulators_SpaceTime.CodeSimulator_Phenon_SpaceTime(
+        code=code, decoder1_x=d1x, decoder1_z=d1z, decoder2_x=d2x, decoder2_z=d2z,
+        pauli_error_probs=[p / 2] * 3, q=p, eval_logical_type="Total", num_rep=3)
+    flags, U = [], []
+    n_u = 2 * (3 * (n + code.hx.shape[0] + code.hz.shape[0])) + (n + code.hx.shape[0] + code.hz.shape[0])
+    for s in range(12):
+        random.seed(9000 + s)
+        flags.append(int(sim._single_run(3)))  # num_rounds = 3 -> 2 noisy rounds of 3 reps + final
+        random.seed(9000 + s)
+        U.append([random.random() for _ in range(n_u)])
+    out["phenst_fail"] = np.array(flags, dtype=np.uint8)
+    out["phenst_u"] = np.array(U)
+    out["phenst_d1z_hist"] = np.array(d1z.seen)
+    out["phenst_d1x_hist"] = np.array(d1x.seen)
+    out["phenst_d2z_synd"] = np.array(d2z.seen)
+    out["phenst_d2x_synd"] = np.array(d2x.seen)
+    # WordErrorRate formula of the ST simulator (:531-548) with injected flags
+    st_wer = []
+    for num_cycles, num_samples, nfail in [(7, 100, 9), (13, 400, 77), (13, 50, 50)]:
+        sim2 = Simulators_SpaceTime.CodeSimulator_Phenon_SpaceTime(
+            code=_K, decoder1_x=None, decoder1_z=None, decoder2_x=None, decoder2_z=None,
+            pauli_error_probs=[p / 2] * 3, q=p, eval_logical_type="Total", num_rep=3)
+        fl = [1] * nfail + [0] * (num_samples - nfail)
+        sim2._single_run = (lambda num_rounds, it=iter(fl): next(it))
+        w, _ = sim2.WordErrorRate(num_cycles, num_samples)
+        st_wer.append([num_cycles, num_samples, nfail, w])
+    out["phenst_wer_cases"] = np.array(st_wer, dtype=np.float64)
+
+    np.savez_compressed(os.path.join(HERE, "reference_harness_n225.npz"), **out)
+    print("wrote", os.path.join(HERE, "reference_harness_n225.npz"), len(out), "arrays")
+
+
+if __name__ == "__main__":
+    main()
