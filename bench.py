@@ -1,0 +1,203 @@
+"""Headline benchmark: BP-decoded shots/s on hgp_34_n1600 (BASELINE.json `metric`).
+
+One *step* = one fused Monte Carlo launch (``qldpc_mc_launch``) over a batch of
+``--shots`` shots per GPU of the reference's code-capacity shot loop
+(``CodeSimulator_DataError._single_run``, src/Simulators.py:117-168, as driven
+by ``CodeFamily.EvalWER('data')``, :759-777): depolarizing Pauli error with
+probabilities ``[p/3]*3`` where ``p = eval_p*3/2``, syndromes on hz and hx, two
+min-sum BP decodes (alpha=0.625, max_iter=int(N/10)=160 -- the notebooks'
+settings), residual and logical check, ``eval_logical_type='Total'``.  The
+counters stay on the device and are all-reduced over RCCL once at the end (the
+only collective of the path).
+
+Run as ``python bench.py`` (N=1) or under ``torch.distributed.run`` with one
+rank per GPU; shots are sharded by global shot index (weak scaling: every rank
+decodes ``--shots`` shots per step).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Headline operating point: BP-only crossing region of the synthetic (3,4) HGP
+# family under this decoder (tools/threshold_scan.py).
+DEFAULT_P = 0.06
+SEED = 0x51D5EED0 + 2  # seed = 0x51D5EED0 + config_id (config 2)
+
+# Peaks (MI355X_MICROARCH.md §LDS / §HBM): LDS aggregate ~75 TB/s for 4-byte
+# ds_read/ds_atomic traffic with every CU streaming; HBM 8 TB/s spec.
+LDS_PEAK_GBS = 75_000.0
+HBM_PEAK_GBS = 8_000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--code", default="hgp_34_n1600")
+    ap.add_argument("--p", type=float, default=DEFAULT_P)
+    ap.add_argument("--shots", type=int, default=1 << 18, help="shots per GPU per step")
+    ap.add_argument("--precision", type=int, default=32, choices=(32, 64))
+    ap.add_argument("--max-iter-ratio", type=float, default=10)
+    ap.add_argument("--logical", default="Total", choices=("X", "Z", "Total"))
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def pauli_probs(eval_p):
+    """EvalWER data branch arithmetic (src/Simulators.py:763-764): p = eval_p*3/2, [p/3]*3."""
+    p = eval_p * 3 / 2
+    return p / 3, p / 3, p / 3
+
+
+def cpu_baseline(code, eval_p, max_iter, logical, budget_s):
+    """Oracle (CPU restatement, fp64, host cores via OpenMP) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker / baseline only
+
+    cores = os.cpu_count() or 1
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    px, py, pz = pauli_probs(eval_p)
+    S = 32 * cores
+    t0 = time.perf_counter()
+    oracle.mc_run(code, px, py, pz, seed=SEED, shot_begin=0, shot_count=S, logical_mode=logical,
+                  probs_x=eval_p, probs_z=eval_p, max_iter=max_iter, precision=64, nthreads=cores)
+    dt = max(time.perf_counter() - t0, 1e-6)
+    S2 = int(max(S, min(4_000_000, S * budget_s / dt)))
+    t0 = time.perf_counter()
+    r = oracle.mc_run(code, px, py, pz, seed=SEED, shot_begin=0, shot_count=S2, logical_mode=logical,
+                      probs_x=eval_p, probs_z=eval_p, max_iter=max_iter, precision=64, nthreads=cores)
+    dt = time.perf_counter() - t0
+    return {"value": S2 / dt, "unit": "shots/s", "cores": cores, "kind": "port",
+            "sample": f"{S2} shots of the same workload (shots 0..{S2 - 1}, same seed), oracle/qldpc_oracle.c "
+                      f"fp64 with {cores} OpenMP threads, {dt:.1f} s; LER={r['failures'] / S2:.4g}"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from qldpc_fault_tolerance_amd import codes
+    from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceMC
+
+    code = codes.get_code(a.code)
+    n = code.N
+    max_iter = int(n / a.max_iter_ratio)
+    p = a.p
+    px, py, pz = pauli_probs(p)
+    need_x, need_z = a.logical != "Z", a.logical != "X"
+    # decoders as EvalWER builds them: p_data = eval_p on hz (X errors) and hx (Z errors)
+    dx = DeviceBP(code.hz, p * np.ones(n), max_iter=max_iter, bp_method="minimum_sum", ms_scaling_factor=0.625,
+                  precision=a.precision, device=local) if need_x else None
+    vpl = dx.geometry()["vars_per_thread"] if dx is not None else 0
+    dz = DeviceBP(code.hx, p * np.ones(n), max_iter=max_iter, bp_method="minimum_sum", ms_scaling_factor=0.625,
+                  precision=a.precision, device=local, vars_per_thread=vpl) if need_z else None
+    mc = DeviceMC(code, dx, dz)
+    S = int(a.shots)
+    stream = torch.cuda.current_stream(dev)
+    cnt = mc.new_counters()
+
+    def step(i):
+        # global shot blocks indexed by (step, rank): shot ranges never overlap across ranks
+        mc.launch(px, py, pz, SEED, (i * world + rank) * S, S, a.logical, cnt)
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    cnt.zero_()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record(stream)
+        step(a.warmup + i)
+        ev[i][1].record(stream)
+    if world > 1:
+        dist.all_reduce(cnt)  # shots, failures, iterations, non-converged, histogram
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    w = cnt.cpu().numpy()
+    shots = int(w[0])
+    if shots != S * a.steps * world:
+        raise RuntimeError(f"counter mismatch: {shots} shots != {S} x {a.steps} x {world}")
+    decodes = int(w[2] + w[3])
+    iters = int(w[4] + w[5])
+    nonconv = int(w[6] + w[7])
+    E = int(code.hz.sum())
+    mh, nh = code.hz.shape
+    # SURVEY.md §8d algorithmic bytes: 16 B (fp32) / 32 B (fp64) per edge-iteration of two-phase
+    # flooding + per decode ceil(m/8)+ceil(n/8)+16 B of syndrome / decision / counters.
+    bpe = 16 if a.precision == 32 else 32
+    bytes_per_launch = (bpe * E * iters + decodes * ((mh + 7) // 8 + (nh + 7) // 8 + 16)) / (a.steps * world)
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    value = shots / elapsed
+    out = {
+        "metric": "BP-decoded shots/sec (node) on hgp_34_n1600 + % of HBM/LDS roofline",
+        "value": value,
+        "unit": "shots/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if a.precision == 32 else "f64",
+        "data": "synthetic: Philox-sampled depolarizing errors on the synthesized [[1600,64]] HGP stand-in "
+                "(the reference's hgp_34_n1600.pkl is missing; DESIGN.md)",
+        "config": {"workload": f"{a.code} code-capacity BP shot loop, eval_p={p}, min-sum alpha=0.625, "
+                               f"max_iter={max_iter}, eval_logical_type={a.logical}",
+                   "code": a.code, "p": p, "shots_per_gpu_step": S, "max_iter": max_iter,
+                   "decodes_per_shot": int(need_x) + int(need_z), "parallelism": f"shot-sharded x{world}"},
+        "decodes_per_s": decodes / elapsed,
+        "mean_iters_per_decode": iters / max(decodes, 1),
+        "nonconverged_frac": nonconv / max(decodes, 1),
+        "logical_error_rate": int(w[1]) / max(shots, 1),
+        "roofline": {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / LDS_PEAK_GBS, "traffic": None,
+                     "hbm_peak": HBM_PEAK_GBS, "frac_of_hbm_peak": achieved / HBM_PEAK_GBS,
+                     "kernel": "qldpc::mc_kernel", "kernel_ms": kern_ms,
+                     "bytes_per_launch": bytes_per_launch},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(code, p, max_iter, a.logical, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
