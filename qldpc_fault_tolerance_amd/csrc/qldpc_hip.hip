@@ -1,13 +1,20 @@
 // qldpc_hip.hip — host runtime + C ABI (include/qldpc_hip.h) of the MI355X engine.
 //
 // Graph/decoder/MC handles own their device buffers; launches take a caller
-// stream.  Kernel variants (fp32/fp64 × variables-per-thread × max column
-// degree) are instantiated here and selected per graph at create time.
+// stream.  Two kernel engines are built:
+//   engine 2 (default) — bp_slot.h: NS decodes in flight per workgroup,
+//                        row-major v2c slots, check-centric gather;
+//   engine 1           — bp_kernels.h: per-check LDS state updated by
+//                        returning LDS atomics (kept for A/B measurements,
+//                        selected with QLDPC_ENGINE=1).
+// Variants (fp32/fp64 × variables per thread × max column degree × slots) are
+// selected per graph at create time.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -50,8 +57,15 @@ struct DevBuf {
   }
 };
 
-constexpr int kVplMax = 12;
 const int kVplSet[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12};
+const int kSVplSet[] = {1, 2, 3, 4};
+constexpr int kLdsMax = 160 * 1024;
+constexpr int kChunkMax = 1024;
+
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return (e && *e) ? std::atoi(e) : dflt;
+}
 
 }  // namespace
 
@@ -64,12 +78,14 @@ struct qldpc_graph {
 
 struct qldpc_bp {
   qldpc_graph* g = nullptr;
+  int engine = 2;
   int max_iter = 0, method = 1, precision = 64;
   double alpha = 0.625;
-  int TB = 64, VPL = 1, DMAX = 4;
+  int TB = 64, VPL = 1, DMAX = 4, NS = 1;
+  int nch = 0;  // engine 2: 16-byte chunks per check row
   int lds_bytes = 0, blocks_per_cu = 0, cus = 0;
   std::vector<double> probs;
-  DevBuf vchk, llr;
+  DevBuf vchk, llr;  // engine 1: packed u16 check ids; engine 2: edge words (check | slot<<16)
 };
 
 struct qldpc_mc {
@@ -77,7 +93,8 @@ struct qldpc_mc {
   int kw[2] = {0, 0};
   DevBuf lmask[2];
   DevBuf counters;
-  int TB = 0, VPL = 0, DMAX = 0, precision = 64, lds_bytes = 0, blocks_per_cu = 0, cus = 0;
+  int engine = 2, TB = 0, VPL = 0, DMAX = 0, NS = 1, precision = 64, lds_bytes = 0, blocks_per_cu = 0, cus = 0;
+  int mmax = 0, vslots = 0, img_bytes = 0;
 };
 
 // --------------------------------------------------------------- dispatch
@@ -88,9 +105,14 @@ Variant get_variant(int precision, int vpl, int dmax) {
   return dmax == 4 ? get_variant_f64_d4(vpl) : get_variant_f64_d8(vpl);
 }
 
+SVariant get_svariant(int precision, int vpl, int dmax, int ns) {
+  if (precision == 32) return dmax == 4 ? get_svariant_f32_d4(vpl, ns) : get_svariant_f32_d8(vpl, ns);
+  return dmax == 4 ? get_svariant_f64_d4(vpl, ns) : get_svariant_f64_d8(vpl, ns);
+}
+
 int round_up(int x, int a) { return (x + a - 1) / a * a; }
 
-// Choose threads-per-shot TB (multiple of 64, <= 512) and variables per thread.
+// ---- engine 1 geometry: threads per shot TB (multiple of 64, <= 512)
 // Largest vars-per-thread whose kernels compile without register spills (gfx950,
 // -Rpass-analysis=kernel-resource-usage).
 int max_spill_free_vpl(int precision, int dmax) {
@@ -107,7 +129,6 @@ int choose_geometry(int n, int m, int requested_vpl, int vmax, int& TB, int& VPL
     TB = round_up((n + VPL - 1) / VPL, 64);
     if (TB > kMaxThreads) return set_err(QLDPC_EINVAL, "vars_per_thread too small for this graph (>512 threads)");
   } else {
-    // smallest padding waste with the per-thread work >= 4 variables when possible
     double best = 1e30;
     for (int v : kVplSet) {
       const int tb = round_up((n + v - 1) / v, 64);
@@ -129,6 +150,63 @@ int choose_geometry(int n, int m, int requested_vpl, int vmax, int& TB, int& VPL
 size_t lds_for(int precision, int mmax) {
   const size_t pair = precision == 32 ? 8 : 16;
   return pair * 2 * (size_t)mmax + 4 * 2 * (size_t)mmax + 64;
+}
+
+// ---- engine 2 geometry: VPL in {1..4}, TB <= 1024, NS slots.
+// Largest VPL whose slot kernels compile without scratch at NS slots (gfx950,
+// tools/kres.sh).  Fewer variables per thread = more threads per shot.
+int smax_vpl(int precision, int dmax, int ns) {
+  if (dmax == 8) return 1;
+  if (ns == 4) return 1;
+  return 2;
+}
+
+int choose_sgeometry(int n, int m, int requested_vpl, int precision, int dmax, int& TB, int& VPL) {
+  if (requested_vpl > 0) {
+    bool ok = false;
+    for (int v : kSVplSet) ok |= (v == requested_vpl);
+    if (!ok) return set_err(QLDPC_EINVAL, "vars_per_thread must be one of 1-4 (engine 2)");
+    VPL = requested_vpl;
+    TB = round_up((n + VPL - 1) / VPL, 64);
+    if (TB > kMaxThreadsS) return set_err(QLDPC_EINVAL, "vars_per_thread too small for this graph (>1024 threads)");
+  } else {
+    VPL = 0;
+    const int vmax = smax_vpl(precision, dmax, 1);
+    for (int v : {2, 1}) {  // measured order on n225/n1600, spill-free first
+      const int tb = round_up((n + v - 1) / v, 64);
+      if (v <= vmax && tb <= kMaxThreadsS) {
+        VPL = v;
+        TB = tb;
+        break;
+      }
+    }
+    if (!VPL) {
+      for (int v : kSVplSet) {
+        const int tb = round_up((n + v - 1) / v, 64);
+        if (tb <= kMaxThreadsS) {
+          VPL = v;
+          TB = tb;
+          break;
+        }
+      }
+    }
+    if (!VPL) return set_err(QLDPC_ENOTSUP, "graph too large for one workgroup per shot (n > 4096)");
+  }
+  if ((m + TB - 1) / TB > 32) return set_err(QLDPC_ENOTSUP, "too many checks per thread (m > 32*threads)");
+  return 0;
+}
+
+// Slots per workgroup: env QLDPC_NS, else the most that fit LDS and stay
+// spill-free at this VPL.
+int choose_ns(int img, int precision, int dmax, int vpl) {
+  const int forced = env_int("QLDPC_NS", 0);
+  if (forced == 1 || forced == 2 || forced == 4) {
+    return slot_lds_bytes(forced, img, kChunkMax) <= (size_t)kLdsMax ? forced : 1;
+  }
+  int best = 1;
+  for (int ns : {2, 4})
+    if (slot_lds_bytes(ns, img, kChunkMax) <= (size_t)kLdsMax && vpl <= smax_vpl(precision, dmax, ns)) best = ns;
+  return best;
 }
 
 int device_cus(int dev, int& cus) {
@@ -228,6 +306,35 @@ static int upload_llr(qldpc_bp* bp) {
   return 0;
 }
 
+// Engine-2 edge table: for variable j = k*TB + t and its d-th check i (rows
+// ascending), the word ((i + 1) | slot<<16) where slot is j's position in row i
+// of the row-major V image (after the 16-byte sink), with the 16-byte chunks of
+// row i XOR-swizzled so that consecutive rows read by consecutive lanes hit
+// distinct LDS banks.  Missing edges are the word 0 (dummies, bp_slot.h).
+static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
+                             std::vector<uint32_t>& out) {
+  const int nv = 16 / tsize;  // messages per 16-byte chunk
+  const int rw = nch * nv;
+  const int swz_mask = (nch == 2) ? 1 : (nch == 4) ? 3 : 0;
+  const int swz_shift = (nch == 2) ? 3 : 2;
+  out.assign((size_t)VPL * DM * TB, kNoEdgeS);
+  for (int k = 0; k < VPL; ++k)
+    for (int t = 0; t < TB; ++t) {
+      const int j = k * TB + t;
+      if (j >= g->n) continue;
+      const auto& rows = g->col_rows[j];
+      for (int d = 0; d < (int)rows.size(); ++d) {
+        const int i = rows[d];
+        const int32_t* b = g->col_idx.data() + g->row_ptr[i];
+        const int32_t* e = g->col_idx.data() + g->row_ptr[i + 1];
+        const int pos = (int)(std::lower_bound(b, e, (int32_t)j) - b);
+        const int chunk = (pos / nv) ^ ((i >> swz_shift) & swz_mask);
+        const int slot = nv + i * rw + chunk * nv + pos % nv;
+        out[((size_t)k * DM + d) * TB + t] = (uint32_t)(i + 1) | ((uint32_t)slot << 16);
+      }
+    }
+}
+
 int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_iter, int32_t bp_method,
                     double ms_scaling_factor, int32_t precision, int32_t vars_per_thread, int32_t min_col_slots,
                     qldpc_bp** out) {
@@ -238,55 +345,64 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
   QLDPC_HIP(hipSetDevice(g->device));
   auto* bp = new qldpc_bp();
   bp->g = g;
+  bp->engine = env_int("QLDPC_ENGINE", 2) == 1 ? 1 : 2;
   bp->max_iter = max_iter > 0 ? max_iter : g->n;
   bp->method = bp_method;
   bp->alpha = ms_scaling_factor;
   bp->precision = precision;
   bp->DMAX = std::max(g->max_col, (int)min_col_slots) <= 4 ? 4 : 8;
   bp->probs.assign(channel_probs, channel_probs + g->n);
-  int rc = choose_geometry(g->n, g->m, vars_per_thread, max_spill_free_vpl(precision, bp->DMAX), bp->TB, bp->VPL);
-  if (rc) {
+  auto fail = [&](int code) {
+    bp->vchk.release();
+    bp->llr.release();
     delete bp;
-    return rc;
-  }
-  const int TB = bp->TB, VPL = bp->VPL, D2 = bp->DMAX / 2;
-  std::vector<uint32_t> vchk((size_t)VPL * D2 * TB, 0xFFFFFFFFu);
-  for (int k = 0; k < VPL; ++k)
-    for (int t = 0; t < TB; ++t) {
-      const int j = k * TB + t;
-      if (j >= g->n) continue;
-      const auto& rows = g->col_rows[j];
-      for (int d = 0; d < bp->DMAX; ++d) {
-        const uint32_t v = d < (int)rows.size() ? (uint32_t)rows[d] : 0xFFFFu;
-        uint32_t& w = vchk[((size_t)k * D2 + d / 2) * TB + t];
-        w = (d & 1) ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
+    return code;
+  };
+  const int tsize = precision == 32 ? 4 : 8;
+  const int DM = bp->DMAX;
+  std::vector<uint32_t> vchk;
+  const void* kern = nullptr;
+  int rc;
+  if (bp->engine == 1) {
+    rc = choose_geometry(g->n, g->m, vars_per_thread, max_spill_free_vpl(precision, DM), bp->TB, bp->VPL);
+    if (rc) return fail(rc);
+    const int TB = bp->TB, VPL = bp->VPL, D2 = DM / 2;
+    vchk.assign((size_t)VPL * D2 * TB, 0xFFFFFFFFu);
+    for (int k = 0; k < VPL; ++k)
+      for (int t = 0; t < TB; ++t) {
+        const int j = k * TB + t;
+        if (j >= g->n) continue;
+        const auto& rows = g->col_rows[j];
+        for (int d = 0; d < DM; ++d) {
+          const uint32_t v = d < (int)rows.size() ? (uint32_t)rows[d] : 0xFFFFu;
+          uint32_t& w = vchk[((size_t)k * D2 + d / 2) * TB + t];
+          w = (d & 1) ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | v);
+        }
       }
-    }
-  if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)VPL * TB * (precision == 32 ? 4 : 8)))) {
-    delete bp;
-    return rc;
+    bp->lds_bytes = (int)lds_for(precision, g->m);
+    kern = get_variant(precision, bp->VPL, DM).dec_k;
+  } else {
+    rc = choose_sgeometry(g->n, g->m, vars_per_thread, precision, DM, bp->TB, bp->VPL);
+    if (rc) return fail(rc);
+    bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
+    const int vslots = (1 + g->m * bp->nch) * (16 / tsize);
+    if (vslots >= 0xFFFF) return fail(set_err(QLDPC_ENOTSUP, "V image exceeds 65535 message slots"));
+    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, vchk);
+    const int img = (int)slot_img_bytes(vslots, g->m, tsize);
+    bp->NS = choose_ns(img, precision, DM, bp->VPL);
+    bp->lds_bytes = (int)slot_lds_bytes(bp->NS, img, kChunkMax);
+    if (bp->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB (use precision 32)"));
+    kern = get_svariant(precision, bp->VPL, DM, bp->NS).dec_k;
   }
-  if (hipMemcpy(bp->vchk.p, vchk.data(), vchk.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-    delete bp;
-    return set_err(QLDPC_EHIP, "upload vchk");
-  }
-  if ((rc = upload_llr(bp))) {
-    delete bp;
-    return rc;
-  }
-  bp->lds_bytes = (int)lds_for(precision, g->m);
-  Variant v = get_variant(precision, VPL, bp->DMAX);
-  if (!v.dec) {
-    delete bp;
-    return set_err(QLDPC_ENOTSUP, "no kernel variant");
-  }
+  if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
+  if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)bp->VPL * bp->TB * tsize))) return fail(rc);
+  if (hipMemcpy(bp->vchk.p, vchk.data(), vchk.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(set_err(QLDPC_EHIP, "upload edge table"));
+  if ((rc = upload_llr(bp))) return fail(rc);
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, v.dec_k, TB, bp->lds_bytes) != hipSuccess) nb = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, bp->TB, bp->lds_bytes) != hipSuccess) nb = 1;
   bp->blocks_per_cu = std::max(1, nb);
-  if ((rc = device_cus(g->device, bp->cus))) {
-    delete bp;
-    return rc;
-  }
+  if ((rc = device_cus(g->device, bp->cus))) return fail(rc);
   *out = bp;
   return 0;
 }
@@ -328,22 +444,64 @@ static SectorDev sector_of(const qldpc_bp* bp, const unsigned long long* lmask, 
   return s;
 }
 
+static SSector ssector_of(const qldpc_bp* bp, const unsigned long long* lmask, int kw) {
+  SSector s;
+  s.edges = static_cast<const uint32_t*>(bp->vchk.p);
+  s.llr = bp->llr.p;
+  s.lmask = lmask;
+  s.m = bp->g->m;
+  s.n = bp->g->n;
+  s.kw = kw;
+  s.max_iter = bp->max_iter;
+  s.nch = bp->nch;
+  s.alpha = bp->alpha;
+  return s;
+}
+
+// Shots (or syndromes) per chunk of a slot kernel: enough chunks to give every
+// resident workgroup work, at most kChunkMax (the LDS fail bitmaps' size).
+static int chunk_for(long long count, long long grid, int ns) {
+  long long c = (count + grid - 1) / grid;
+  c = std::max<long long>(c, ns);
+  c = std::min<long long>(c, kChunkMax);
+  return (int)c;
+}
+
 int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, int32_t* d_iters, uint8_t* d_conv,
                           int64_t B, void* stream) {
   if (!bp || (B > 0 && (!d_synd || !d_corr))) return set_err(QLDPC_EINVAL, "NULL argument");
   if (B == 0) return 0;
   QLDPC_HIP(hipSetDevice(bp->g->device));
-  DecArgs a;
-  a.sec = sector_of(bp, nullptr, 0);
-  a.synd = d_synd;
-  a.corr = d_corr;
-  a.iters = d_iters;
-  a.conv = d_conv;
-  a.B = B;
-  Variant v = get_variant(bp->precision, bp->VPL, bp->DMAX);
   const long long cap = (long long)bp->blocks_per_cu * bp->cus;
-  const int grid = (int)std::max<long long>(1, std::min<long long>(B, cap));
-  QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
+  if (bp->engine == 1) {
+    DecArgs a;
+    a.sec = sector_of(bp, nullptr, 0);
+    a.synd = d_synd;
+    a.corr = d_corr;
+    a.iters = d_iters;
+    a.conv = d_conv;
+    a.B = B;
+    const int grid = (int)std::max<long long>(1, std::min<long long>(B, cap));
+    Variant v = get_variant(bp->precision, bp->VPL, bp->DMAX);
+    QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
+  } else {
+    const int tsize = bp->precision == 32 ? 4 : 8;
+    SDecArgs a;
+    a.sec = ssector_of(bp, nullptr, 0);
+    a.synd = d_synd;
+    a.corr = d_corr;
+    a.iters = d_iters;
+    a.conv = d_conv;
+    a.B = B;
+    a.mmax = bp->g->m;
+    a.vslots = (1 + bp->g->m * bp->nch) * (16 / tsize);
+    a.img_bytes = (int)slot_img_bytes(a.vslots, a.mmax, tsize);
+    a.chunk = chunk_for(B, cap, bp->NS);
+    const long long nchunks = (B + a.chunk - 1) / a.chunk;
+    const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
+    SVariant v = get_svariant(bp->precision, bp->VPL, bp->DMAX, bp->NS);
+    QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
+  }
   return 0;
 }
 
@@ -373,39 +531,50 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   if (dec_x && dec_z) {
     if (dec_x->g->n != dec_z->g->n) return set_err(QLDPC_EINVAL, "sector code lengths differ");
     if (dec_x->TB != dec_z->TB || dec_x->VPL != dec_z->VPL || dec_x->DMAX != dec_z->DMAX ||
-        dec_x->precision != dec_z->precision)
+        dec_x->precision != dec_z->precision || dec_x->engine != dec_z->engine)
       return set_err(QLDPC_EINVAL, "sector decoders need identical geometry/precision (same vars_per_thread)");
     if (dec_x->g->device != dec_z->g->device) return set_err(QLDPC_EINVAL, "sector decoders on different devices");
   }
   QLDPC_HIP(hipSetDevice(d0->g->device));
   auto* mc = new qldpc_mc();
+  auto fail = [&](int code) {
+    mc->lmask[0].release();
+    mc->lmask[1].release();
+    mc->counters.release();
+    delete mc;
+    return code;
+  };
   mc->dec[0] = dec_x;
   mc->dec[1] = dec_z;
   int rc = 0;
-  if (dec_x && (rc = build_lmask(logical_x, dec_x->g->n, mc->lmask[0], mc->kw[0]))) {
-    delete mc;
-    return rc;
-  }
-  if (dec_z && (rc = build_lmask(logical_z, dec_z->g->n, mc->lmask[1], mc->kw[1]))) {
-    mc->lmask[0].release();
-    delete mc;
-    return rc;
-  }
+  if (dec_x && (rc = build_lmask(logical_x, dec_x->g->n, mc->lmask[0], mc->kw[0]))) return fail(rc);
+  if (dec_z && (rc = build_lmask(logical_z, dec_z->g->n, mc->lmask[1], mc->kw[1]))) return fail(rc);
+  mc->engine = d0->engine;
   mc->TB = d0->TB;
   mc->VPL = d0->VPL;
   mc->DMAX = d0->DMAX;
   mc->precision = d0->precision;
-  int mmax = std::max(dec_x ? dec_x->g->m : 0, dec_z ? dec_z->g->m : 0);
-  mc->lds_bytes = (int)lds_for(mc->precision, mmax);
-  Variant v = get_variant(mc->precision, mc->VPL, mc->DMAX);
+  mc->mmax = std::max(dec_x ? dec_x->g->m : 0, dec_z ? dec_z->g->m : 0);
+  const void* kern;
+  if (mc->engine == 1) {
+    mc->lds_bytes = (int)lds_for(mc->precision, mc->mmax);
+    kern = get_variant(mc->precision, mc->VPL, mc->DMAX).mc_k;
+  } else {
+    const int tsize = mc->precision == 32 ? 4 : 8;
+    for (qldpc_bp* d : {dec_x, dec_z})
+      if (d) mc->vslots = std::max(mc->vslots, (1 + d->g->m * d->nch) * (16 / tsize));
+    mc->img_bytes = (int)slot_img_bytes(mc->vslots, mc->mmax, tsize);
+    mc->NS = choose_ns(mc->img_bytes, mc->precision, mc->DMAX, mc->VPL);
+    mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
+    kern = get_svariant(mc->precision, mc->VPL, mc->DMAX, mc->NS).mc_k;
+  }
+  if (mc->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB"));
+  if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, v.mc_k, mc->TB, mc->lds_bytes) != hipSuccess) nb = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, mc->TB, mc->lds_bytes) != hipSuccess) nb = 1;
   mc->blocks_per_cu = std::max(1, nb);
   mc->cus = d0->cus;
-  if ((rc = mc->counters.alloc(sizeof(qldpc_counters)))) {
-    delete mc;
-    return rc;
-  }
+  if ((rc = mc->counters.alloc(sizeof(qldpc_counters)))) return fail(rc);
   *out = mc;
   return 0;
 }
@@ -433,42 +602,65 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
   if (logical_mode < 0 || logical_mode > 2) return set_err(QLDPC_EINVAL, "logical_mode must be 0 (X), 1 (Z), 2 (Total)");
   if (!(px >= 0 && py >= 0 && pz >= 0)) return set_err(QLDPC_EINVAL, "negative Pauli probability");
   if (shot_count <= 0) return 0;
-  McArgs a;
-  std::memset(&a, 0, sizeof(a));
   const bool need[2] = {logical_mode != 1, logical_mode != 0};
-  a.nsec = 0;
   for (int q = 0; q < 2; ++q) {
     if (!need[q]) continue;
     if (!mc->dec[q]) return set_err(QLDPC_EINVAL, q == 0 ? "logical_mode needs the X sector (hz decoder)"
                                                           : "logical_mode needs the Z sector (hx decoder)");
     if (!mc->lmask[q].p) return set_err(QLDPC_EINVAL, "sector has no logical operators");
-    a.sec[a.nsec] = sector_of(mc->dec[q], static_cast<const unsigned long long*>(mc->lmask[q].p), mc->kw[q]);
-    a.sec_id[a.nsec] = q;
-    a.nsec++;
   }
-  a.logical_mode = logical_mode;
-  a.mmax = std::max(mc->dec[0] ? mc->dec[0]->g->m : 0, mc->dec[1] ? mc->dec[1]->g->m : 0);
-  a.t1 = pz;
-  a.t2 = pz + px;
-  a.t3 = (pz + px) + py;  // evaluation order of src/Simulators.py:108
-  a.K1 = ceil_2p53(a.t1);
-  a.K2 = ceil_2p53(a.t2);
-  a.K3 = ceil_2p53(a.t3);
-  a.seed = seed;
-  a.shot_begin = shot_begin;
-  a.shot_count = shot_count;
-  a.uniforms = d_uniforms;
-  a.counters = static_cast<unsigned long long*>(d_counters);
-  a.fail = d_fail;
-  a.err = d_err;
-  a.corr = d_corr;
-  a.iters = d_iters;
   QLDPC_HIP(hipSetDevice((mc->dec[0] ? mc->dec[0] : mc->dec[1])->g->device));
-  Variant v = get_variant(mc->precision, mc->VPL, mc->DMAX);
   const long long cap = (long long)mc->blocks_per_cu * mc->cus;
-  long long grid = grid_blocks > 0 ? grid_blocks : cap;
-  grid = std::max<long long>(1, std::min<long long>(grid, shot_count));
-  QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
+  // thresholds of the 3-way split, in the evaluation order of src/Simulators.py:102-108
+  const double t1 = pz, t2 = pz + px, t3 = (pz + px) + py;
+  if (mc->engine == 1) {
+    McArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (int q = 0; q < 2; ++q) {
+      if (!need[q]) continue;
+      a.sec[a.nsec] = sector_of(mc->dec[q], static_cast<const unsigned long long*>(mc->lmask[q].p), mc->kw[q]);
+      a.sec_id[a.nsec++] = q;
+    }
+    a.logical_mode = logical_mode;
+    a.mmax = mc->mmax;
+    a.t1 = t1; a.t2 = t2; a.t3 = t3;
+    a.K1 = ceil_2p53(t1); a.K2 = ceil_2p53(t2); a.K3 = ceil_2p53(t3);
+    a.seed = seed; a.shot_begin = shot_begin; a.shot_count = shot_count;
+    a.uniforms = d_uniforms;
+    a.counters = static_cast<unsigned long long*>(d_counters);
+    a.fail = d_fail; a.err = d_err; a.corr = d_corr; a.iters = d_iters;
+    long long grid = grid_blocks > 0 ? grid_blocks : cap;
+    grid = std::max<long long>(1, std::min<long long>(grid, shot_count));
+    Variant v = get_variant(mc->precision, mc->VPL, mc->DMAX);
+    QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
+  } else {
+    SMcArgs a;
+    std::memset(&a, 0, sizeof(a));
+    int ids[2] = {0, 0};
+    for (int q = 0; q < 2; ++q) {
+      if (!need[q]) continue;
+      a.sec[a.nsec] = ssector_of(mc->dec[q], static_cast<const unsigned long long*>(mc->lmask[q].p), mc->kw[q]);
+      ids[a.nsec++] = q;
+    }
+    a.sec_id0 = ids[0];
+    a.sec_id1 = ids[1];
+    a.logical_mode = logical_mode;
+    a.mmax = mc->mmax;
+    a.vslots = mc->vslots;
+    a.img_bytes = mc->img_bytes;
+    const long long want = grid_blocks > 0 ? grid_blocks : cap;
+    a.chunk = chunk_for(shot_count, want, mc->NS);
+    a.t1 = t1; a.t2 = t2; a.t3 = t3;
+    a.K1 = ceil_2p53(t1); a.K2 = ceil_2p53(t2); a.K3 = ceil_2p53(t3);
+    a.seed = seed; a.shot_begin = shot_begin; a.shot_count = shot_count;
+    a.uniforms = d_uniforms;
+    a.counters = static_cast<unsigned long long*>(d_counters);
+    a.fail = d_fail; a.err = d_err; a.corr = d_corr; a.iters = d_iters;
+    const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
+    const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
+    SVariant v = get_svariant(mc->precision, mc->VPL, mc->DMAX, mc->NS);
+    QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
+  }
   return 0;
 }
 

@@ -1,13 +1,18 @@
 // variants.h — launchable kernel variants (fp32/fp64 × vars-per-thread × max column degree).
 // Each kern_*.hip translation unit instantiates one (T, DMAX) family so the
 // build compiles them in parallel.
+//   v1 (bp_kernels.h): per-check LDS state updated by returning LDS atomics;
+//   v3 (bp_slot.h):    row-major v2c slots, check-centric gather, NS shots in
+//                      flight per workgroup (default engine).
 #pragma once
-#include "bp_kernels.h"
+#include "bp_slot.h"
 
 namespace qldpc {
 
 using DecLaunch = hipError_t (*)(dim3, dim3, size_t, hipStream_t, const DecArgs&);
 using McLaunch = hipError_t (*)(dim3, dim3, size_t, hipStream_t, const McArgs&);
+using SDecLaunch = hipError_t (*)(dim3, dim3, size_t, hipStream_t, const SDecArgs&);
+using SMcLaunch = hipError_t (*)(dim3, dim3, size_t, hipStream_t, const SMcArgs&);
 
 struct Variant {
   DecLaunch dec;
@@ -16,10 +21,21 @@ struct Variant {
   const void* mc_k;
 };
 
+struct SVariant {
+  SDecLaunch dec;
+  SMcLaunch mc;
+  const void* dec_k;
+  const void* mc_k;
+};
+
 Variant get_variant_f32_d4(int vpl);
 Variant get_variant_f32_d8(int vpl);
 Variant get_variant_f64_d4(int vpl);
 Variant get_variant_f64_d8(int vpl);
+SVariant get_svariant_f32_d4(int vpl, int ns);
+SVariant get_svariant_f32_d8(int vpl, int ns);
+SVariant get_svariant_f64_d4(int vpl, int ns);
+SVariant get_svariant_f64_d8(int vpl, int ns);
 
 #ifdef QLDPC_VARIANT_TU
 template <typename T, int VPL, int DMAX>
@@ -52,6 +68,42 @@ Variant pick_vpl(int vpl) {
     case 10: return make_variant<T, 10, DMAX>();
     case 12: return make_variant<T, 12, DMAX>();
     default: return Variant{nullptr, nullptr, nullptr, nullptr};
+  }
+}
+
+template <typename T, int VPL, int DMAX, int NS>
+hipError_t slaunch_dec(dim3 g, dim3 b, size_t lds, hipStream_t s, const SDecArgs& a) {
+  hipLaunchKernelGGL((sdec_kernel<T, VPL, DMAX, NS>), g, b, lds, s, a);
+  return hipGetLastError();
+}
+template <typename T, int VPL, int DMAX, int NS>
+hipError_t slaunch_mc(dim3 g, dim3 b, size_t lds, hipStream_t s, const SMcArgs& a) {
+  hipLaunchKernelGGL((smc_kernel<T, VPL, DMAX, NS>), g, b, lds, s, a);
+  return hipGetLastError();
+}
+template <typename T, int VPL, int DMAX, int NS>
+SVariant make_svariant() {
+  return SVariant{&slaunch_dec<T, VPL, DMAX, NS>, &slaunch_mc<T, VPL, DMAX, NS>,
+                  reinterpret_cast<const void*>(&sdec_kernel<T, VPL, DMAX, NS>),
+                  reinterpret_cast<const void*>(&smc_kernel<T, VPL, DMAX, NS>)};
+}
+template <typename T, int DMAX, int NS>
+SVariant pick_svpl_ns(int vpl) {
+  switch (vpl) {
+    case 1: return make_svariant<T, 1, DMAX, NS>();
+    case 2: return make_svariant<T, 2, DMAX, NS>();
+    case 3: return make_svariant<T, 3, DMAX, NS>();
+    case 4: return make_svariant<T, 4, DMAX, NS>();
+    default: return SVariant{nullptr, nullptr, nullptr, nullptr};
+  }
+}
+template <typename T, int DMAX>
+SVariant pick_svpl(int vpl, int ns) {
+  switch (ns) {
+    case 1: return pick_svpl_ns<T, DMAX, 1>(vpl);
+    case 2: return pick_svpl_ns<T, DMAX, 2>(vpl);
+    case 4: return pick_svpl_ns<T, DMAX, 4>(vpl);
+    default: return SVariant{nullptr, nullptr, nullptr, nullptr};
   }
 }
 #endif
