@@ -1,34 +1,40 @@
-// bp_slot.h — v3 CDNA4 (gfx950) BP engine: NS shots in flight per workgroup.
+// bp_slot.h — CDNA4 (gfx950) BP engine: small workgroups, NS decodes in flight each.
 //
-// Each workgroup owns NS "slots"; a slot holds one decode's LDS image
-//   V [m][RW]  v2c messages in row-major slot order (row = check, its edges in
+// A workgroup of TB threads (default 256-320) owns NS "slots"; a slot holds one
+// decode's LDS image
+//   V [1+m·RW] v2c messages in row-major slot order (row = check, its edges in
 //              ascending column order, 16-byte chunks XOR-swizzled so a wave's
-//              row reads are bank-conflict free), padding = min-sum sentinel;
-//   CS[m]      compressed check state {m1 | parity<<sign, m2};
-//   F [m]      bit0 = (H x)_i accumulator, bit1 = syndrome staging;
+//              row reads are bank-conflict free), padding = min-sum sentinel,
+//              the first 16 bytes a write sink for missing edges;
+//   CS[1+m]    compressed check state {m1 | parity<<sign, m2}, CS[0] = {0,0};
+//   F [1+m]    bit0 = (H x)_i accumulator, bit1 = syndrome staging, F[0] sink;
 //   lred[8]    logical syndrome of the finished residual; flags[2] block-OR.
-// All slots advance in lock-step phases separated by ONE workgroup barrier each
-// (variable phase | check phase), but every slot has its own shot and its own
-// iteration counter: a slot whose decode converged (or hit max_iter) is
-// finalised and refilled with the next shot at the next round, so early exit
-// wastes nothing and the two barriers of an iteration are paid once per NS
-// decodes.  Messages are stored "canonical": magnitude bits with the sign bit
-// replaced by ldpc's (v2c <= 0) predicate, so the check phase gets the parity
-// from the sign bits directly and the variable phase finds each edge's previous
-// v2c, which the variable phase re-reads from its own slot (no per-slot
-// registers besides three bit masks, so NS costs LDS, not VGPRs).  Arithmetic is ldpc's, operation for operation (see
-// DESIGN.md §Kernels and oracle/qldpc_oracle.c), hence bit-exact.
+// A thread owns variables j = k·TB + tid (k < VPL, a RUNTIME count) and checks
+// i = q·TB + tid.  The variable phase streams each variable's edge words and
+// prior from global memory (L1-resident: one sector's table is n·DMAX·4 bytes,
+// prefetched one variable ahead), gathers CS and its own previous v2c from LDS,
+// applies ldpc's arithmetic and scatters the new v2c; registers no longer grow
+// with VPL, so several workgroups (independent barrier domains) share a CU and
+// one's LDS phase overlaps another's VALU phase.
+// All slots of a workgroup advance in lock-step phases separated by ONE barrier
+// each, but every slot has its own shot and iteration counter: a converged (or
+// max_iter) decode is finalised and its slot refilled at the next round.
+// Messages are stored "canonical": magnitude bits with the sign bit replaced by
+// ldpc's (v2c <= 0) predicate, so the check phase reads the parity from sign bits
+// and the variable phase recovers its own previous v2c from its slot.
+// Arithmetic is ldpc's, operation for operation (DESIGN.md §Kernels,
+// oracle/qldpc_oracle.c), hence bit-exact.
 #pragma once
 #include "bp_kernels.h"
 
 namespace qldpc {
 
 constexpr int kMaxThreadsS = 1024;
-// Edge word: (check + 1) in bits 0-15 | V slot in bits 16-31.  Entry 0 of CS and
-// F and the first 16 bytes of V are per-image dummies: a missing edge (column
-// degree < DMAX) is the word 0, so it gathers CS[0] = {0, 0} (its c2v is ±0,
-// which leaves every ldpc sum unchanged), writes its v2c into the V sink and
-// xors into F[0].  No branch on edge validity remains in the hot loops.
+constexpr int kMaxVplS = 32;  // variables per thread (bit masks are 32-bit)
+// Edge word: (check + 1) in bits 0-15 | V slot in bits 16-31.  A missing edge
+// (column degree < DMAX) is the word 0: it gathers CS[0] = {0, 0} (its c2v is
+// ±0, which leaves every ldpc sum unchanged), writes its v2c into the V sink
+// and xors into F[0].  No branch on edge validity remains in the hot loops.
 constexpr uint32_t kNoEdgeS = 0u;
 __device__ inline uint32_t echk(uint32_t e) { return e & 0xFFFFu; }
 __device__ inline uint32_t eslot(uint32_t e) { return e >> 16; }
@@ -37,7 +43,7 @@ struct SSector {
   const uint32_t* edges;            // [VPL][DMAX][TB]
   const void* llr;                  // T [VPL][TB]
   const unsigned long long* lmask;  // [n][kw] logical-row masks per column (MC only)
-  int m, n, kw, max_iter, nch;      // nch = 16-byte chunks per row
+  int m, n, kw, max_iter, nch, vpl; // nch = 16-byte chunks per row; vpl = variables per thread
   double alpha;                     // 0 => 1 - 2^-iter
 };
 
@@ -117,21 +123,6 @@ __device__ inline Img<T> slot_img(unsigned char* smem, int q, int img_bytes, int
   return I;
 }
 
-template <typename T, int VPL, int DMAX>
-struct SEdges {
-  uint32_t ed[VPL][DMAX];
-  T L[VPL];
-  __device__ inline void load(const SSector& S, int tid, int TB) {
-    const T* llr = static_cast<const T*>(S.llr);
-#pragma unroll
-    for (int k = 0; k < VPL; ++k) {
-      L[k] = llr[k * TB + tid];
-#pragma unroll
-      for (int t = 0; t < DMAX; ++t) ed[k][t] = S.edges[(k * DMAX + t) * TB + tid];
-    }
-  }
-};
-
 // canonical message bits: |v| with sign bit := (v <= 0)  (ldpc's sign test)
 template <typename T>
 __device__ inline typename FT<T>::U canon(T v) {
@@ -139,48 +130,65 @@ __device__ inline typename FT<T>::U canon(T v) {
   return (FT<T>::bits(v) & ~FT<T>::kSign) | ((v <= (T)0) ? FT<T>::kSign : (U)0);
 }
 
+template <int DMAX>
+__device__ inline void load_edges(const SSector& S, int k, int tid, int TB, uint32_t (&e)[DMAX]) {
+#pragma unroll
+  for (int t = 0; t < DMAX; ++t) e[t] = S.edges[(k * DMAX + t) * TB + tid];
+}
+
 // v2c = prior on every edge (ldpc's first check update reads the channel LLRs).
-template <typename T, int VPL, int DMAX>
-__device__ inline void s_priors(const SEdges<T, VPL, DMAX>& E, T* V) {
+template <typename T, int DMAX>
+__device__ inline void s_priors(const SSector& S, T* V, int tid, int TB) {
+  const T* llr = static_cast<const T*>(S.llr);
+  for (int k = 0; k < S.vpl; ++k) {
+    uint32_t e[DMAX];
+    load_edges<DMAX>(S, k, tid, TB, e);
+    const T c = FT<T>::val(canon<T>(llr[k * TB + tid]));
 #pragma unroll
-  for (int k = 0; k < VPL; ++k) {
-    const T c = FT<T>::val(canon<T>(E.L[k]));
-#pragma unroll
-    for (int t = 0; t < DMAX; ++t) V[eslot(E.ed[k][t])] = c;
+    for (int t = 0; t < DMAX; ++t) V[eslot(e[t])] = c;
   }
 }
 
 // Variable phase of one flooding iteration for one slot.  Returns decision bits.
-template <typename T, int VPL, int DMAX>
-__device__ inline uint32_t s_var(const SEdges<T, VPL, DMAX>& E, const Img<T>& I, T alpha, int tid, int TB, int n) {
+template <typename T, int DMAX>
+__device__ inline uint32_t s_var(const SSector& S, const Img<T>& I, T alpha, int tid, int TB) {
   using U = typename FT<T>::U;
   constexpr U kS = FT<T>::kSign;
-  // issue every gather first: check states and this edge's own previous v2c
-  Pair<T> pr[VPL][DMAX];
-  U ov[VPL][DMAX];
+  const T* llr = static_cast<const T*>(S.llr);
+  const int n = S.n, vpl = S.vpl;
+  uint32_t xbits = 0;
+  uint32_t en[DMAX];
+  load_edges<DMAX>(S, 0, tid, TB, en);
+  T Ln = llr[tid];
+  for (int k = 0; k < vpl; ++k) {
+    uint32_t e[DMAX];
 #pragma unroll
-  for (int k = 0; k < VPL; ++k)
+    for (int t = 0; t < DMAX; ++t) e[t] = en[t];
+    const T L = Ln;
+    if (k + 1 < vpl) {  // next variable's edge words / prior stream in under this one's work
+      load_edges<DMAX>(S, k + 1, tid, TB, en);
+      Ln = llr[(k + 1) * TB + tid];
+    }
+    Pair<T> pr[DMAX];
+    U ov[DMAX];
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
-      pr[k][t] = I.CS[echk(E.ed[k][t])];
-      ov[k][t] = FT<T>::bits(I.V[eslot(E.ed[k][t])]);
+      pr[t] = I.CS[echk(e[t])];
+      ov[t] = FT<T>::bits(I.V[eslot(e[t])]);
     }
-  uint32_t xbits = 0;
-#pragma unroll
-  for (int k = 0; k < VPL; ++k) {
     T c[DMAX];
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
-      const U a = pr[k][t].a;
+      const U a = pr[t].a;
       const U m1 = a & ~kS;
       // min over the OTHER edges of the check: m2 if this edge holds m1, else m1
-      const U sel = ((ov[k][t] & ~kS) == m1) ? pr[k][t].b : m1;
+      const U sel = ((ov[t] & ~kS) == m1) ? pr[t].b : m1;
       // c2v = sel * (±alpha): x*(-a) == -(x*a) exactly, so flip the product's sign bit
-      const U cb = FT<T>::bits(FT<T>::val(sel) * alpha) ^ ((a ^ ov[k][t]) & kS);
-      c[t] = FT<T>::val(cb);
+      c[t] = FT<T>::val(FT<T>::bits(FT<T>::val(sel) * alpha) ^ ((a ^ ov[t]) & kS));
     }
+    // ldpc column pass (rows ascending): forward partial sums from the prior
     T f[DMAX];
-    T acc = E.L[k];
+    T acc = L;
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
       f[t] = acc;
@@ -191,11 +199,10 @@ __device__ inline uint32_t s_var(const SEdges<T, VPL, DMAX>& E, const Img<T>& I,
     T b = (T)0;
 #pragma unroll
     for (int t = DMAX - 1; t >= 0; --t) {
-      const uint32_t e = E.ed[k][t];
       const T v = f[t] + b;
       b = b + c[t];
-      I.V[eslot(e)] = FT<T>::val(canon<T>(v));
-      if (x) atomicXor(&I.F[echk(e)], 1u);
+      I.V[eslot(e[t])] = FT<T>::val(canon<T>(v));
+      if (x) atomicXor(&I.F[echk(e[t])], 1u);
     }
   }
   return xbits;
@@ -267,13 +274,11 @@ __device__ inline int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 // One sector pass over `cn` shots (chunk-relative 0..cn-1) with NS slots.
 // MC: shots are sampled (Philox / external u) and checked against the logicals;
 // DEC: syndromes come from D->synd and corrections/iters/conv are written.
-template <typename T, int VPL, int DMAX, int NS, bool MC>
+template <typename T, int DMAX, int NS, bool MC>
 __device__ void s_pass(const SSector& S, int q, long long c0, int cn, unsigned char* smem, int img_bytes, int vslots,
                        int mmax, uint32_t* failmap, unsigned long long* cnt, const SMcArgs* A, const SDecArgs* D,
                        int tid, int TB) {
-  const int m = S.m, n = S.n, nch = S.nch;
-  SEdges<T, VPL, DMAX> E;
-  E.load(S, tid, TB);
+  const int m = S.m, n = S.n, nch = S.nch, vpl = S.vpl;
   for (int s = 0; s < NS; ++s) s_fill<T>(slot_img<T>(smem, s, img_bytes, vslots, mmax), vslots, mmax, tid, TB);
   __syncthreads();
 
@@ -308,15 +313,14 @@ __device__ void s_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       if (shot[s] < 0) continue;
       const Img<T> I = slot_img<T>(smem, s, img_bytes, vslots, mmax);
       if (it[s] == 0) {
-        s_priors<T, VPL, DMAX>(E, I.V);
+        s_priors<T, DMAX>(S, I.V, tid, TB);
         sb[s] = 0;
         if (MC) {
           // sample this shot's Pauli error (src/Simulators.py:99-113); stage s = H e in F bit1
           const long long sl = c0 + shot[s];
           const unsigned long long gshot = A->shot_begin + (unsigned long long)sl;
           uint32_t ebits = 0;
-#pragma unroll
-          for (int k = 0; k < VPL; ++k) {
+          for (int k = 0; k < vpl; ++k) {
             const int j = k * TB + tid;
             if (j < n) {
               uint32_t cls;
@@ -331,8 +335,10 @@ __device__ void s_pass(const SSector& S, int q, long long c0, int cn, unsigned c
               ebits |= e << k;
               if (A->err && q == A->sec_id0) A->err[sl * (long long)n + j] = (uint8_t)cls;
               if (e) {
+                uint32_t ed[DMAX];
+                load_edges<DMAX>(S, k, tid, TB, ed);
 #pragma unroll
-                for (int t = 0; t < DMAX; ++t) atomicXor(&I.F[echk(E.ed[k][t])], 2u);
+                for (int t = 0; t < DMAX; ++t) atomicXor(&I.F[echk(ed[t])], 2u);
               }
             }
           }
@@ -343,7 +349,7 @@ __device__ void s_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         }
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it[s])) : alpha_fixed;
-        xb[s] = s_var<T, VPL, DMAX>(E, I, alpha, tid, TB, n);
+        xb[s] = s_var<T, DMAX>(S, I, alpha, tid, TB);
       }
     }
     __syncthreads();
@@ -411,8 +417,7 @@ __device__ void s_pass(const SSector& S, int q, long long c0, int cn, unsigned c
           const uint32_t r = eb[s] ^ xb[s];
           if (r) {
             unsigned long long acc[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < VPL; ++k) {
+            for (int k = 0; k < vpl; ++k) {
               if ((r >> k) & 1u) {
                 const int j = k * TB + tid;
 #pragma unroll
@@ -427,15 +432,13 @@ __device__ void s_pass(const SSector& S, int q, long long c0, int cn, unsigned c
             }
           }
           if (A->corr) {
-#pragma unroll
-            for (int k = 0; k < VPL; ++k) {
+            for (int k = 0; k < vpl; ++k) {
               const int j = k * TB + tid;
               if (j < n) A->corr[(sl * 2 + q) * (long long)n + j] = (uint8_t)((xb[s] >> k) & 1u);
             }
           }
         } else {
-#pragma unroll
-          for (int k = 0; k < VPL; ++k) {
+          for (int k = 0; k < vpl; ++k) {
             const int j = k * TB + tid;
             if (j < n) D->corr[sl * (long long)n + j] = (uint8_t)((xb[s] >> k) & 1u);
           }
@@ -463,11 +466,12 @@ __device__ inline SSector pick_ssector(const SMcArgs& A, int qi) {
   S.kw = b ? A.sec[1].kw : A.sec[0].kw;
   S.max_iter = b ? A.sec[1].max_iter : A.sec[0].max_iter;
   S.nch = b ? A.sec[1].nch : A.sec[0].nch;
+  S.vpl = b ? A.sec[1].vpl : A.sec[0].vpl;
   S.alpha = b ? A.sec[1].alpha : A.sec[0].alpha;
   return S;
 }
 
-template <typename T, int VPL, int DMAX, int NS>
+template <typename T, int DMAX, int NS>
 __global__ __launch_bounds__(kMaxThreadsS) void smc_kernel(SMcArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
@@ -489,8 +493,8 @@ __global__ __launch_bounds__(kMaxThreadsS) void smc_kernel(SMcArgs A) {
     for (int qi = 0; qi < A.nsec; ++qi) {
       const SSector S = pick_ssector(A, qi);
       const int q = qi == 0 ? A.sec_id0 : A.sec_id1;
-      s_pass<T, VPL, DMAX, NS, true>(S, q, c0, cn, smem, A.img_bytes, A.vslots, A.mmax, q == 0 ? fm0 : fm1, cnt, &A,
-                                     nullptr, tid, TB);
+      s_pass<T, DMAX, NS, true>(S, q, c0, cn, smem, A.img_bytes, A.vslots, A.mmax, q == 0 ? fm0 : fm1, cnt, &A,
+                                nullptr, tid, TB);
     }
     // combine the sectors per shot (eval_logical_type, src/Simulators.py:162-168)
     unsigned long long nf = 0;
@@ -508,7 +512,7 @@ __global__ __launch_bounds__(kMaxThreadsS) void smc_kernel(SMcArgs A) {
   if (tid < kCntHist && cnt[tid]) atomicAdd(&A.counters[tid], cnt[tid]);
 }
 
-template <typename T, int VPL, int DMAX, int NS>
+template <typename T, int DMAX, int NS>
 __global__ __launch_bounds__(kMaxThreadsS) void sdec_kernel(SDecArgs D) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
@@ -517,8 +521,8 @@ __global__ __launch_bounds__(kMaxThreadsS) void sdec_kernel(SDecArgs D) {
   for (long long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const long long c0 = ch * CH;
     const int cn = (int)(D.B - c0 < CH ? D.B - c0 : CH);
-    s_pass<T, VPL, DMAX, NS, false>(D.sec, 0, c0, cn, smem, D.img_bytes, D.vslots, D.mmax, nullptr, nullptr, nullptr,
-                                    &D, tid, TB);
+    s_pass<T, DMAX, NS, false>(D.sec, 0, c0, cn, smem, D.img_bytes, D.vslots, D.mmax, nullptr, nullptr, nullptr, &D,
+                               tid, TB);
   }
 }
 

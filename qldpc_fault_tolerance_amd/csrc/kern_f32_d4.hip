@@ -1,8 +1,8 @@
-// kern_f32_d4.hip — float kernels, max column degree 4 (v1 atomic and v3 slot families).
+// kern_f32_d4.hip — float kernels, max column degree 4 (v1 atomic and v4 slot families).
 #define QLDPC_VARIANT_TU 1
 #include "variants.h"
 
 namespace qldpc {
 Variant get_variant_f32_d4(int vpl) { return pick_vpl<float, 4>(vpl); }
-SVariant get_svariant_f32_d4(int vpl, int ns) { return pick_svpl<float, 4>(vpl, ns); }
+SVariant get_svariant_f32_d4(int ns) { return pick_sns<float, 4>(ns); }
 }  // namespace qldpc

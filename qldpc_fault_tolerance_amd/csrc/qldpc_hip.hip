@@ -2,8 +2,9 @@
 //
 // Graph/decoder/MC handles own their device buffers; launches take a caller
 // stream.  Two kernel engines are built:
-//   engine 2 (default) — bp_slot.h: NS decodes in flight per workgroup,
-//                        row-major v2c slots, check-centric gather;
+//   engine 2 (default) — bp_slot.h: small workgroups with streamed variables,
+//                        row-major v2c slots, check-centric gather, NS decodes
+//                        in flight per workgroup;
 //   engine 1           — bp_kernels.h: per-check LDS state updated by
 //                        returning LDS atomics (kept for A/B measurements,
 //                        selected with QLDPC_ENGINE=1).
@@ -58,7 +59,6 @@ struct DevBuf {
 };
 
 const int kVplSet[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12};
-const int kSVplSet[] = {1, 2, 3, 4};
 constexpr int kLdsMax = 160 * 1024;
 constexpr int kChunkMax = 1024;
 
@@ -105,9 +105,9 @@ Variant get_variant(int precision, int vpl, int dmax) {
   return dmax == 4 ? get_variant_f64_d4(vpl) : get_variant_f64_d8(vpl);
 }
 
-SVariant get_svariant(int precision, int vpl, int dmax, int ns) {
-  if (precision == 32) return dmax == 4 ? get_svariant_f32_d4(vpl, ns) : get_svariant_f32_d8(vpl, ns);
-  return dmax == 4 ? get_svariant_f64_d4(vpl, ns) : get_svariant_f64_d8(vpl, ns);
+SVariant get_svariant(int precision, int dmax, int ns) {
+  if (precision == 32) return dmax == 4 ? get_svariant_f32_d4(ns) : get_svariant_f32_d8(ns);
+  return dmax == 4 ? get_svariant_f64_d4(ns) : get_svariant_f64_d8(ns);
 }
 
 int round_up(int x, int a) { return (x + a - 1) / a * a; }
@@ -152,61 +152,44 @@ size_t lds_for(int precision, int mmax) {
   return pair * 2 * (size_t)mmax + 4 * 2 * (size_t)mmax + 64;
 }
 
-// ---- engine 2 geometry: VPL in {1..4}, TB <= 1024, NS slots.
-// Largest VPL whose slot kernels compile without scratch at NS slots (gfx950,
-// tools/kres.sh).  Fewer variables per thread = more threads per shot.
-int smax_vpl(int precision, int dmax, int ns) {
-  if (dmax == 8) return 1;
-  if (ns == 4) return 1;
-  return 2;
-}
-
-int choose_sgeometry(int n, int m, int requested_vpl, int precision, int dmax, int& TB, int& VPL) {
+// ---- engine 2 geometry: threads per shot TB (multiple of 64, 64..1024) and a
+// runtime count of variables per thread VPL = ceil(n / TB) <= 32.  Default TB:
+// the least padding waste with TB in [192, 512] (several workgroups per CU);
+// QLDPC_TB or vars_per_thread override it.
+int choose_sgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
+  const int forced_tb = env_int("QLDPC_TB", 0);
   if (requested_vpl > 0) {
-    bool ok = false;
-    for (int v : kSVplSet) ok |= (v == requested_vpl);
-    if (!ok) return set_err(QLDPC_EINVAL, "vars_per_thread must be one of 1-4 (engine 2)");
     VPL = requested_vpl;
     TB = round_up((n + VPL - 1) / VPL, 64);
-    if (TB > kMaxThreadsS) return set_err(QLDPC_EINVAL, "vars_per_thread too small for this graph (>1024 threads)");
+  } else if (forced_tb > 0) {
+    TB = round_up(forced_tb, 64);
+    VPL = (n + TB - 1) / TB;
   } else {
-    VPL = 0;
-    const int vmax = smax_vpl(precision, dmax, 1);
-    for (int v : {2, 1}) {  // measured order on n225/n1600, spill-free first
-      const int tb = round_up((n + v - 1) / v, 64);
-      if (v <= vmax && tb <= kMaxThreadsS) {
-        VPL = v;
+    int best = 1 << 30;
+    TB = 0;
+    for (int tb = 192; tb <= 512; tb += 64) {
+      const int v = (n + tb - 1) / tb;
+      const int waste = v * tb - n;
+      if (v <= kMaxVplS && waste < best) {
+        best = waste;
         TB = tb;
-        break;
       }
     }
-    if (!VPL) {
-      for (int v : kSVplSet) {
-        const int tb = round_up((n + v - 1) / v, 64);
-        if (tb <= kMaxThreadsS) {
-          VPL = v;
-          TB = tb;
-          break;
-        }
-      }
-    }
-    if (!VPL) return set_err(QLDPC_ENOTSUP, "graph too large for one workgroup per shot (n > 4096)");
+    if (!TB) TB = std::min(kMaxThreadsS, round_up((n + kMaxVplS - 1) / kMaxVplS, 64));
+    VPL = (n + TB - 1) / TB;
   }
+  if (TB > kMaxThreadsS || TB < 64) return set_err(QLDPC_EINVAL, "threads per shot out of range (64..1024)");
+  if (VPL > kMaxVplS) return set_err(QLDPC_ENOTSUP, "more than 32 variables per thread (n > 32768)");
   if ((m + TB - 1) / TB > 32) return set_err(QLDPC_ENOTSUP, "too many checks per thread (m > 32*threads)");
   return 0;
 }
 
-// Slots per workgroup: env QLDPC_NS, else the most that fit LDS and stay
-// spill-free at this VPL.
-int choose_ns(int img, int precision, int dmax, int vpl) {
-  const int forced = env_int("QLDPC_NS", 0);
-  if (forced == 1 || forced == 2 || forced == 4) {
-    return slot_lds_bytes(forced, img, kChunkMax) <= (size_t)kLdsMax ? forced : 1;
-  }
-  int best = 1;
-  for (int ns : {2, 4})
-    if (slot_lds_bytes(ns, img, kChunkMax) <= (size_t)kLdsMax && vpl <= smax_vpl(precision, dmax, ns)) best = ns;
-  return best;
+// Slots per workgroup: QLDPC_NS, else 1 (independent workgroups interleave
+// better than lock-stepped slots).
+int choose_ns(int img) {
+  const int forced = env_int("QLDPC_NS", 1);
+  const int ns = (forced == 2 || forced == 4) ? forced : 1;
+  return slot_lds_bytes(ns, img, kChunkMax) <= (size_t)kLdsMax ? ns : 1;
 }
 
 int device_cus(int dev, int& cus) {
@@ -382,17 +365,17 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
     bp->lds_bytes = (int)lds_for(precision, g->m);
     kern = get_variant(precision, bp->VPL, DM).dec_k;
   } else {
-    rc = choose_sgeometry(g->n, g->m, vars_per_thread, precision, DM, bp->TB, bp->VPL);
+    rc = choose_sgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL);
     if (rc) return fail(rc);
     bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
     const int vslots = (1 + g->m * bp->nch) * (16 / tsize);
     if (vslots >= 0xFFFF) return fail(set_err(QLDPC_ENOTSUP, "V image exceeds 65535 message slots"));
     build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, vchk);
     const int img = (int)slot_img_bytes(vslots, g->m, tsize);
-    bp->NS = choose_ns(img, precision, DM, bp->VPL);
+    bp->NS = choose_ns(img);
     bp->lds_bytes = (int)slot_lds_bytes(bp->NS, img, kChunkMax);
     if (bp->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB (use precision 32)"));
-    kern = get_svariant(precision, bp->VPL, DM, bp->NS).dec_k;
+    kern = get_svariant(precision, DM, bp->NS).dec_k;
   }
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
   if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)bp->VPL * bp->TB * tsize))) return fail(rc);
@@ -454,6 +437,7 @@ static SSector ssector_of(const qldpc_bp* bp, const unsigned long long* lmask, i
   s.kw = kw;
   s.max_iter = bp->max_iter;
   s.nch = bp->nch;
+  s.vpl = bp->VPL;
   s.alpha = bp->alpha;
   return s;
 }
@@ -499,7 +483,7 @@ int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, 
     a.chunk = chunk_for(B, cap, bp->NS);
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
-    SVariant v = get_svariant(bp->precision, bp->VPL, bp->DMAX, bp->NS);
+    SVariant v = get_svariant(bp->precision, bp->DMAX, bp->NS);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;
@@ -564,9 +548,9 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
     for (qldpc_bp* d : {dec_x, dec_z})
       if (d) mc->vslots = std::max(mc->vslots, (1 + d->g->m * d->nch) * (16 / tsize));
     mc->img_bytes = (int)slot_img_bytes(mc->vslots, mc->mmax, tsize);
-    mc->NS = choose_ns(mc->img_bytes, mc->precision, mc->DMAX, mc->VPL);
+    mc->NS = choose_ns(mc->img_bytes);
     mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
-    kern = get_svariant(mc->precision, mc->VPL, mc->DMAX, mc->NS).mc_k;
+    kern = get_svariant(mc->precision, mc->DMAX, mc->NS).mc_k;
   }
   if (mc->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB"));
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
@@ -658,7 +642,7 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.fail = d_fail; a.err = d_err; a.corr = d_corr; a.iters = d_iters;
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
-    SVariant v = get_svariant(mc->precision, mc->VPL, mc->DMAX, mc->NS);
+    SVariant v = get_svariant(mc->precision, mc->DMAX, mc->NS);
     QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;

@@ -2,8 +2,8 @@
 // Each kern_*.hip translation unit instantiates one (T, DMAX) family so the
 // build compiles them in parallel.
 //   v1 (bp_kernels.h): per-check LDS state updated by returning LDS atomics;
-//   v3 (bp_slot.h):    row-major v2c slots, check-centric gather, NS shots in
-//                      flight per workgroup (default engine).
+//   v4 (bp_slot.h):    row-major v2c slots, check-centric gather, streamed
+//                      variables, NS shots in flight per workgroup (default).
 #pragma once
 #include "bp_slot.h"
 
@@ -32,10 +32,10 @@ Variant get_variant_f32_d4(int vpl);
 Variant get_variant_f32_d8(int vpl);
 Variant get_variant_f64_d4(int vpl);
 Variant get_variant_f64_d8(int vpl);
-SVariant get_svariant_f32_d4(int vpl, int ns);
-SVariant get_svariant_f32_d8(int vpl, int ns);
-SVariant get_svariant_f64_d4(int vpl, int ns);
-SVariant get_svariant_f64_d8(int vpl, int ns);
+SVariant get_svariant_f32_d4(int ns);
+SVariant get_svariant_f32_d8(int ns);
+SVariant get_svariant_f64_d4(int ns);
+SVariant get_svariant_f64_d8(int ns);
 
 #ifdef QLDPC_VARIANT_TU
 template <typename T, int VPL, int DMAX>
@@ -71,38 +71,28 @@ Variant pick_vpl(int vpl) {
   }
 }
 
-template <typename T, int VPL, int DMAX, int NS>
+template <typename T, int DMAX, int NS>
 hipError_t slaunch_dec(dim3 g, dim3 b, size_t lds, hipStream_t s, const SDecArgs& a) {
-  hipLaunchKernelGGL((sdec_kernel<T, VPL, DMAX, NS>), g, b, lds, s, a);
+  hipLaunchKernelGGL((sdec_kernel<T, DMAX, NS>), g, b, lds, s, a);
   return hipGetLastError();
-}
-template <typename T, int VPL, int DMAX, int NS>
-hipError_t slaunch_mc(dim3 g, dim3 b, size_t lds, hipStream_t s, const SMcArgs& a) {
-  hipLaunchKernelGGL((smc_kernel<T, VPL, DMAX, NS>), g, b, lds, s, a);
-  return hipGetLastError();
-}
-template <typename T, int VPL, int DMAX, int NS>
-SVariant make_svariant() {
-  return SVariant{&slaunch_dec<T, VPL, DMAX, NS>, &slaunch_mc<T, VPL, DMAX, NS>,
-                  reinterpret_cast<const void*>(&sdec_kernel<T, VPL, DMAX, NS>),
-                  reinterpret_cast<const void*>(&smc_kernel<T, VPL, DMAX, NS>)};
 }
 template <typename T, int DMAX, int NS>
-SVariant pick_svpl_ns(int vpl) {
-  switch (vpl) {
-    case 1: return make_svariant<T, 1, DMAX, NS>();
-    case 2: return make_svariant<T, 2, DMAX, NS>();
-    case 3: return make_svariant<T, 3, DMAX, NS>();
-    case 4: return make_svariant<T, 4, DMAX, NS>();
-    default: return SVariant{nullptr, nullptr, nullptr, nullptr};
-  }
+hipError_t slaunch_mc(dim3 g, dim3 b, size_t lds, hipStream_t s, const SMcArgs& a) {
+  hipLaunchKernelGGL((smc_kernel<T, DMAX, NS>), g, b, lds, s, a);
+  return hipGetLastError();
+}
+template <typename T, int DMAX, int NS>
+SVariant make_svariant() {
+  return SVariant{&slaunch_dec<T, DMAX, NS>, &slaunch_mc<T, DMAX, NS>,
+                  reinterpret_cast<const void*>(&sdec_kernel<T, DMAX, NS>),
+                  reinterpret_cast<const void*>(&smc_kernel<T, DMAX, NS>)};
 }
 template <typename T, int DMAX>
-SVariant pick_svpl(int vpl, int ns) {
+SVariant pick_sns(int ns) {
   switch (ns) {
-    case 1: return pick_svpl_ns<T, DMAX, 1>(vpl);
-    case 2: return pick_svpl_ns<T, DMAX, 2>(vpl);
-    case 4: return pick_svpl_ns<T, DMAX, 4>(vpl);
+    case 1: return make_svariant<T, DMAX, 1>();
+    case 2: return make_svariant<T, DMAX, 2>();
+    case 4: return make_svariant<T, DMAX, 4>();
     default: return SVariant{nullptr, nullptr, nullptr, nullptr};
   }
 }
