@@ -153,9 +153,8 @@ size_t lds_for(int precision, int mmax) {
 }
 
 // ---- engine 2 geometry: threads per shot TB (multiple of 64, 64..1024) and a
-// runtime count of variables per thread VPL = ceil(n / TB) <= 32.  Default TB:
-// the least padding waste with TB in [192, 512] (several workgroups per CU);
-// QLDPC_TB or vars_per_thread override it.
+// runtime count of variables per thread VPL = ceil(n / TB) <= 32.  Default TB
+// 256; QLDPC_TB or vars_per_thread override it.
 int choose_sgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
   const int forced_tb = env_int("QLDPC_TB", 0);
   if (requested_vpl > 0) {
@@ -165,18 +164,14 @@ int choose_sgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
     TB = round_up(forced_tb, 64);
     VPL = (n + TB - 1) / TB;
   } else {
-    int best = 1 << 30;
-    TB = 0;
-    for (int tb = 192; tb <= 512; tb += 64) {
-      const int v = (n + tb - 1) / tb;
-      const int waste = v * tb - n;
-      if (v <= kMaxVplS && waste < best) {
-        best = waste;
-        TB = tb;
-      }
-    }
-    if (!TB) TB = std::min(kMaxThreadsS, round_up((n + kMaxVplS - 1) / kMaxVplS, 64));
+    // 256 threads (4 waves) per shot measured best on n225..n1600 (DESIGN.md
+    // §Kernels): four workgroups per CU, short check-phase tails.
+    TB = std::min(256, round_up(n, 64));
     VPL = (n + TB - 1) / TB;
+    if (VPL > kMaxVplS) {
+      TB = std::min(kMaxThreadsS, round_up((n + kMaxVplS - 1) / kMaxVplS, 64));
+      VPL = (n + TB - 1) / TB;
+    }
   }
   if (TB > kMaxThreadsS || TB < 64) return set_err(QLDPC_EINVAL, "threads per shot out of range (64..1024)");
   if (VPL > kMaxVplS) return set_err(QLDPC_ENOTSUP, "more than 32 variables per thread (n > 32768)");
