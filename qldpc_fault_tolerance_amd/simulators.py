@@ -1,0 +1,287 @@
+"""Drop-in Monte Carlo simulators with the reference's names and signatures.
+
+Mirrors the code-capacity part of ``src/Simulators.py``:
+
+* :class:`CodeSimulator_DataError` (``:75-188``) — ``WordErrorRate(num_run)``
+  returns ``(wer, wer_eb)`` with the reference's formulas (incl. quirk Q2).
+  When both decoders are this engine's :class:`~.decoders.BPDecoder`, the shot
+  loop runs as ONE fused HIP launch per GPU (sample → syndrome → BP →
+  residual → logical check, ``qldpc_mc_launch``), shots sharded over the
+  ``torch.distributed`` ranks with a single counter all-reduce
+  (:mod:`.parallel`).  Decoders from elsewhere (any object with
+  ``.decode(synd)``, the reference's plugin contract ``src/Decoders.py:94-97``)
+  run through the per-shot ``_single_run`` loop, as in the reference.
+* :class:`CodeFamily` (``:746-908``) — ``EvalWER('data', ...)``.
+* the threshold-fit helpers (``:675-741``), host-side post-processing.
+
+Shot randomness: the reference draws ``random.random()`` per qubit (MT19937,
+re-seeded per forked worker, so not reproducible).  The fused path draws the
+same 53-bit uniforms from Philox4x32-10 keyed by ``(seed, global shot, qubit)``
+— reproducible and identical for any GPU count; ``seed`` defaults to 64 bits
+of Python's ``random`` so ``random.seed(s)`` still pins a run.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+
+from . import parallel
+from .codes import load_code
+
+# ------------------------------------------------------------------ formulas
+
+
+def pauli_split(u, pauli_error_probs):
+    """Reference 3-way split of uniforms ``u`` (``src/Simulators.py:99-113``) -> (e_x, e_z) int arrays.
+
+    ``pauli_error_probs = [px, py, pz]``: Z if ``u < pz``; X if ``pz <= u < pz+px``;
+    Y (both) if ``pz+px <= u < pz+px+py`` — thresholds summed in that order.
+    """
+    px, py, pz = (float(x) for x in pauli_error_probs)
+    u = np.asarray(u, dtype=np.float64)
+    t1, t2, t3 = pz, pz + px, (pz + px) + py
+    z_only = u < t1
+    x_only = (t1 <= u) & (u < t2)
+    y = (t2 <= u) & (u < t3)
+    e_x = (x_only | y).astype(np.int64)
+    e_z = (z_only | y).astype(np.int64)
+    return e_x, e_z
+
+
+def word_error_rate(error_count: int, num_run: int, K: int):
+    """``WordErrorRate`` arithmetic of ``src/Simulators.py:174-188`` (keeps quirk Q2: ``eb`` for LER)."""
+    ler = error_count / num_run
+    ler_eb = np.sqrt((1 - ler) * ler / num_run)
+    wer = 1.0 - (1 - ler) ** (1 / K)
+    wer_eb = ler_eb * ((1 - ler_eb) ** (1 / K - 1)) / K
+    return wer, wer_eb
+
+
+def word_error_rate_per_cycle(error_count: int, num_samples: int, K: int, total_num_cycles: int):
+    """Per-qubit per-cycle WER of the multi-round simulators (``src/Simulators_SpaceTime.py:538-548``)."""
+    assert int(total_num_cycles) % 2 == 1
+    ler = error_count / num_samples
+    ler_q = 1.0 - (1 - ler) ** (1 / K)
+    if ler_q <= 0.5:
+        return (1.0 - (1 - 2 * ler_q) ** (1 / total_num_cycles)) / 2
+    return (1.0 + (-1 + 2 * ler_q) ** (1 / total_num_cycles)) / 2
+
+
+def load_object(filename):
+    """``load_object`` (``src/Simulators.py:69-71``) for code files, without unpickling."""
+    return load_code(filename)
+
+
+# --------------------------------------------------------------- simulators
+
+
+def _engine_bp(decoder):
+    """The engine's DeviceBP behind a drop-in decoder, or None for a foreign decoder."""
+    from .engine import DeviceBP
+
+    bp = getattr(decoder, "decoder", None)
+    return bp if isinstance(bp, DeviceBP) else None
+
+
+class CodeSimulator_DataError:
+    """Data-error simulator (``src/Simulators.py:75-188``).
+
+    Extra keyword arguments (not in the reference): ``seed`` for the fused
+    path's Philox stream.
+    """
+
+    def __init__(self, code=None, decoder_x=None, decoder_z=None, pauli_error_probs=(0.01, 0.01, 0.01),
+                 eval_logical_type="Total", seed=None):
+        self.code = code
+        self.decoder_z, self.decoder_x = decoder_z, decoder_x
+        self.N = code.N
+        self.K = code.K
+        self.channel_probs = list(pauli_error_probs)
+        self.error_x = np.zeros(self.N).astype(int)
+        self.error_z = np.zeros(self.N).astype(int)
+        self.min_logical_weight = self.N
+        self.eval_logical_type = eval_logical_type
+        self.seed = int(seed) if seed is not None else None
+        self._shot_offset = 0
+        self._mc = None
+        self.last_result = None
+
+    # -- reference per-shot API (plugin path) --------------------------------
+    def _generate_error(self):
+        u = np.array([random.random() for _ in range(self.N)])
+        self.error_x, self.error_z = pauli_split(u, self.channel_probs)
+        return self.error_x, self.error_z
+
+    def _single_run(self):
+        self.error_x, self.error_z = self._generate_error()
+        code = self.code
+        synd_z = code.hx @ self.error_z % 2
+        decoded_z = self.decoder_z.decode(synd_z)
+        synd_x = code.hz @ self.error_x % 2
+        decoded_x = self.decoder_x.decode(synd_x)
+        residual_x = (self.error_x + decoded_x) % 2
+        residual_z = (self.error_z + decoded_z) % 2
+        X_failure = int(((code.hz @ residual_x) % 2).any() or ((code.lz @ residual_x) % 2).any())
+        Z_failure = int(((code.hx @ residual_z) % 2).any() or ((code.lx @ residual_z) % 2).any())
+        for fail, r, L in ((X_failure, residual_x, code.lz), (Z_failure, residual_z, code.lx)):
+            if fail and ((L @ r) % 2).any():
+                self.min_logical_weight = min(self.min_logical_weight, int(np.sum(r)))
+        assert self.eval_logical_type in ["X", "Z", "Total"]
+        if self.eval_logical_type == "X":
+            return X_failure
+        if self.eval_logical_type == "Z":
+            return Z_failure
+        return X_failure or Z_failure
+
+    # -- fused engine path ----------------------------------------------------
+    def _engine_ready(self):
+        need_x = self.eval_logical_type != "Z"
+        need_z = self.eval_logical_type != "X"
+        bx = _engine_bp(self.decoder_x) if need_x else None
+        bz = _engine_bp(self.decoder_z) if need_z else None
+        return (not need_x or bx is not None) and (not need_z or bz is not None), bx, bz
+
+    def _device_mc(self, bx, bz):
+        from .engine import DeviceMC
+
+        if self._mc is None:
+            self._mc = DeviceMC(self.code, bx, bz)
+        return self._mc
+
+    def fused_counts(self, num_run: int):
+        """Run ``num_run`` shots through the fused HIP path; returns the all-reduced :class:`~.engine.MCResult`."""
+        ok, bx, bz = self._engine_ready()
+        if not ok:
+            raise TypeError("fused path needs engine BPDecoder instances for the sectors eval_logical_type uses")
+        from .engine import MCResult, _torch
+
+        torch = _torch()
+        if self.seed is None:
+            self.seed = random.getrandbits(64)
+        mc = self._device_mc(bx, bz)
+        rank, ws = parallel.world()
+        b, c = parallel.shard_range(num_run, rank, ws, begin=self._shot_offset)
+        self._shot_offset += int(num_run)
+        px, py, pz = self.channel_probs
+        cnt = mc.new_counters()
+        mc.launch(px, py, pz, self.seed, b, c, self.eval_logical_type, cnt)
+        parallel.allreduce_counters(cnt)
+        torch.cuda.synchronize(cnt.device)
+        res = MCResult.from_words(cnt.cpu().numpy())
+        self.last_result = res
+        return res
+
+    def WordErrorRate(self, num_run: int):
+        ok, _, _ = self._engine_ready()
+        if ok:
+            error_count = self.fused_counts(num_run).failures
+        else:
+            error_count = int(np.sum([self._single_run() for _ in range(num_run)]))
+        return word_error_rate(error_count, num_run, self.K)
+
+
+# -------------------------------------------------------------- code family
+
+
+class CodeFamily:
+    """``src/Simulators.py:746-963`` (code-capacity ``'data'`` noise model)."""
+
+    def __init__(self, code_list: list, decoder1_class, decoder2_class):
+        self.code_list = code_list
+        self.decoder1_class = decoder1_class
+        self.decoder2_class = decoder2_class
+
+    def EvalWER(self, noise_model: str, eval_logical_type: str, eval_p_list: list, num_samples: int, num_cycles=1,
+                data_synd_noise_ratio=1, circuit_type="coloration", circuit_error_params=None, if_plot=True):
+        assert noise_model in ["data", "phenl", "circuit"], "noise_model should be one of [data, phenl, circuit]"
+        assert eval_logical_type in ["X", "Z", "Total"], "eval_type should be one of [X, Y, Total]"
+        if noise_model != "data":
+            raise NotImplementedError(f"noise_model={noise_model!r}: the engine covers the code-capacity path "
+                                      "(phenomenological: CodeSimulator_Phenon_SpaceTime; circuit level needs stim)")
+        eval_wer_list = []
+        for eval_code in self.code_list:
+            for eval_p in eval_p_list:
+                p = eval_p * 3 / 2
+                pauli_error_probs = [p / 3, p / 3, p / 3]  # src/Simulators.py:763-764
+                decoder_x = self.decoder2_class.GetDecoder({"h": eval_code.hz, "p_data": eval_p})
+                decoder_z = self.decoder2_class.GetDecoder({"h": eval_code.hx, "p_data": eval_p})
+                sim = CodeSimulator_DataError(code=eval_code, decoder_x=decoder_x, decoder_z=decoder_z,
+                                              pauli_error_probs=pauli_error_probs,
+                                              eval_logical_type=eval_logical_type)
+                eval_wer_list.append(sim.WordErrorRate(num_samples)[0])
+        eval_wer_array = np.reshape(np.array(eval_wer_list), [len(self.code_list), len(eval_p_list)])
+        if if_plot:
+            _plot_wer(self.code_list, eval_p_list, eval_wer_array, num_cycles)
+        return eval_wer_array
+
+    def EvalThreshold(self, noise_model: str, eval_logical_type: str, eval_method: str, est_threshold: float,
+                      num_samples: int, num_cycles=1, data_synd_noise_ratio=1, circuit_type="coloration",
+                      circuit_error_params=None, if_plot=False):
+        """``src/Simulators.py:912-924``."""
+        assert eval_method in ["extrapolation"], "eval_method should be one of [extrapolation]"
+        eval_p_list = 10 ** (np.linspace(np.log10(est_threshold * 0.4), np.log10(est_threshold * 0.8), 6))
+        eval_wer_array = self.EvalWER(noise_model, eval_logical_type, eval_p_list, num_samples, num_cycles,
+                                      data_synd_noise_ratio, circuit_type, circuit_error_params, if_plot=False)
+        return ThresholdEst_extrapolation(eval_p_list, eval_wer_array, if_plot)
+
+
+def _plot_wer(code_list, eval_p_list, eval_wer_array, num_cycles):
+    try:
+        import matplotlib.pyplot as plt
+    except ImportError:  # plotting is cosmetic in the reference too
+        return
+    per_qubit = (1 - (1 - 2 * eval_wer_array) ** num_cycles) / 2
+    total = np.zeros(eval_wer_array.shape)
+    for i, code in enumerate(code_list):
+        total[i, :] = 1 - (1 - per_qubit[i, :]) ** code.K
+    fig, ax = plt.subplots(1, 3, figsize=(15, 3))
+    for arr, a, lab in ((total, ax[0], "Logical error"), (per_qubit, ax[1], "Logical error per qubit"),
+                        (eval_wer_array, ax[2], "WER")):
+        for row in arr:
+            a.plot(eval_p_list, row, "D--")
+        a.set_xscale("log")
+        a.set_yscale("log")
+        a.set_xlabel(r"$p$")
+        a.set_ylabel(lab)
+    plt.close(fig)
+
+
+# ------------------------------------------------------- threshold fitting
+
+
+def EmpericalFit(xdata_tuple, pc, A):
+    p, d = xdata_tuple
+    return A * (p / pc) ** (d / 2)
+
+
+def FitDistance(p, A, d):
+    return A * p ** (d / 2)
+
+
+def DistanceEst(sweep_p_list, sweep_pl_total_list, if_plot=False):
+    """``src/Simulators.py:690-699``."""
+    from scipy.optimize import curve_fit
+
+    out = []
+    for sweep_pl_list in sweep_pl_total_list:
+        popt, _ = curve_fit(FitDistance, np.array(sweep_p_list), np.array(sweep_pl_list) + 1e-10, p0=(0.01, 3))
+        out.append(popt[1])
+    return out
+
+
+def ThresholdEst_extrapolation(sweep_p_list, sweep_pl_total_list, if_plot=False):
+    """``src/Simulators.py:701-741`` (fit ``A (p/p_c)^(d/2)`` with per-code fitted d)."""
+    from scipy.optimize import curve_fit
+
+    num_p = len(sweep_p_list)
+    num_code = len(sweep_pl_total_list)
+    d_list = DistanceEst(sweep_p_list, sweep_pl_total_list)
+    p_all = list(sweep_p_list) * num_code
+    d_all = [d for d in d_list for _ in range(num_p)]
+    fit_X = np.vstack([np.reshape(np.array(p_all), [1, num_p * num_code]),
+                       np.reshape(np.array(d_all), [1, num_p * num_code])])
+    fit_Z = np.reshape(np.array(sweep_pl_total_list), [num_p * num_code])
+    popt, _ = curve_fit(EmpericalFit, fit_X, fit_Z, p0=(0.04, 0.1))
+    print("p_c:", popt[0])
+    return popt[0]

@@ -1,0 +1,162 @@
+"""CPU tests: the oracle and the host logic against the reference's own harness.
+
+``tests/golden/reference_harness_n225.npz`` was produced by running the
+reference's ``Simulators.py`` / ``Decoders*.py`` (stub-imported, BP backed by
+this repository's oracle: tests/golden/make_golden.py).  Everything except the
+BP arithmetic is therefore the reference's behaviour; BP parity is pinned by the
+oracle's known-answer tests below (the reference has no BP fixtures: DESIGN.md
+§Oracle, "parity of the BP arithmetic unpinned by the reference").
+"""
+import os
+
+import numpy as np
+import pytest
+
+from qldpc_fault_tolerance_amd import codes, decoders, simulators
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_harness_n225.npz")
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(GOLD, allow_pickle=False)
+
+
+@pytest.fixture(scope="module")
+def n225():
+    return codes.get_code("hgp_34_n225")
+
+
+@pytest.mark.parametrize("tag", ["dep05", "dep10", "asym"])
+def test_pauli_split_matches_reference_generate_error(gold, tag):
+    """A5: src/Simulators.py:89-115 on identical uniforms."""
+    u = gold[f"gen_{tag}_u"]
+    ex, ez = simulators.pauli_split(u, gold[f"gen_{tag}_probs"])
+    assert np.array_equal(ex, gold[f"gen_{tag}_ex"])
+    assert np.array_equal(ez, gold[f"gen_{tag}_ez"])
+
+
+@pytest.mark.parametrize("pc", [3, 6])
+def test_bp_factory_matches_reference(gold, n225, pc):
+    """A2: BP_Decoder_Class.GetDecoder arguments (max_iter = n/ratio as float, quirk Q1)."""
+    cls = decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    n, probs = cls._probs({"h": n225.hz, "p_data": pc / 100})
+    assert n / 10 == gold[f"factory_p{pc}_max_iter_arg"][0]
+    assert np.array_equal(probs, gold[f"factory_p{pc}_probs"][0])
+    assert decoders._int_max_iter(n / 10, n) == 22
+
+
+def test_factory_asserts_like_reference():
+    cls = decoders.BP_Decoder_Class(10, "minimum_sum", 0.625)
+    with pytest.raises(AssertionError):
+        cls.GetDecoder({"p_data": 0.1})
+    with pytest.raises(AssertionError):
+        cls.GetDecoder({"h": np.eye(3)})
+    st = decoders.ST_BP_Decoder_Class(10, "minimum_sum", 0.625)
+    with pytest.raises(AssertionError):
+        st.GetDecoder({"h": np.eye(3), "p_data": 0.1})
+
+
+@pytest.mark.parametrize("pc", [3, 6])
+@pytest.mark.parametrize("mode", ["X", "Z", "Total"])
+def test_oracle_mc_replays_reference_single_run(gold, n225, oracle, pc, mode):
+    """A5-A7: the fused shot loop on the reference's uniforms gives its failure flags."""
+    p = pc / 100
+    u = gold[f"run_p{pc}_u"]
+    ref = oracle.mc_run(n225, p / 2, p / 2, p / 2, seed=0, shot_begin=0, shot_count=u.shape[0], logical_mode=mode,
+                        probs_x=p, probs_z=p, max_iter=22, precision=64, uniforms=u, per_shot=True)
+    fx, fz = ref["fail"] & 1, ref["fail"] >> 1
+    want = gold[f"run_p{pc}_{mode}_fail"]
+    got = fx if mode == "X" else fz if mode == "Z" else (fx | fz)
+    assert np.array_equal(got, want)
+    assert ref["failures"] == int(want.sum())
+
+
+def test_wer_formula_matches_reference(gold):
+    """A8: WordErrorRate arithmetic incl. quirk Q2."""
+    for num_run, nfail, wer, eb in gold["wer_cases"]:
+        w, e = simulators.word_error_rate(int(nfail), int(num_run), 17)
+        assert w == wer
+        assert (e == eb) or (np.isnan(e) and np.isnan(eb))
+
+
+def test_spacetime_wer_formula_matches_reference(gold):
+    """A13: per-cycle WER of CodeSimulator_Phenon_SpaceTime.WordErrorRate (Simulators_SpaceTime.py:531-548)."""
+    for num_cycles, num_samples, nfail, w in gold["phenst_wer_cases"]:
+        num_rounds = int((num_cycles - 1) / 3 + 1)
+        total = (num_rounds - 1) * 3 + 1
+        assert simulators.word_error_rate_per_cycle(int(nfail), int(num_samples), 17, total) == w
+
+
+@pytest.mark.parametrize("t0", [1, 2, 3])
+def test_space_time_matrix_matches_reference(gold, n225, t0):
+    """A10: GetSpaceTimeCheckMat (Decoders_SpaceTime.py:179-194)."""
+    c = codes.space_time_csr(n225.hx, t0)
+    assert [c.m, c.n] == list(gold[f"st_t{t0}_shape"])
+    assert np.array_equal(c.row_ptr, gold[f"st_t{t0}_row_ptr"])
+    assert np.array_equal(c.col_idx, gold[f"st_t{t0}_col_idx"])
+    assert np.array_equal(decoders.GetSpaceTimeCheckMat(n225.hx, t0), c.to_dense().astype(float))
+
+
+def test_space_time_decoder_matches_reference(gold, n225, oracle):
+    """A11/A12: ST_BP_Decoder_Class factory priors/max_iter and the decode+fold of ST_BP_Decoder_syndrome."""
+    assert gold["stfactory_max_iter_arg"][0] == n225.N / 10
+    probs = np.hstack([0.02 * np.ones(n225.N), 0.02 * np.ones(n225.hz.shape[0])] * 3)
+    assert np.array_equal(probs, gold["stfactory_probs"])
+    st = codes.space_time_csr(n225.hz, 3)
+    hist = gold["stdec_hist"]
+    synd = hist.reshape(hist.shape[0], -1)
+    corr, _, _ = oracle.bp_decode_batch(st, probs, 22, "minimum_sum", 0.625, synd, 64)
+    folded = decoders.fold_space_time_correction(corr, n225.N, n225.hz.shape[0], 3)
+    assert np.array_equal(folded, gold["stdec_corr"])
+
+
+# ----------------------------------------------------------- oracle KATs
+
+
+def test_oracle_zero_syndrome_is_zero_correction(n225, oracle):
+    s = np.zeros((3, n225.hz.shape[0]), np.uint8)
+    corr, iters, conv = oracle.bp_decode_batch(n225.hz, 0.05, 22, "minimum_sum", 0.625, s, 64)
+    assert not corr.any() and (iters == 1).all() and conv.all()
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+def test_oracle_corrects_every_weight_one_error(n225, oracle, precision):
+    H = n225.hz
+    E = np.eye(n225.N, dtype=np.uint8)
+    S = (E.astype(np.int64) @ H.T.astype(np.int64) % 2).astype(np.uint8)
+    corr, iters, conv = oracle.bp_decode_batch(H, 0.05, 22, "minimum_sum", 0.625, S, precision)
+    assert conv.all()
+    # the decoding reproduces the syndrome (the residual is a stabiliser or zero)
+    assert np.array_equal(codes.CSR.from_dense(H).matvec(corr), S)
+
+
+def test_oracle_is_deterministic_and_threaded_identically(n225, oracle):
+    rng = np.random.default_rng(5)
+    e = (rng.random((64, n225.N)) < 0.06).astype(np.uint8)
+    S = codes.CSR.from_dense(n225.hx).matvec(e).astype(np.uint8)
+    a = oracle.bp_decode_batch(n225.hx, 0.06, 22, "minimum_sum", 0.625, S, 64, nthreads=1)
+    b = oracle.bp_decode_batch(n225.hx, 0.06, 22, "minimum_sum", 0.625, S, 64, nthreads=4)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_oracle_philox_known_answer(oracle):
+    """Philox4x32-10 published KAT (Salmon et al., SC'11 / Random123 kat_vectors)."""
+    assert oracle.philox4x32_10([0, 0, 0, 0], [0, 0]) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert oracle.philox4x32_10([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6,
+                                                                       0x6D5451FD]
+    assert oracle.philox4x32_10([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344],
+                                [0xA4093822, 0x299F31D0]) == [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_oracle_mc_shard_invariance(n225, oracle):
+    """Counters over a shot range do not depend on how the range is split (multi-GPU invariant)."""
+    kw = dict(logical_mode="Total", probs_x=0.05, probs_z=0.05, max_iter=22, precision=32)
+    whole = oracle.mc_run(n225, 0.025, 0.025, 0.025, seed=3, shot_begin=100, shot_count=600, **kw)
+    parts = [oracle.mc_run(n225, 0.025, 0.025, 0.025, seed=3, shot_begin=b, shot_count=c, **kw)
+             for b, c in [(100, 250), (350, 350)]]
+    for key in ("shots", "failures", "sector_iters", "sector_nonconv", "sector_fail"):
+        tot = parts[0][key]
+        tot = tot + parts[1][key] if not isinstance(tot, list) else [x + y for x, y in zip(tot, parts[1][key])]
+        assert tot == whole[key], key
