@@ -83,6 +83,17 @@ def cpu_baseline(code, eval_p, max_iter, logical, budget_s):
                       f"fp64 with {cores} OpenMP threads, {dt:.1f} s; LER={r['failures'] / S2:.4g}"}
 
 
+def measured_traffic(code, p, shots, logical, precision):
+    """HBM bytes per launch measured by rocprofv3 PMC passes for this exact config (profiles/traffic.json)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = t.get(f"{code}|{p}|{shots}|{logical}|{precision}")
+    return e["bytes"] if e else None
+
+
 def main():
     a = parse()
     import torch
@@ -186,7 +197,8 @@ def main():
         "nonconverged_frac": nonconv / max(decodes, 1),
         "logical_error_rate": int(w[1]) / max(shots, 1),
         "roofline": {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / LDS_PEAK_GBS, "traffic": None,
+                     "frac": achieved / LDS_PEAK_GBS,
+                     "traffic": measured_traffic(a.code, p, S, a.logical, a.precision),
                      "hbm_peak": HBM_PEAK_GBS, "frac_of_hbm_peak": achieved / HBM_PEAK_GBS,
                      "kernel": "qldpc::mc_kernel", "kernel_ms": kern_ms,
                      "bytes_per_launch": bytes_per_launch},

@@ -1,0 +1,109 @@
+"""GPU tests of the drop-in decoder / simulator classes (fused path) against the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+from qldpc_fault_tolerance_amd import codes, decoders, simulators
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_harness_n225.npz")
+
+
+def test_word_error_rate_fused_matches_oracle(gpu, oracle):
+    """CodeSimulator_DataError.WordErrorRate (fused HIP path) == the A8 formula on the oracle's counts."""
+    code = codes.get_code("hgp_34_n225")
+    p = 0.05
+    cls = decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625,
+                                    precision=64)
+    dx = cls.GetDecoder({"h": code.hz, "p_data": p})
+    dz = cls.GetDecoder({"h": code.hx, "p_data": p})
+    pp = p * 3 / 2 / 3
+    sim = simulators.CodeSimulator_DataError(code=code, decoder_x=dx, decoder_z=dz, pauli_error_probs=[pp] * 3,
+                                             eval_logical_type="Total", seed=1234)
+    wer, eb = sim.WordErrorRate(3000)
+    ref = oracle.mc_run(code, pp, pp, pp, seed=1234, shot_begin=0, shot_count=3000, logical_mode="Total",
+                        probs_x=p, probs_z=p, max_iter=22, precision=64)
+    assert (wer, eb) == simulators.word_error_rate(ref["failures"], 3000, code.K)
+    assert sim.last_result.sector_iters == ref["sector_iters"]
+    # a second call continues the shot stream (no reuse of shots)
+    sim.WordErrorRate(1000)
+    ref2 = oracle.mc_run(code, pp, pp, pp, seed=1234, shot_begin=3000, shot_count=1000, logical_mode="Total",
+                         probs_x=p, probs_z=p, max_iter=22, precision=64)
+    assert sim.last_result.failures == ref2["failures"]
+
+
+def test_bpdecoder_decode_contract(gpu, oracle):
+    """BPDecoder.decode(synd) -> int ndarray [n] (src/Decoders.py:88-90), iter/converge attributes."""
+    code = codes.get_code("hgp_34_n225")
+    dec = decoders.BPDecoder(code.hx, 0.05 * np.ones(code.N), 22, "minimum_sum", 0.625)
+    rng = np.random.default_rng(2)
+    e = (rng.random(code.N) < 0.04).astype(np.int64)
+    s = code.hx @ e % 2
+    c = dec.decode(s.astype(float))
+    assert c.shape == (code.N,) and c.dtype.kind == "i"
+    oc, oi, ov = oracle.bp_decode_batch(code.hx, 0.05, 22, "minimum_sum", 0.625, s.reshape(1, -1), 64)
+    assert np.array_equal(c, oc[0]) and dec.iter == oi[0] and dec.converge == int(ov[0])
+
+
+def test_spacetime_decoder_matches_reference_fixture(gpu):
+    """ST_BP_Decoder_Class on the GPU reproduces the reference harness's ST decodes (fp64, bit-exact)."""
+    g = np.load(GOLD, allow_pickle=False)
+    code = codes.get_code("hgp_34_n225")
+    st = decoders.ST_BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    dec = st.GetDecoder({"h": code.hz, "p_data": 0.02, "p_syndrome": 0.02, "num_rep": 3})
+    out = dec.decode_batch(g["stdec_hist"])
+    assert np.array_equal(out, g["stdec_corr"])
+    assert np.array_equal(dec.decode(g["stdec_hist"][0]), g["stdec_corr"][0])
+
+
+def test_spacetime_graph_n1225_fp32_matches_oracle(gpu, oracle):
+    """Config 5's stacked graph (1764 x 5439, E = 15,288) through the engine, fp32, vs the oracle's fp32 mode."""
+    code = codes.get_code("hgp_34_n1225_q3")
+    st = codes.space_time_csr(code.hx, 3)
+    assert (st.m, st.n, st.nnz) == (1764, 5439, 15288)
+    from qldpc_fault_tolerance_amd.engine import DeviceBP
+
+    p = 0.02
+    probs = np.hstack([p * np.ones(code.N), p * np.ones(code.hx.shape[0])] * 3)
+    rng = np.random.default_rng(9)
+    e = (rng.random((200, st.n)) < p).astype(np.uint8)
+    synd = st.matvec(e).astype(np.uint8)
+    dec = DeviceBP(st, probs, max_iter=int(code.N / 10), precision=32)
+    corr, iters, conv = dec.decode_batch(synd)
+    oc, oi, ov = oracle.bp_decode_batch(st, probs, int(code.N / 10), "minimum_sum", 0.625, synd, 32)
+    assert np.array_equal(iters, oi) and np.array_equal(conv, ov) and np.array_equal(corr, oc)
+
+
+def test_fp32_logical_error_rate_statistically_identical_to_fp64_oracle(gpu, oracle):
+    """North-star criterion: fp32 fast mode's LER within binomial 95% CI of the fp64 reference arithmetic."""
+    code = codes.get_code("hgp_34_n625")
+    p = 0.04
+    pp = p / 2
+    S = 20000
+    from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceMC
+
+    dx = DeviceBP(code.hz, p, max_iter=62, precision=32)
+    dz = DeviceBP(code.hx, p, max_iter=62, precision=32)
+    g = DeviceMC(code, dx, dz).run(pp, pp, pp, seed=77, shot_begin=0, shot_count=S, logical_mode="Total")
+    r = oracle.mc_run(code, pp, pp, pp, seed=77, shot_begin=0, shot_count=S, logical_mode="Total", probs_x=p,
+                      probs_z=p, max_iter=62, precision=64)
+    a, b = g.failures / S, r["failures"] / S
+    se = np.sqrt(a * (1 - a) / S + b * (1 - b) / S)
+    assert abs(a - b) <= 1.96 * se + 1e-12, (a, b, se)
+
+
+def test_fp32_decoded_vectors_agree_with_fp64(gpu, oracle):
+    """Report-level check: fp32 decoded vectors vs the fp64 reference arithmetic on the same syndromes."""
+    code = codes.get_code("hgp_34_n1600")
+    from qldpc_fault_tolerance_amd.engine import DeviceBP
+
+    rng = np.random.default_rng(4)
+    e = (rng.random((1000, code.N)) < 0.03).astype(np.uint8)
+    synd = code.csr("hz").matvec(e).astype(np.uint8)
+    dec = DeviceBP(code.hz, 0.03, max_iter=160, precision=32)
+    corr, _, conv = dec.decode_batch(synd)
+    oc, _, ov = oracle.bp_decode_batch(code.hz, 0.03, 160, "minimum_sum", 0.625, synd, 64)
+    both = conv & ov
+    agree_conv = np.mean([np.array_equal(corr[i], oc[i]) for i in np.flatnonzero(both)])
+    assert agree_conv >= 0.999, agree_conv
