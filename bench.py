@@ -200,7 +200,7 @@ def main():
                      "frac": achieved / LDS_PEAK_GBS,
                      "traffic": measured_traffic(a.code, p, S, a.logical, a.precision),
                      "hbm_peak": HBM_PEAK_GBS, "frac_of_hbm_peak": achieved / HBM_PEAK_GBS,
-                     "kernel": "qldpc::mc_kernel", "kernel_ms": kern_ms,
+                     "kernel": "qldpc::smc_kernel", "kernel_ms": kern_ms,
                      "bytes_per_launch": bytes_per_launch},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
