@@ -140,6 +140,12 @@ int qldpc_mc_run(qldpc_mc *mc, double px, double py, double pz, uint64_t seed, u
 int qldpc_bp_geometry(const qldpc_bp *bp, int32_t *threads, int32_t *vars_per_thread, int32_t *lds_bytes,
                       int32_t *blocks_per_cu);
 
+/* Kernel engine serving a decoder: 3 = register-resident variables (default
+ * when the graph fits: column degree <= 4, <= 8 variables per thread, image
+ * < 64 KiB), 2 = streamed variables, 1 = LDS-atomic check state.  QLDPC_ENGINE
+ * in the environment selects 1 or 2 explicitly. */
+int qldpc_bp_engine(const qldpc_bp *bp, int32_t *engine);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,7 +19,7 @@ EXPORTED = [
     "qldpc_abi_version", "qldpc_last_error", "qldpc_device_count", "qldpc_graph_create", "qldpc_graph_destroy",
     "qldpc_graph_info", "qldpc_bp_create", "qldpc_bp_destroy", "qldpc_bp_set_channel_probs",
     "qldpc_bp_decode_batch", "qldpc_mc_create", "qldpc_mc_destroy", "qldpc_mc_launch", "qldpc_mc_run",
-    "qldpc_bp_geometry",
+    "qldpc_bp_geometry", "qldpc_bp_engine",
 ]
 
 
@@ -89,6 +89,8 @@ def _declare(L):
     L.qldpc_mc_run.argtypes = [_vp, _dbl, _dbl, _dbl, _u64, _u64, _i64, _i32, ctypes.POINTER(Counters), _vp]
     L.qldpc_bp_geometry.restype = ctypes.c_int
     L.qldpc_bp_geometry.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 4
+    L.qldpc_bp_engine.restype = ctypes.c_int
+    L.qldpc_bp_engine.argtypes = [_vp, ctypes.POINTER(_i32)]
 
 
 def lib():

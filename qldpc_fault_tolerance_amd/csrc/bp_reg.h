@@ -1,0 +1,640 @@
+// bp_reg.h — engine 3: register-resident variables (gfx950).
+//
+// Same flooding min-sum as engine 2 (bp_slot.h: compressed check state
+// {m1 | parity<<sign, m2}, row-major v2c slots, canonical messages, dummies for
+// missing edges) with the per-variable state moved out of the memory system:
+//   * each thread's VPL (compile-time) variables keep, in VGPRs for the whole
+//     pass, their DMAX edge words pre-converted to absolute LDS byte addresses
+//     (CS address | V address << 16), their prior, and (float) their own
+//     previous v2c messages — the variable phase issues one random LDS read per
+//     edge (the CS gather) and one write (the new v2c), no global traffic;
+//   * the CS gathers of variable k+1 are issued before variable k's arithmetic
+//     (software pipeline), so LDS latency hides under VALU work;
+//   * padding variables (j >= n) have only dummy edges and prior +1, so no
+//     per-variable bounds test remains in the hot loop;
+//   * redundant ops of ldpc's backward pass (`0 + c`, `f + 0`) are dropped: they
+//     change at most the sign of a zero, which the canonical encoding (sign :=
+//     v <= 0) erases, so the stored messages and decisions stay bit-identical.
+// The LDS image puts CS first so that its byte address is the edge word's low
+// half: [CS (m+1) pairs][V: 16-byte sink + m rows][F (m+1)][lred 8][flags 2].
+// One decode in flight per workgroup; several workgroups share a CU.
+//
+// Engine 4 (same file, ENG = 4) moves the c2v arithmetic into the check phase:
+// the check thread, which holds its whole row in registers, computes every
+// edge's c2v (m2 if the edge holds m1 else m1, times ±alpha) and writes them
+// back into the row's slots; the variable phase then reads its c2v with one
+// 4-byte LDS read per edge and overwrites the slot with the new v2c.  No CS
+// array and no own-message registers remain, the random LDS reads halve in
+// width, and the image shrinks by 8 bytes per check.  Padding slots of a row
+// (logical position >= row degree) are rewritten with the sentinel, so the
+// next min pass ignores them.  Missing edges read a constant zero chunk and
+// write a sink.  Image: [V: zero chunk + m rows][F (m+1): bit0 (H x)_i, bit1
+// syndrome, bits 16.. row degree][sink 16][lred 8][flags 2].
+#pragma once
+#include "bp_slot.h"
+
+namespace qldpc {
+
+struct RLayout {
+  uint32_t v, f, sink, lred, total;  // byte offsets (engine 3: CS at 0; engine 4: V at 0)
+};
+
+__host__ __device__ inline RLayout r_layout(int eng, int vslots, int mmax, int tsize) {
+  RLayout L;
+  L.v = eng == 4 ? 0u : (uint32_t)a16((size_t)(mmax + 1) * 2 * tsize);
+  L.f = L.v + (uint32_t)a16((size_t)vslots * tsize);
+  L.sink = L.f + (uint32_t)a16((size_t)(mmax + 1) * 4);
+  L.lred = L.sink + (eng == 4 ? 16u : 0u);
+  L.total = L.lred + 48;
+  return L;
+}
+// Block LDS: image + 2 sector fail bitmaps of `chunk` shots + counters.
+__host__ __device__ inline size_t r_lds_bytes(int img, int chunk) {
+  return (size_t)img + 2 * a16((size_t)((chunk + 31) / 32) * 4) + 8 * 12;
+}
+
+template <typename T>
+__device__ inline T& lds_at(unsigned char* smem, uint32_t off) {
+  return *reinterpret_cast<T*>(smem + off);
+}
+
+// canonical bits: |v| with the sign bit := (v <= 0).  Only +0 differs from the
+// raw bits (-0 and negatives already carry the sign bit; NaN never occurs).
+template <typename T>
+__device__ inline typename FT<T>::U canon2(T v) {
+  const typename FT<T>::U b = FT<T>::bits(v);
+  return b == 0 ? FT<T>::kSign : b;
+}
+
+// median of three (the backend selects v_med3_u32 for this pattern)
+__device__ inline uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+  const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+  const uint32_t h2 = hi < c ? hi : c;
+  return lo > h2 ? lo : h2;
+}
+
+// Register state of one thread in one sector pass.  Edge words: engine 3 =
+// CS address | V slot address << 16; engine 4 = read address | write address
+// << 16 (equal for real edges; zero chunk / sink for missing ones).
+template <typename T, int DMAX, int VPL, int ENG = 3>
+struct RState {
+  using U = typename FT<T>::U;
+  static constexpr bool kKeepV = ENG == 3 && sizeof(T) == 4;  // own v2c in VGPRs (engine 3, float)
+  uint32_t ea[VPL][DMAX];
+  T L[VPL];
+  U ov[kKeepV ? VPL : 1][kKeepV ? DMAX : 1];
+};
+
+template <typename T, int DMAX, int VPL, int ENG>
+__device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, const RLayout& Ly, int tid, int TB) {
+  const T* llr = static_cast<const T*>(S.llr);
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) {
+      const uint32_t e = S.edges[(k * DMAX + t) * TB + tid];
+      const uint32_t va = Ly.v + eslot(e) * (uint32_t)sizeof(T);
+      if (ENG == 4)
+        R.ea[k][t] = e == kNoEdgeS ? (Ly.v | (Ly.sink << 16)) : (va | (va << 16));
+      else
+        R.ea[k][t] = (echk(e) * (uint32_t)(2 * sizeof(T))) | (va << 16);
+    }
+    R.L[k] = (k * TB + tid < S.n) ? llr[k * TB + tid] : (T)1;
+  }
+}
+
+// F word of an edge.  Engine 3: from the CS address.  Engine 4: from the row
+// of the read address (rows start 16 bytes into V, row stride 1 << rsh); the
+// zero chunk maps to row -1, i.e. the F[0] sink.
+struct FMap {
+  uint32_t fbase;   // engine 3: Ly.f; engine 4: Ly.f + 4
+  uint32_t rstart;  // engine 4: Ly.v + 16
+  int rsh;          // engine 4: log2(row stride)
+};
+template <typename T, int ENG>
+__device__ inline uint32_t f_addr(uint32_t ea, const FMap& M) {
+  if (ENG == 4) return M.fbase + 4u * (uint32_t)((int)((ea & 0xFFFFu) - M.rstart) >> M.rsh);
+  return ((ea & 0xFFFFu) >> (sizeof(T) == 4 ? 1 : 2)) + M.fbase;
+}
+
+// Opaque redefinition of the edge words (no instruction): without it the
+// compiler hoists their derived CS / V / F addresses out of the iteration and
+// shot loops, tripling the VGPRs per edge and spilling.
+template <typename T, int DMAX, int VPL, int ENG>
+__device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
+#pragma unroll
+  for (int k = 0; k < VPL; ++k)
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) asm volatile("" : "+v"(R.ea[k][t]));
+}
+
+// Variable phase (one flooding iteration's column pass).  Returns decision bits.
+template <typename T, int DMAX, int VPL>
+__device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, uint32_t fdelta, T alpha) {
+  using U = typename FT<T>::U;
+  constexpr U kS = FT<T>::kSign;
+  constexpr bool KV = RState<T, DMAX, VPL>::kKeepV;
+  r_launder(R);
+  uint32_t xbits = 0;
+  Pair<T> pn[DMAX];
+  U on[DMAX];
+#pragma unroll
+  for (int t = 0; t < DMAX; ++t) {
+    pn[t] = lds_at<Pair<T>>(smem, R.ea[0][t] & 0xFFFFu);
+    if (!KV) on[t] = FT<T>::bits(lds_at<T>(smem, R.ea[0][t] >> 16));
+  }
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    Pair<T> pr[DMAX];
+    U o[DMAX];
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) {
+      pr[t] = pn[t];
+      o[t] = KV ? R.ov[KV ? k : 0][KV ? t : 0] : on[t];
+    }
+    if (k + 1 < VPL) {  // next variable's gathers go out before this one's arithmetic
+#pragma unroll
+      for (int t = 0; t < DMAX; ++t) {
+        pn[t] = lds_at<Pair<T>>(smem, R.ea[k + 1][t] & 0xFFFFu);
+        if (!KV) on[t] = FT<T>::bits(lds_at<T>(smem, R.ea[k + 1][t] >> 16));
+      }
+    }
+    T c[DMAX];
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) {
+      const U a = pr[t].a;
+      const U d = a ^ o[t];
+      // min over the other edges: m2 if this edge holds m1 (|own| == m1), else m1
+      // (m2 carries no sign bit, so masking after the select is the same value;
+      // masking `a` before it trips an instruction-selection crash in this LLVM)
+      const U sel = (((d & ~kS) == 0) ? pr[t].b : a) & ~kS;
+      c[t] = FT<T>::val(FT<T>::bits(FT<T>::val(sel) * alpha) ^ (d & kS));
+    }
+    // ldpc column pass: forward partial sums from the prior, then backward
+    T f[DMAX];
+    T acc = R.L[k];
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) {
+      f[t] = acc;
+      acc = acc + c[t];
+    }
+    const bool x = acc <= (T)0;
+    xbits |= (x ? 1u : 0u) << k;
+    T b = c[DMAX - 1];
+    U nv[DMAX];
+    nv[DMAX - 1] = canon2<T>(f[DMAX - 1]);
+#pragma unroll
+    for (int t = DMAX - 2; t >= 0; --t) {
+      nv[t] = canon2<T>(f[t] + b);
+      if (t > 0) b = b + c[t];
+    }
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) {
+      lds_at<U>(smem, R.ea[k][t] >> 16) = nv[t];
+      if (KV) R.ov[KV ? k : 0][KV ? t : 0] = nv[t];
+    }
+    if (x) {
+#pragma unroll
+      for (int t = 0; t < DMAX; ++t)
+        atomicXor(&lds_at<uint32_t>(smem, ((R.ea[k][t] & 0xFFFFu) >> (sizeof(T) == 4 ? 1 : 2)) + fdelta), 1u);
+    }
+  }
+  return xbits;
+}
+
+// Check phase: FIRST records the syndrome bits (F bit1) into sbits; otherwise
+// tests (H x)_i == s_i (F bit0).  Clears F and rebuilds CS from the rows.
+template <typename T, bool FIRST>
+__device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int nch, int tid, int TB,
+                              uint32_t& sbits) {
+  using U = typename FT<T>::U;
+  using VT = typename V16<T>::type;
+  constexpr int NV = V16<T>::N;
+  constexpr U kS = FT<T>::kSign;
+  int mism = 0;
+  int q = 0;
+  for (int i = tid; i < m; i += TB, ++q) {
+    const VT* row = reinterpret_cast<const VT*>(smem + Ly.v + 16 + (uint32_t)i * (uint32_t)nch * 16u);
+    uint32_t& F = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
+    const uint32_t f = F;
+    uint32_t s;
+    if (FIRST) {
+      s = (f >> 1) & 1u;
+      sbits |= s << q;
+    } else {
+      s = (sbits >> q) & 1u;
+      mism |= (int)((f ^ s) & 1u);
+    }
+    F = 0;
+    U m1 = FT<T>::kSent, m2 = FT<T>::kSent;
+    U px = s ? kS : (U)0;
+    for (int c = 0; c < nch; ++c) {
+      const VT v = row[c];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const U xb = FT<T>::bits(V16<T>::get(v, k));
+        const U a = xb & ~kS;
+        if constexpr (sizeof(U) == 4) {
+          m2 = med3u(m1, m2, a);  // m1 <= m2 holds, so the median is the new second minimum
+        } else {
+          const U hi = m1 > a ? m1 : a;
+          m2 = m2 < hi ? m2 : hi;
+        }
+        m1 = m1 < a ? m1 : a;
+        px ^= xb;
+      }
+    }
+    Pair<T> st;
+    st.a = m1 | (px & kS);
+    st.b = m2;
+    lds_at<Pair<T>>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
+  }
+  return mism;
+}
+
+// Engine-4 variable phase: c2v from the slots, ldpc's column pass, v2c back.
+// Variable VPL-1 is skipped by waves whose lanes are all padding.
+template <typename T, int DMAX, int VPL>
+__device__ inline uint32_t c_var(unsigned char* smem, RState<T, DMAX, VPL, 4>& R, const FMap& M, bool last_live) {
+  using U = typename FT<T>::U;
+  r_launder(R);
+  uint32_t xbits = 0;
+  T cn[DMAX];
+#pragma unroll
+  for (int t = 0; t < DMAX; ++t) cn[t] = lds_at<T>(smem, R.ea[0][t] & 0xFFFFu);
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    T c[DMAX];
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) c[t] = cn[t];
+    if (k + 1 < VPL) {  // next variable's reads go out before this one's arithmetic
+#pragma unroll
+      for (int t = 0; t < DMAX; ++t) cn[t] = lds_at<T>(smem, R.ea[k + 1][t] & 0xFFFFu);
+    }
+    if (k == VPL - 1 && !last_live) break;
+    T f[DMAX];
+    T acc = R.L[k];
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) {
+      f[t] = acc;
+      acc = acc + c[t];
+    }
+    const bool x = acc <= (T)0;
+    xbits |= (x ? 1u : 0u) << k;
+    T b = c[DMAX - 1];
+    U nv[DMAX];
+    nv[DMAX - 1] = canon2<T>(f[DMAX - 1]);
+#pragma unroll
+    for (int t = DMAX - 2; t >= 0; --t) {
+      nv[t] = canon2<T>(f[t] + b);
+      if (t > 0) b = b + c[t];
+    }
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) lds_at<U>(smem, R.ea[k][t] >> 16) = nv[t];
+    if (x) {
+#pragma unroll
+      for (int t = 0; t < DMAX; ++t) atomicXor(&lds_at<uint32_t>(smem, f_addr<T, 4>(R.ea[k][t], M)), 1u);
+    }
+  }
+  return xbits;
+}
+
+// Engine-4 check phase over rows with NCH 16-byte chunks: syndrome / (H x)
+// test as r_check, then every slot of the row receives its c2v for the next
+// variable phase (computed with `alpha`); padding slots get the sentinel.
+template <typename T, bool FIRST, int NCH>
+__device__ inline int c_check(unsigned char* smem, const RLayout& Ly, int m, int tid, int TB, uint32_t& sbits,
+                              T alpha) {
+  using U = typename FT<T>::U;
+  using VT = typename V16<T>::type;
+  constexpr int NV = V16<T>::N;
+  constexpr U kS = FT<T>::kSign;
+  int mism = 0;
+  int q = 0;
+  for (int i = tid; i < m; i += TB, ++q) {
+    VT* row = reinterpret_cast<VT*>(smem + Ly.v + 16 + (uint32_t)i * (uint32_t)(NCH * 16));
+    uint32_t& F = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
+    const uint32_t f = F;
+    uint32_t s;
+    if (FIRST) {
+      s = (f >> 1) & 1u;
+      sbits |= s << q;
+    } else {
+      s = (sbits >> q) & 1u;
+      mism |= (int)((f ^ s) & 1u);
+    }
+    F = f & 0xFFFF0000u;  // keep the row degree
+    const int deg = (int)(f >> 16);
+    U xb[NCH * NV];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const VT v = row[c];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) xb[c * NV + k] = FT<T>::bits(V16<T>::get(v, k));
+    }
+    U m1 = FT<T>::kSent, m2 = FT<T>::kSent;
+    U px = s ? kS : (U)0;
+#pragma unroll
+    for (int e = 0; e < NCH * NV; ++e) {
+      const U a = xb[e] & ~kS;
+      if constexpr (sizeof(U) == 4) {
+        m2 = med3u(m1, m2, a);
+      } else {
+        const U hi = m1 > a ? m1 : a;
+        m2 = m2 < hi ? m2 : hi;
+      }
+      m1 = m1 < a ? m1 : a;
+      px ^= xb[e];
+    }
+    // chunk swizzle of build_slot_edges (qldpc_hip.hip): physical chunk c holds logical chunk c ^ swz
+    const int swz = NCH == 2 ? ((i >> 3) & 1) : NCH == 4 ? ((i >> 2) & 3) : 0;
+    const T sm1 = FT<T>::val(m1) * alpha, sm2 = FT<T>::val(m2) * alpha;
+    const U b1 = FT<T>::bits(sm1), b2 = FT<T>::bits(sm2);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int lim = deg - (c ^ swz) * NV;  // slots k < lim of this chunk are real edges
+      U o[NV];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const U x = xb[c * NV + k];
+        const U sel = ((x & ~kS) == m1) ? b2 : b1;  // |c2v| = alpha * (min over the other edges)
+        const U cv = sel ^ ((px ^ x) & kS);         // sign = parity of the others and the syndrome
+        o[k] = k < lim ? cv : FT<T>::kSent;
+      }
+      VT w;
+      if constexpr (NV == 4) {
+        w = make_float4(FT<T>::val(o[0]), FT<T>::val(o[1]), FT<T>::val(o[2]), FT<T>::val(o[3]));
+      } else {
+        w = make_double2(FT<T>::val(o[0]), FT<T>::val(o[1]));
+      }
+      row[c] = w;
+    }
+  }
+  return mism;
+}
+
+template <typename T, int ENG>
+__device__ inline void r_fill(const SSector& S, unsigned char* smem, const RLayout& Ly, int vslots, int mmax, int tid,
+                              int TB) {
+  using VT = typename V16<T>::type;
+  VT* V4 = reinterpret_cast<VT*>(smem + Ly.v);
+  const VT s = V16<T>::splat(FT<T>::val(FT<T>::kSent));
+  // engine 4: the first chunk is the zero chunk missing edges read
+  for (int i = tid; i < vslots / V16<T>::N; i += TB) V4[i] = (ENG == 4 && i == 0) ? V16<T>::splat((T)0) : s;
+  uint32_t* F = reinterpret_cast<uint32_t*>(smem + Ly.f);
+  for (int i = tid; i <= mmax; i += TB) F[i] = (ENG == 4 && i >= 1 && i <= S.m) ? ((uint32_t)S.rdeg[i - 1] << 16) : 0u;
+  uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);
+  if (tid < 10) lred[tid] = 0;  // lred[0..7], flags[0..1]
+  if (ENG == 3 && tid == 0) {
+    Pair<T> z;
+    z.a = 0;
+    z.b = 0;
+    lds_at<Pair<T>>(smem, 0) = z;  // missing-edge dummy: c2v = ±0
+  }
+}
+
+// Engine 4 lays every row out as 8 slots (row degree <= 8): 2 chunks in fp32,
+// 4 in fp64 (one compile-time row width keeps the check phase's VGPRs low).
+template <typename T>
+constexpr int kRowChunks4 = 8 * (int)sizeof(T) / 16;
+template <typename T, bool FIRST>
+__device__ inline int c_check_any(unsigned char* smem, const RLayout& Ly, int m, int nch, int tid, int TB,
+                                  uint32_t& sbits, T alpha) {
+  (void)nch;  // == kRowChunks4<T> (host-enforced)
+  return c_check<T, FIRST, kRowChunks4<T>>(smem, Ly, m, tid, TB, sbits, alpha);
+}
+
+// One sector pass over `cn` shots (chunk-relative), one decode in flight.
+template <typename T, int DMAX, int VPL, bool MC, int ENG>
+__device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned char* smem, const RLayout& Ly,
+                       int vslots, int mmax, uint32_t* failmap, unsigned long long* cnt, const SMcArgs* A,
+                       const SDecArgs* D, int tid, int TB) {
+  using U = typename FT<T>::U;
+  constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
+  const int m = S.m, n = S.n, nch = S.nch;
+  RState<T, DMAX, VPL, ENG> R;
+  r_load<T, DMAX, VPL, ENG>(S, R, Ly, tid, TB);
+  r_fill<T, ENG>(S, smem, Ly, vslots, mmax, tid, TB);
+  FMap M;
+  M.fbase = ENG == 4 ? Ly.f + 4u : Ly.f;
+  M.rstart = Ly.v + 16u;
+  M.rsh = 4 + __builtin_ctz((unsigned)nch);
+  const uint32_t fdelta = Ly.f;
+  // waves whose lanes all hold padding variables skip the last variable (engine 4)
+  const bool last_live = uni((VPL - 1) * TB + (tid & ~63) < n ? 1 : 0) != 0;
+  uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);
+  uint32_t* flags = lred + 8;
+  const bool adaptive = S.alpha == 0.0;
+  const T alpha_fixed = (T)S.alpha;
+  __syncthreads();
+
+  int pshot = -1, pit = 0, pconv = 0;
+  for (int sh = 0; sh <= cn; ++sh) {
+    const bool have = sh < cn;
+    uint32_t eb = 0, sb = 0;
+    r_launder(R);
+    int tidl = tid;  // opaque copy: keeps per-variable addresses from being hoisted (VGPRs)
+    asm volatile("" : "+v"(tidl));
+    // ---------------------------------------------------------- priors / sampling
+    if (have) {
+#pragma unroll
+      for (int k = 0; k < VPL; ++k) {
+        const U cl = canon2<T>(R.L[k]);
+#pragma unroll
+        for (int t = 0; t < DMAX; ++t) {
+          lds_at<U>(smem, R.ea[k][t] >> 16) = cl;
+          if (KV) R.ov[KV ? k : 0][KV ? t : 0] = cl;
+        }
+      }
+      if (MC) {
+        // sample this shot's Pauli error (src/Simulators.py:99-113); stage s = H e in F bit1
+        const long long sl = c0 + sh;
+        const unsigned long long gshot = A->shot_begin + (unsigned long long)sl;
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+          const int j = k * TB + tidl;
+          if (j < n) {
+            uint32_t cls;
+            if (A->uniforms) {
+              const double u = A->uniforms[sl * (long long)n + j];
+              cls = (u < A->t1) ? 2u : (A->t1 <= u && u < A->t2) ? 1u : (A->t2 <= u && u < A->t3) ? 3u : 0u;
+            } else {
+              const unsigned long long kk = philox_k53(A->seed, gshot, (uint32_t)j);
+              cls = (kk < A->K1) ? 2u : (kk < A->K2) ? 1u : (kk < A->K3) ? 3u : 0u;
+            }
+            const uint32_t e = (q == 0) ? (cls & 1u) : (cls >> 1);
+            eb |= e << k;
+            if (A->err && q == A->sec_id0) A->err[sl * (long long)n + j] = (uint8_t)cls;
+            if (e) {
+#pragma unroll
+              for (int t = 0; t < DMAX; ++t) atomicXor(&lds_at<uint32_t>(smem, f_addr<T, ENG>(R.ea[k][t], M)), 2u);
+            }
+          }
+        }
+      } else {
+        const uint8_t* srow = D->synd + (c0 + sh) * (long long)m;
+        for (int i = tidl; i < m; i += TB) {
+          uint32_t& F = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
+          F = (ENG == 4 ? (F & 0xFFFF0000u) : 0u) | ((uint32_t)(srow[i] & 1u) << 1);
+        }
+      }
+    }
+    __syncthreads();
+    // ---------------------------------------------------------- finish the previous decode
+    if (pshot >= 0) {
+      uint32_t lf = 0;
+      if (MC) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) lf |= lred[w];
+      }
+      const int f = (!pconv || lf) ? 1 : 0;
+      if (tid == 0) {
+        const long long sl = c0 + pshot;
+        if (MC) {
+          if (f) failmap[pshot >> 5] |= 1u << (pshot & 31);
+          cnt[kCntDec + q] += 1;
+          cnt[kCntIters + q] += (unsigned long long)pit;
+          cnt[kCntNonconv + q] += pconv ? 0 : 1;
+          cnt[kCntSecFail + q] += (unsigned long long)f;
+          atomicAdd(&A->counters[kCntHist + q * kHistBins + (pit < kHistBins ? pit : kHistBins - 1)], 1ull);
+          if (A->iters) A->iters[sl * 2 + q] = pit;
+        } else {
+          if (D->iters) D->iters[sl] = pit;
+          if (D->conv) D->conv[sl] = pconv ? 1 : 0;
+        }
+      }
+    }
+    if (!have) break;
+    // ---------------------------------------------------------- first check pass (CS / c2v from priors)
+    if constexpr (ENG == 4)
+      c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
+    else
+      r_check<T, true>(smem, Ly, m, nch, tid, TB, sb);
+    __syncthreads();
+    if (tid < 10) lred[tid] = 0;  // lred read above (before the barrier); flags[0..1] start clear
+    // ---------------------------------------------------------- iterations
+    int it = 1;
+    bool conv = false;
+    uint32_t xb = 0;
+    while (true) {
+      int mism;
+      if constexpr (ENG == 4) {
+        xb = c_var<T, DMAX, VPL>(smem, R, M, last_live);
+        __syncthreads();
+        // c2v for iteration it + 1 (wasted if this one converged)
+        const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
+        mism = c_check_any<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha);
+      } else {
+        const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
+        xb = r_var<T, DMAX, VPL>(smem, R, fdelta, alpha);
+        __syncthreads();
+        mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb);
+      }
+      if (__any(mism) && (tid & 63) == 0) flags[it & 1] = 1u;
+      __syncthreads();
+      const int any = uni((int)flags[it & 1]);
+      if (tid == 0) flags[(it & 1) ^ 1] = 0;  // read by everyone before this barrier
+      conv = any == 0;
+      if (conv || it >= S.max_iter) break;
+      ++it;
+    }
+    const long long sl = c0 + sh;
+    if (MC) {
+      // residual r = e ^ x and its logical syndrome L r (src/Simulators.py:135-160)
+      const uint32_t r = eb ^ xb;
+      if (r) {
+        unsigned long long acc[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+          if ((r >> k) & 1u) {
+            const int j = k * TB + tidl;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+              if (w < S.kw) acc[w] ^= S.lmask[(long long)j * S.kw + w];
+          }
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          if ((uint32_t)acc[w]) atomicXor(&lred[2 * w], (uint32_t)acc[w]);
+          if ((uint32_t)(acc[w] >> 32)) atomicXor(&lred[2 * w + 1], (uint32_t)(acc[w] >> 32));
+        }
+      }
+      if (A->corr) {
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+          const int j = k * TB + tidl;
+          if (j < n) A->corr[(sl * 2 + q) * (long long)n + j] = (uint8_t)((xb >> k) & 1u);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < VPL; ++k) {
+        const int j = k * TB + tidl;
+        if (j < n) D->corr[sl * (long long)n + j] = (uint8_t)((xb >> k) & 1u);
+      }
+    }
+    pshot = sh;
+    pit = conv ? it : S.max_iter;
+    pconv = conv ? 1 : 0;
+  }
+  __syncthreads();  // image reused by the next pass
+}
+
+template <typename T, int DMAX, int VPL, int ENG>
+__global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, TB = blockDim.x;
+  const int CH = A.chunk;
+  const int fw = (CH + 31) / 32;
+  const RLayout Ly = r_layout(ENG, A.vslots, A.mmax, (int)sizeof(T));
+  uint32_t* fm0 = reinterpret_cast<uint32_t*>(smem + Ly.total);
+  uint32_t* fm1 = fm0 + ((fw + 3) & ~3);
+  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(fm1 + ((fw + 3) & ~3));
+  if (tid < kCntHist) cnt[tid] = 0;
+  const long long nchunks = (A.shot_count + CH - 1) / CH;
+  for (long long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const long long c0 = ch * CH;
+    const int cn = (int)(A.shot_count - c0 < CH ? A.shot_count - c0 : CH);
+    for (int i = tid; i < fw; i += TB) {
+      fm0[i] = 0;
+      fm1[i] = 0;
+    }
+    __syncthreads();
+    for (int qi = 0; qi < A.nsec; ++qi) {
+      const SSector S = pick_ssector(A, qi);
+      const int q = qi == 0 ? A.sec_id0 : A.sec_id1;
+      r_pass<T, DMAX, VPL, true, ENG>(S, q, c0, cn, smem, Ly, A.vslots, A.mmax, q == 0 ? fm0 : fm1, cnt, &A, nullptr,
+                                 tid, TB);
+    }
+    // combine the sectors per shot (eval_logical_type, src/Simulators.py:162-168)
+    unsigned long long nf = 0;
+    for (int j = tid; j < cn; j += TB) {
+      const uint32_t fx = (fm0[j >> 5] >> (j & 31)) & 1u, fz = (fm1[j >> 5] >> (j & 31)) & 1u;
+      const uint32_t f = A.logical_mode == 0 ? fx : A.logical_mode == 1 ? fz : (fx | fz);
+      nf += f;
+      if (A.fail) A.fail[c0 + j] = (uint8_t)(fx | (fz << 1));
+    }
+    if (nf) atomicAdd(&cnt[kCntFail], nf);
+    if (tid == 0) cnt[kCntShots] += (unsigned long long)cn;
+    __syncthreads();
+  }
+  __syncthreads();
+  if (tid < kCntHist && cnt[tid]) atomicAdd(&A.counters[tid], cnt[tid]);
+}
+
+template <typename T, int DMAX, int VPL, int ENG>
+__global__ __launch_bounds__(kMaxThreadsS) void rdec_kernel(SDecArgs D) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, TB = blockDim.x;
+  const int CH = D.chunk;
+  const RLayout Ly = r_layout(ENG, D.vslots, D.mmax, (int)sizeof(T));
+  const long long nchunks = (D.B + CH - 1) / CH;
+  for (long long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const long long c0 = ch * CH;
+    const int cn = (int)(D.B - c0 < CH ? D.B - c0 : CH);
+    r_pass<T, DMAX, VPL, false, ENG>(D.sec, 0, c0, cn, smem, Ly, D.vslots, D.mmax, nullptr, nullptr, nullptr, &D, tid,
+                                TB);
+  }
+}
+
+}  // namespace qldpc

@@ -43,6 +43,7 @@ struct SSector {
   const uint32_t* edges;            // [VPL][DMAX][TB]
   const void* llr;                  // T [VPL][TB]
   const unsigned long long* lmask;  // [n][kw] logical-row masks per column (MC only)
+  const uint8_t* rdeg;              // [m] row degrees (engine 4 only)
   int m, n, kw, max_iter, nch, vpl; // nch = 16-byte chunks per row; vpl = variables per thread
   double alpha;                     // 0 => 1 - 2^-iter
 };
@@ -461,6 +462,7 @@ __device__ inline SSector pick_ssector(const SMcArgs& A, int qi) {
   S.edges = b ? A.sec[1].edges : A.sec[0].edges;
   S.llr = b ? A.sec[1].llr : A.sec[0].llr;
   S.lmask = b ? A.sec[1].lmask : A.sec[0].lmask;
+  S.rdeg = b ? A.sec[1].rdeg : A.sec[0].rdeg;
   S.m = b ? A.sec[1].m : A.sec[0].m;
   S.n = b ? A.sec[1].n : A.sec[0].n;
   S.kw = b ? A.sec[1].kw : A.sec[0].kw;

@@ -1,10 +1,14 @@
 // qldpc_hip.hip — host runtime + C ABI (include/qldpc_hip.h) of the MI355X engine.
 //
 // Graph/decoder/MC handles own their device buffers; launches take a caller
-// stream.  Two kernel engines are built:
-//   engine 2 (default) — bp_slot.h: small workgroups with streamed variables,
+// stream.  Three kernel engines are built:
+//   engine 3 (default) — bp_reg.h: engine 2's LDS image with each thread's
+//                        variables (edge addresses, priors, own messages)
+//                        resident in VGPRs, compile-time VPL <= 8, column
+//                        degree <= 4 and an image addressable with 16 bits;
+//   engine 2           — bp_slot.h: small workgroups with streamed variables,
 //                        row-major v2c slots, check-centric gather, NS decodes
-//                        in flight per workgroup;
+//                        in flight per workgroup (any graph that fits LDS);
 //   engine 1           — bp_kernels.h: per-check LDS state updated by
 //                        returning LDS atomics (kept for A/B measurements,
 //                        selected with QLDPC_ENGINE=1).
@@ -85,7 +89,8 @@ struct qldpc_bp {
   int nch = 0;  // engine 2: 16-byte chunks per check row
   int lds_bytes = 0, blocks_per_cu = 0, cus = 0;
   std::vector<double> probs;
-  DevBuf vchk, llr;  // engine 1: packed u16 check ids; engine 2: edge words (check | slot<<16)
+  DevBuf vchk, llr;  // engine 1: packed u16 check ids; engines 2-4: edge words (check | slot<<16)
+  DevBuf rdeg;       // engine 4: u8 row degrees
 };
 
 struct qldpc_mc {
@@ -108,6 +113,16 @@ Variant get_variant(int precision, int vpl, int dmax) {
 SVariant get_svariant(int precision, int dmax, int ns) {
   if (precision == 32) return dmax == 4 ? get_svariant_f32_d4(ns) : get_svariant_f32_d8(ns);
   return dmax == 4 ? get_svariant_f64_d4(ns) : get_svariant_f64_d8(ns);
+}
+
+SVariant get_rvariant(int engine, int precision, int vpl) {
+  if (engine == 4) return precision == 32 ? get_r4variant_f32(vpl) : get_r4variant_f64(vpl);
+  return precision == 32 ? get_rvariant_f32(vpl) : get_rvariant_f64(vpl);
+}
+
+// Slot-family kernels of an engine (2, 3 or 4).
+SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl) {
+  return engine >= 3 ? get_rvariant(engine, precision, vpl) : get_svariant(precision, dmax, ns);
 }
 
 int round_up(int x, int a) { return (x + a - 1) / a * a; }
@@ -177,6 +192,42 @@ int choose_sgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
   if (VPL > kMaxVplS) return set_err(QLDPC_ENOTSUP, "more than 32 variables per thread (n > 32768)");
   if ((m + TB - 1) / TB > 32) return set_err(QLDPC_ENOTSUP, "too many checks per thread (m > 32*threads)");
   return 0;
+}
+
+// ---- engine 3 geometry: compile-time VPL <= 8.  Default: the TB (multiple of
+// 64) with the fewest padded variable slots VPL*TB, ties to the smaller TB;
+// QLDPC_TB or vars_per_thread override it.  Returns nonzero if engine 3 cannot
+// take the graph (the caller falls back to engine 2).
+constexpr int kMaxVplR = 8;
+int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
+  const int forced_tb = env_int("QLDPC_TB", 0);
+  if (requested_vpl > 0) {
+    VPL = requested_vpl;
+    TB = round_up((n + VPL - 1) / VPL, 64);
+  } else if (forced_tb > 0) {
+    TB = round_up(forced_tb, 64);
+    VPL = (n + TB - 1) / TB;
+  } else {
+    long best = -1;
+    for (int tb = 64; tb <= kMaxThreadsS; tb += 64) {
+      const int v = (n + tb - 1) / tb;
+      if (v > kMaxVplR || (m + tb - 1) / tb > 32) continue;
+      if (best < 0 || (long)v * tb < best) {
+        best = (long)v * tb;
+        TB = tb;
+        VPL = v;
+      }
+    }
+    if (best < 0) return 1;
+  }
+  if (TB > kMaxThreadsS || TB < 64 || VPL < 1 || VPL > kMaxVplR || (m + TB - 1) / TB > 32) return 1;
+  return 0;
+}
+
+// Engines 3 and 4 address their image with 16-bit byte offsets.
+bool r_fits(int eng, int vslots, int mmax, int tsize) {
+  const RLayout L = r_layout(eng, vslots, mmax, tsize);
+  return L.lred <= 65536u && r_lds_bytes((int)L.total, kChunkMax) <= (size_t)kLdsMax;
 }
 
 // Slots per workgroup: QLDPC_NS, else 1 (independent workgroups interleave
@@ -323,7 +374,8 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
   QLDPC_HIP(hipSetDevice(g->device));
   auto* bp = new qldpc_bp();
   bp->g = g;
-  bp->engine = env_int("QLDPC_ENGINE", 2) == 1 ? 1 : 2;
+  const int want_engine = env_int("QLDPC_ENGINE", 3);
+  bp->engine = (want_engine >= 1 && want_engine <= 4) ? want_engine : 3;
   bp->max_iter = max_iter > 0 ? max_iter : g->n;
   bp->method = bp_method;
   bp->alpha = ms_scaling_factor;
@@ -333,6 +385,7 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
   auto fail = [&](int code) {
     bp->vchk.release();
     bp->llr.release();
+    bp->rdeg.release();
     delete bp;
     return code;
   };
@@ -360,23 +413,42 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
     bp->lds_bytes = (int)lds_for(precision, g->m);
     kern = get_variant(precision, bp->VPL, DM).dec_k;
   } else {
-    rc = choose_sgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL);
-    if (rc) return fail(rc);
-    bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
+    if (bp->engine == 4 && g->max_row > 8) bp->engine = 3;  // engine 4 rows are 8 slots wide
+    bp->nch = bp->engine == 4 ? 8 * tsize / 16 : (std::max(1, g->max_row) * tsize + 15) / 16;
     const int vslots = (1 + g->m * bp->nch) * (16 / tsize);
     if (vslots >= 0xFFFF) return fail(set_err(QLDPC_ENOTSUP, "V image exceeds 65535 message slots"));
-    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, vchk);
-    const int img = (int)slot_img_bytes(vslots, g->m, tsize);
-    bp->NS = choose_ns(img);
-    bp->lds_bytes = (int)slot_lds_bytes(bp->NS, img, kChunkMax);
+    if (bp->engine >= 3 && (DM != 4 || choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL) ||
+                            !r_fits(bp->engine, vslots, g->m, tsize))) {
+      bp->engine = 2;  // graph outside the register engines' envelope
+      bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
+    }
+    const int vslots2 = (1 + g->m * bp->nch) * (16 / tsize);
+    if (bp->engine >= 3) {
+      bp->NS = 1;
+      bp->lds_bytes = (int)r_lds_bytes((int)r_layout(bp->engine, vslots2, g->m, tsize).total, kChunkMax);
+    } else {
+      rc = choose_sgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL);
+      if (rc) return fail(rc);
+      const int img = (int)slot_img_bytes(vslots2, g->m, tsize);
+      bp->NS = choose_ns(img);
+      bp->lds_bytes = (int)slot_lds_bytes(bp->NS, img, kChunkMax);
+    }
     if (bp->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB (use precision 32)"));
-    kern = get_svariant(precision, DM, bp->NS).dec_k;
+    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, vchk);
+    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL).dec_k;
   }
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
   if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)bp->VPL * bp->TB * tsize))) return fail(rc);
   if (hipMemcpy(bp->vchk.p, vchk.data(), vchk.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return fail(set_err(QLDPC_EHIP, "upload edge table"));
   if ((rc = upload_llr(bp))) return fail(rc);
+  if (bp->engine == 4) {
+    std::vector<uint8_t> deg(std::max(1, g->m));
+    for (int i = 0; i < g->m; ++i) deg[i] = (uint8_t)(g->row_ptr[i + 1] - g->row_ptr[i]);
+    if ((rc = bp->rdeg.alloc(deg.size()))) return fail(rc);
+    if (hipMemcpy(bp->rdeg.p, deg.data(), deg.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return fail(set_err(QLDPC_EHIP, "upload row degrees"));
+  }
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, bp->TB, bp->lds_bytes) != hipSuccess) nb = 1;
   bp->blocks_per_cu = std::max(1, nb);
@@ -389,6 +461,7 @@ int qldpc_bp_destroy(qldpc_bp* bp) {
   if (!bp) return 0;
   bp->vchk.release();
   bp->llr.release();
+  bp->rdeg.release();
   delete bp;
   return 0;
 }
@@ -397,6 +470,12 @@ int qldpc_bp_set_channel_probs(qldpc_bp* bp, const double* channel_probs) {
   if (!bp || !channel_probs) return set_err(QLDPC_EINVAL, "NULL argument");
   bp->probs.assign(channel_probs, channel_probs + bp->g->n);
   return upload_llr(bp);
+}
+
+int qldpc_bp_engine(const qldpc_bp* bp, int32_t* engine) {
+  if (!bp || !engine) return set_err(QLDPC_EINVAL, "NULL argument");
+  *engine = bp->engine;
+  return 0;
 }
 
 int qldpc_bp_geometry(const qldpc_bp* bp, int32_t* threads, int32_t* vpl, int32_t* lds_bytes,
@@ -427,6 +506,7 @@ static SSector ssector_of(const qldpc_bp* bp, const unsigned long long* lmask, i
   s.edges = static_cast<const uint32_t*>(bp->vchk.p);
   s.llr = bp->llr.p;
   s.lmask = lmask;
+  s.rdeg = static_cast<const uint8_t*>(bp->rdeg.p);
   s.m = bp->g->m;
   s.n = bp->g->n;
   s.kw = kw;
@@ -478,7 +558,7 @@ int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, 
     a.chunk = chunk_for(B, cap, bp->NS);
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
-    SVariant v = get_svariant(bp->precision, bp->DMAX, bp->NS);
+    SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;
@@ -543,9 +623,16 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
     for (qldpc_bp* d : {dec_x, dec_z})
       if (d) mc->vslots = std::max(mc->vslots, (1 + d->g->m * d->nch) * (16 / tsize));
     mc->img_bytes = (int)slot_img_bytes(mc->vslots, mc->mmax, tsize);
-    mc->NS = choose_ns(mc->img_bytes);
-    mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
-    kern = get_svariant(mc->precision, mc->DMAX, mc->NS).mc_k;
+    if (mc->engine >= 3) {
+      if (!r_fits(mc->engine, mc->vslots, mc->mmax, tsize))
+        return fail(set_err(QLDPC_ENOTSUP, "sector images exceed the register engines' 64 KiB addressing (QLDPC_ENGINE=2)"));
+      mc->NS = 1;
+      mc->lds_bytes = (int)r_lds_bytes((int)r_layout(mc->engine, mc->vslots, mc->mmax, tsize).total, kChunkMax);
+    } else {
+      mc->NS = choose_ns(mc->img_bytes);
+      mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
+    }
+    kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL).mc_k;
   }
   if (mc->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB"));
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
@@ -637,7 +724,7 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.fail = d_fail; a.err = d_err; a.corr = d_corr; a.iters = d_iters;
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
-    SVariant v = get_svariant(mc->precision, mc->DMAX, mc->NS);
+    SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL);
     QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;

@@ -3,9 +3,11 @@
 // build compiles them in parallel.
 //   v1 (bp_kernels.h): per-check LDS state updated by returning LDS atomics;
 //   v4 (bp_slot.h):    row-major v2c slots, check-centric gather, streamed
-//                      variables, NS shots in flight per workgroup (default).
+//                      variables, NS shots in flight per workgroup;
+//   v5 (bp_reg.h):     v4's LDS image with register-resident variables and
+//                      a compile-time VPL (default when the graph fits).
 #pragma once
-#include "bp_slot.h"
+#include "bp_reg.h"
 
 namespace qldpc {
 
@@ -32,6 +34,10 @@ Variant get_variant_f32_d4(int vpl);
 Variant get_variant_f32_d8(int vpl);
 Variant get_variant_f64_d4(int vpl);
 Variant get_variant_f64_d8(int vpl);
+SVariant get_rvariant_f32(int vpl);
+SVariant get_rvariant_f64(int vpl);
+SVariant get_r4variant_f32(int vpl);
+SVariant get_r4variant_f64(int vpl);
 SVariant get_svariant_f32_d4(int ns);
 SVariant get_svariant_f32_d8(int ns);
 SVariant get_svariant_f64_d4(int ns);
@@ -93,6 +99,37 @@ SVariant pick_sns(int ns) {
     case 1: return make_svariant<T, DMAX, 1>();
     case 2: return make_svariant<T, DMAX, 2>();
     case 4: return make_svariant<T, DMAX, 4>();
+    default: return SVariant{nullptr, nullptr, nullptr, nullptr};
+  }
+}
+
+template <typename T, int VPL, int ENG>
+hipError_t rlaunch_dec(dim3 g, dim3 b, size_t lds, hipStream_t s, const SDecArgs& a) {
+  hipLaunchKernelGGL((rdec_kernel<T, 4, VPL, ENG>), g, b, lds, s, a);
+  return hipGetLastError();
+}
+template <typename T, int VPL, int ENG>
+hipError_t rlaunch_mc(dim3 g, dim3 b, size_t lds, hipStream_t s, const SMcArgs& a) {
+  hipLaunchKernelGGL((rmc_kernel<T, 4, VPL, ENG>), g, b, lds, s, a);
+  return hipGetLastError();
+}
+template <typename T, int VPL, int ENG>
+SVariant make_rvariant() {
+  return SVariant{&rlaunch_dec<T, VPL, ENG>, &rlaunch_mc<T, VPL, ENG>,
+                  reinterpret_cast<const void*>(&rdec_kernel<T, 4, VPL, ENG>),
+                  reinterpret_cast<const void*>(&rmc_kernel<T, 4, VPL, ENG>)};
+}
+template <typename T, int ENG>
+SVariant pick_rvpl(int vpl) {
+  switch (vpl) {
+    case 1: return make_rvariant<T, 1, ENG>();
+    case 2: return make_rvariant<T, 2, ENG>();
+    case 3: return make_rvariant<T, 3, ENG>();
+    case 4: return make_rvariant<T, 4, ENG>();
+    case 5: return make_rvariant<T, 5, ENG>();
+    case 6: return make_rvariant<T, 6, ENG>();
+    case 7: return make_rvariant<T, 7, ENG>();
+    case 8: return make_rvariant<T, 8, ENG>();
     default: return SVariant{nullptr, nullptr, nullptr, nullptr};
   }
 }

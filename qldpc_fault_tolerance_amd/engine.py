@@ -104,7 +104,11 @@ class DeviceBP:
     def geometry(self):
         v = [ctypes.c_int32() for _ in range(4)]
         _native.check(_native.lib().qldpc_bp_geometry(self.handle, *[ctypes.byref(x) for x in v]), "bp_geometry")
-        return dict(zip(["threads", "vars_per_thread", "lds_bytes", "blocks_per_cu"], [x.value for x in v]))
+        e = ctypes.c_int32()
+        _native.check(_native.lib().qldpc_bp_engine(self.handle, ctypes.byref(e)), "bp_engine")
+        g = dict(zip(["threads", "vars_per_thread", "lds_bytes", "blocks_per_cu"], [x.value for x in v]))
+        g["engine"] = e.value
+        return g
 
     def decode_batch_device(self, synd_dev, corr_dev, iters_dev=None, conv_dev=None, stream=None):
         """Decode device uint8 syndromes [B, m] into device corrections [B, n] (async)."""

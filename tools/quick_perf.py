@@ -41,6 +41,6 @@ for prec in precs:
             ms = e0.elapsed_time(e1)
             w = cnt.cpu().numpy()
             its = w[4] / w[0]
-            print(f"{name} fp{prec} vpl={g['vars_per_thread']} TB={g['threads']} bpc={g['blocks_per_cu']} "
+            print(f"{name} e{g['engine']} fp{prec} vpl={g['vars_per_thread']} TB={g['threads']} bpc={g['blocks_per_cu']} "
                   f"grid={grid} p={p}: {S / ms * 1e3:,.0f} decodes/s  iters={its:.1f}  "
                   f"edge-iters/s={S * its * E / ms * 1e3:.3e}", flush=True)
