@@ -22,6 +22,9 @@ HIPCC_FLAGS = [
     # exact operation order is part of the contract (bit parity with the oracle):
     # no FMA contraction of the v2c sums / c2v products.
     "-ffp-contract=off",
+    # scalar f32 arithmetic: SLP-packed v_pk_add/mul plus their pairing moves
+    # cost more issue slots than they save in the BP loops (measured).
+    "-fno-slp-vectorize",
     "-I", os.path.join(REPO, "include"),
 ]
 

@@ -60,10 +60,13 @@ __device__ inline T& lds_at(unsigned char* smem, uint32_t off) {
 
 // canonical bits: |v| with the sign bit := (v <= 0).  Only +0 differs from the
 // raw bits (-0 and negatives already carry the sign bit; NaN never occurs).
+// Branch- and VCC-free form: b | ((b - 1) & ~b & sign) sets the sign bit only
+// for b == 0 (one add and one three-input bit op; no compare hazard nops).
 template <typename T>
 __device__ inline typename FT<T>::U canon2(T v) {
-  const typename FT<T>::U b = FT<T>::bits(v);
-  return b == 0 ? FT<T>::kSign : b;
+  using U = typename FT<T>::U;
+  const U b = FT<T>::bits(v);
+  return b | ((b - (U)1) & ~b & FT<T>::kSign);
 }
 
 // median of three (the backend selects v_med3_u32 for this pattern)
@@ -129,8 +132,11 @@ __device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
 }
 
 // Variable phase (one flooding iteration's column pass).  Returns decision bits.
+// F bit0 holds (H x)_i for the current decisions: only variables whose decision
+// flipped since the previous iteration (xprev) xor their checks.
 template <typename T, int DMAX, int VPL>
-__device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, uint32_t fdelta, T alpha) {
+__device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, uint32_t fdelta, T alpha,
+                                 uint32_t xprev, bool last_live) {
   using U = typename FT<T>::U;
   constexpr U kS = FT<T>::kSign;
   constexpr bool KV = RState<T, DMAX, VPL>::kKeepV;
@@ -159,6 +165,7 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, u
         if (!KV) on[t] = FT<T>::bits(lds_at<T>(smem, R.ea[k + 1][t] >> 16));
       }
     }
+    if (k == VPL - 1 && !last_live) break;  // every lane of this wave holds padding
     T c[DMAX];
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
@@ -193,7 +200,7 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, u
       lds_at<U>(smem, R.ea[k][t] >> 16) = nv[t];
       if (KV) R.ov[KV ? k : 0][KV ? t : 0] = nv[t];
     }
-    if (x) {
+    if (x != (((xprev >> k) & 1u) != 0)) {
 #pragma unroll
       for (int t = 0; t < DMAX; ++t)
         atomicXor(&lds_at<uint32_t>(smem, ((R.ea[k][t] & 0xFFFFu) >> (sizeof(T) == 4 ? 1 : 2)) + fdelta), 1u);
@@ -221,11 +228,11 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
     if (FIRST) {
       s = (f >> 1) & 1u;
       sbits |= s << q;
+      F = 0;  // H x starts at 0; the variable phases keep it current
     } else {
       s = (sbits >> q) & 1u;
       mism |= (int)((f ^ s) & 1u);
     }
-    F = 0;
     U m1 = FT<T>::kSent, m2 = FT<T>::kSent;
     U px = s ? kS : (U)0;
     for (int c = 0; c < nch; ++c) {
@@ -526,7 +533,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         mism = c_check_any<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha);
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
-        xb = r_var<T, DMAX, VPL>(smem, R, fdelta, alpha);
+        xb = r_var<T, DMAX, VPL>(smem, R, fdelta, alpha, xb, last_live);
         __syncthreads();
         mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb);
       }
