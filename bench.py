@@ -83,6 +83,16 @@ def cpu_baseline(code, eval_p, max_iter, logical, budget_s):
                       f"fp64 with {cores} OpenMP threads, {dt:.1f} s; LER={r['failures'] / S2:.4g}"}
 
 
+def kernel_name(dec):
+    """Name of the fused MC kernel the decoder's geometry selects (as rocprofv3 reports it)."""
+    g = dec.geometry()
+    t = "float" if dec.precision == 32 else "double"
+    dmax = 4 if dec.graph.info()["max_col_deg"] <= 4 else 8
+    if g["engine"] >= 3:
+        return f"qldpc::rmc_kernel<{t}, {dmax}, {g['vars_per_thread']}, {g['engine']}>"
+    return f"qldpc::smc_kernel<{t}, {dmax}, 1> (engine {g['engine']})"
+
+
 def measured_traffic(code, p, shots, logical, precision):
     """HBM bytes per launch measured by rocprofv3 PMC passes for this exact config (profiles/traffic.json)."""
     try:
@@ -200,7 +210,7 @@ def main():
                      "frac": achieved / LDS_PEAK_GBS,
                      "traffic": measured_traffic(a.code, p, S, a.logical, a.precision),
                      "hbm_peak": HBM_PEAK_GBS, "frac_of_hbm_peak": achieved / HBM_PEAK_GBS,
-                     "kernel": "qldpc::smc_kernel", "kernel_ms": kern_ms,
+                     "kernel": kernel_name(dx or dz), "kernel_ms": kern_ms,
                      "bytes_per_launch": bytes_per_launch},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -194,11 +194,15 @@ int choose_sgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
   return 0;
 }
 
-// ---- engine 3 geometry: compile-time VPL <= 8.  Default: the TB (multiple of
-// 64) with the fewest padded variable slots VPL*TB, ties to the smaller TB;
-// QLDPC_TB or vars_per_thread override it.  Returns nonzero if engine 3 cannot
-// take the graph (the caller falls back to engine 2).
+// ---- engine 3 geometry: compile-time VPL <= 8.  Default: the smallest
+// power-of-two TB (64..1024) with VPL = ceil(n / TB) <= 7 -- measured best or
+// within 4 % of the best on n126..n1600 (profiles/r01/geometry_sweep_e3.txt:
+// n1600 256x7, n625 128x5, n225 64x4, GBC A4 256x4, GBC A1 64x2; fewer,
+// longer threads win through the software-pipelined variable loop and shorter
+// check-phase tails).  QLDPC_TB or vars_per_thread override it.  Returns
+// nonzero if engine 3 cannot take the graph (the caller falls back to engine 2).
 constexpr int kMaxVplR = 8;
+constexpr int kPrefVplR = 7;
 int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
   const int forced_tb = env_int("QLDPC_TB", 0);
   if (requested_vpl > 0) {
@@ -208,17 +212,9 @@ int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
     TB = round_up(forced_tb, 64);
     VPL = (n + TB - 1) / TB;
   } else {
-    long best = -1;
-    for (int tb = 64; tb <= kMaxThreadsS; tb += 64) {
-      const int v = (n + tb - 1) / tb;
-      if (v > kMaxVplR || (m + tb - 1) / tb > 32) continue;
-      if (best < 0 || (long)v * tb < best) {
-        best = (long)v * tb;
-        TB = tb;
-        VPL = v;
-      }
-    }
-    if (best < 0) return 1;
+    TB = 64;
+    while (TB < kMaxThreadsS && ((n + TB - 1) / TB > kPrefVplR || (m + TB - 1) / TB > 32)) TB *= 2;
+    VPL = (n + TB - 1) / TB;
   }
   if (TB > kMaxThreadsS || TB < 64 || VPL < 1 || VPL > kMaxVplR || (m + TB - 1) / TB > 32) return 1;
   return 0;
