@@ -44,6 +44,7 @@ extern "C" {
 typedef struct qldpc_graph qldpc_graph;
 typedef struct qldpc_bp qldpc_bp;
 typedef struct qldpc_mc qldpc_mc;
+typedef struct qldpc_phenl qldpc_phenl;
 
 /* Counters of one fused Monte Carlo run (summed over calls if not reset). */
 typedef struct {
@@ -134,6 +135,41 @@ int qldpc_mc_launch(qldpc_mc *mc, double px, double py, double pz, uint64_t seed
 /* Synchronous convenience: launch + copy counters to host (accumulating into *out). */
 int qldpc_mc_run(qldpc_mc *mc, double px, double py, double pz, uint64_t seed, uint64_t shot_begin,
                  int64_t shot_count, int32_t logical_mode, qldpc_counters *out, void *stream);
+
+/*
+ * Phenomenological space-time shot loop = CodeSimulator_Phenon_SpaceTime
+ * (src/Simulators_SpaceTime.py:382-548): per sample, num_rounds - 1 noisy
+ * rounds of num_rep repetitions (fresh depolarizing data error + syndrome
+ * flips with probability q, :395-431), each decoded by BP on the stacked
+ * space-time graph (ST_BP_Decoder_syndrome, src/Decoders_SpaceTime.py:200-223)
+ * from its detector history (Z sector differenced, X sector raw: quirk Q3,
+ * :464-476), then a perfect final round decoded by dec2 and the failure check
+ * of :500-529.
+ *   st_x / st_z   : decoders on GetSpaceTimeCheckMat(hz / hx, num_rep)
+ *                   (checked against the final decoders' graphs);
+ *   dec2_x/dec2_z : final-round decoders on hz / hx;
+ *   logical_x/_z  : lz / lx.
+ *   max_batch     : samples in flight per pass (0 = 65536); device buffers
+ *                   are sized for it at create time.
+ * Both sectors are required (the uniform stream interleaves both check sets).
+ */
+int qldpc_phenl_create(qldpc_bp *st_x, qldpc_bp *st_z, qldpc_bp *dec2_x, qldpc_bp *dec2_z,
+                       const qldpc_graph *logical_x, const qldpc_graph *logical_z, int32_t num_rep, int64_t max_batch,
+                       qldpc_phenl **out);
+int qldpc_phenl_destroy(qldpc_phenl *ph);
+/* Bytes per sample of the optional trace: per noisy round the Z then X
+ * detector histories ([num_rep][m_x], [num_rep][m_z]), then the final Z and X
+ * syndromes. */
+int qldpc_phenl_trace_len(const qldpc_phenl *ph, int32_t num_rounds, int64_t *out);
+/* Async launch on `stream`; counters accumulate into d_counters (device
+ * qldpc_counters, zeroed by the caller; sector_* count the ST and final
+ * decodes).  Sample s uses global index shot_begin + s for its Philox stream,
+ * or d_uniforms[s][n_u] (n_u = ((num_rounds-1)*num_rep + 1)*(n + m_x + m_z),
+ * CPython's draw order) when non-NULL.  d_fail uint8 [S] (bit0 X, bit1 Z) and
+ * d_trace uint8 [S][trace_len] are optional. */
+int qldpc_phenl_launch(qldpc_phenl *ph, double px, double py, double pz, double q, uint64_t seed,
+                       uint64_t shot_begin, int64_t shot_count, int32_t num_rounds, int32_t logical_mode,
+                       const double *d_uniforms, void *d_counters, uint8_t *d_fail, uint8_t *d_trace, void *stream);
 
 /* Launch geometry chosen for a decoder (threads per shot, vars per thread,
  * LDS bytes, resident blocks per CU) — reported by bench.py / DESIGN.md. */

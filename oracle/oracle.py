@@ -154,3 +154,70 @@ def mc_run(code, px, py, pz, seed, shot_begin, shot_count, logical_mode="X", max
     if per_shot:
         out.update(fail=fail, err=err, corr=corr, iters=iters)
     return out
+
+
+STREAM_PHEN = 0x51D50002
+
+
+def phenl_trace_len(code, num_rep, num_rounds):
+    mx, mz = code.hx.shape[0], code.hz.shape[0]
+    return (num_rounds - 1) * num_rep * (mx + mz) + mx + mz
+
+
+def phenl_run(code, px, py, pz, q, seed, shot_begin, shot_count, num_rounds, num_rep, logical_mode="Total",
+              p_data=None, p_synd=None, max_iter_st=None, max_iter_2=None, bp_method="minimum_sum",
+              ms_scaling_factor=0.625, precision=64, uniforms=None, per_shot=False, nthreads=0):
+    """Phenomenological space-time shot loop on the CPU (CodeSimulator_Phenon_SpaceTime restated)."""
+    n = code.N
+    hz, lz, hx, lx = code.csr("hz"), code.csr("lz"), code.csr("hx"), code.csr("lx")
+    mz, mx = hz.m, hx.m
+    if p_data is None:
+        p_data = px + py
+    if p_synd is None:
+        p_synd = p_data
+    if max_iter_st is None:
+        max_iter_st = int(n / 10)
+    if max_iter_2 is None:
+        max_iter_2 = int(n / 10)
+    pst_x = np.ascontiguousarray(np.hstack([p_data * np.ones(n), p_synd * np.ones(mz)] * num_rep))
+    pst_z = np.ascontiguousarray(np.hstack([p_data * np.ones(n), p_synd * np.ones(mx)] * num_rep))
+    p2 = np.ascontiguousarray(p_data * np.ones(n))
+    mode = {"X": 0, "Z": 1, "Total": 2}[logical_mode]
+    S = int(shot_count)
+    tl = phenl_trace_len(code, num_rep, num_rounds)
+    fail = trace = None
+    if per_shot:
+        fail = np.zeros(S, np.uint8)
+        trace = np.zeros((S, tl), np.uint8)
+    if uniforms is not None:
+        uniforms = np.ascontiguousarray(uniforms, np.float64)
+        assert uniforms.shape == (S, ((num_rounds - 1) * num_rep + 1) * (n + mx + mz))
+    cnt = Counters()
+
+    def p(a, t):
+        return a.ctypes.data_as(ctypes.POINTER(t)) if a is not None else None
+
+    i32, f64 = ctypes.c_int32, ctypes.c_double
+    keep = [np.ascontiguousarray(a, np.int32) for a in
+            (hz.row_ptr, hz.col_idx, lz.row_ptr, lz.col_idx, hx.row_ptr, hx.col_idx, lx.row_ptr, lx.col_idx)]
+    L = lib()
+    L.oracle_phenl_run.restype = ctypes.c_int
+    rc = L.oracle_phenl_run(
+        ctypes.c_int(n),
+        ctypes.c_int(mz), p(keep[0], i32), p(keep[1], i32),
+        ctypes.c_int(lz.m), p(keep[2], i32), p(keep[3], i32),
+        ctypes.c_int(mx), p(keep[4], i32), p(keep[5], i32),
+        ctypes.c_int(lx.m), p(keep[6], i32), p(keep[7], i32),
+        p(pst_x, f64), p(pst_z, f64), p(p2, f64), p(p2, f64),
+        ctypes.c_int(num_rep), ctypes.c_int(int(max_iter_st)), ctypes.c_int(int(max_iter_2)),
+        ctypes.c_int(METHODS[bp_method]), f64(ms_scaling_factor), ctypes.c_int(precision),
+        f64(px), f64(py), f64(pz), f64(q), ctypes.c_uint64(seed), ctypes.c_uint64(shot_begin), ctypes.c_int64(S),
+        ctypes.c_int(num_rounds), ctypes.c_int(mode), p(uniforms, f64), ctypes.byref(cnt),
+        p(fail, ctypes.c_uint8), p(trace, ctypes.c_uint8), ctypes.c_int(int(nthreads)))
+    del keep
+    if rc:
+        raise RuntimeError("oracle_phenl_run failed")
+    out = cnt.as_dict()
+    if per_shot:
+        out.update(fail=fail, trace=trace)
+    return out

@@ -420,3 +420,199 @@ ORACLE_API int oracle_mc_run(int n,
     if (out) *out = tot;
     return rc ? -1 : 0;
 }
+
+/* ------------------------------------------- phenomenological space-time */
+#define QLDPC_STREAM_PHEN 0x51D50002u
+
+/* GetSpaceTimeCheckMat(h, reps) as CSR (src/Decoders_SpaceTime.py:179-194):
+ * row block i = [h | I] on column block i, [0 | I] on column block i-1. */
+static int st_graph(int m, int n, const int32_t *rp, const int32_t *ci, int reps, int32_t **orp, int32_t **oci) {
+    int w = n + m, E = 0;
+    int32_t *r = (int32_t *)malloc(sizeof(int32_t) * ((size_t)reps * m + 1));
+    int32_t *c = (int32_t *)malloc(sizeof(int32_t) * ((size_t)reps * (rp[m] + 2 * m) + 1));
+    if (!r || !c) { free(r); free(c); return -1; }
+    r[0] = 0;
+    for (int i = 0; i < reps; i++)
+        for (int a = 0; a < m; a++) {
+            if (i > 0) c[E++] = (i - 1) * w + n + a;
+            for (int e = rp[a]; e < rp[a + 1]; e++) c[E++] = i * w + ci[e];
+            c[E++] = i * w + n + a;
+            r[i * m + a + 1] = E;
+        }
+    *orp = r; *oci = c;
+    return 0;
+}
+
+static void csr_mulvec(const int32_t *rp, const int32_t *ci, int m, const uint8_t *x, uint8_t *y) {
+    for (int i = 0; i < m; i++) {
+        uint8_t a = 0;
+        for (int e = rp[i]; e < rp[i + 1]; e++) a ^= x[ci[e]];
+        y[i] = a;
+    }
+}
+
+/*
+ * CodeSimulator_Phenon_SpaceTime._single_run (src/Simulators_SpaceTime.py:433-529)
+ * for shot_count samples, with ST_BP_Decoder_syndrome as decoder1
+ * (src/Decoders_SpaceTime.py:200-223) and BPDecoder as decoder2.  Sector 0 = X
+ * errors (hz, lz), sector 1 = Z errors (hx, lx).  Per repetition the uniforms
+ * are drawn in the reference's order: n data qubits (3-way split, :408-422),
+ * m_x flips of the hx syndrome (Z sector, :425-427), m_z flips of the hz
+ * syndrome (X sector, :429-431); uniform index ((r*reps + j)*P + p), P = n+m_x+m_z.
+ * probs_st_*: [reps*(n+m)] ST priors; probs2_*: [n].  trace_out: per sample,
+ * per noisy round the Z then X detector histories, then the final Z then X
+ * syndromes (the arrays the decoders are handed).
+ */
+ORACLE_API int oracle_phenl_run(int n,
+                                int mz, const int32_t *hz_rp, const int32_t *hz_ci,
+                                int kx, const int32_t *lz_rp, const int32_t *lz_ci,
+                                int mx, const int32_t *hx_rp, const int32_t *hx_ci,
+                                int kz, const int32_t *lx_rp, const int32_t *lx_ci,
+                                const double *probs_st_x, const double *probs_st_z,
+                                const double *probs2_x, const double *probs2_z,
+                                int reps, int max_iter_st, int max_iter_2, int method, double alpha, int precision,
+                                double px, double py, double pz, double q, uint64_t seed, uint64_t shot_begin,
+                                int64_t shot_count, int num_rounds, int logical_mode, const double *uniforms,
+                                oracle_counters_t *out, uint8_t *fail_out, uint8_t *trace_out, int nthreads) {
+    const int m[2] = {mz, mx};
+    const int32_t *hrp[2] = {hz_rp, hx_rp}, *hci[2] = {hz_ci, hx_ci};
+    const int32_t *lrp[2] = {lz_rp, lx_rp}, *lci[2] = {lz_ci, lx_ci};
+    const int kk[2] = {kx, kz};
+    const double *pst[2] = {probs_st_x, probs_st_z}, *p2[2] = {probs2_x, probs2_z};
+    graph_t G2[2], GS[2];
+    int32_t *srp[2] = {0, 0}, *sci[2] = {0, 0};
+    for (int s = 0; s < 2; s++) {
+        if (graph_init(&G2[s], m[s], n, hrp[s], hci[s])) return -1;
+        if (st_graph(m[s], n, hrp[s], hci[s], reps, &srp[s], &sci[s])) return -1;
+        if (graph_init(&GS[s], reps * m[s], reps * (n + m[s]), srp[s], sci[s])) return -1;
+    }
+    /* ldpc's max_iter = 0 means the decoder's own n (ST: reps*(n+m) of that sector) */
+    bp_params_t PSs[2] = {{norm_max_iter(max_iter_st, GS[0].n), method, alpha},
+                          {norm_max_iter(max_iter_st, GS[1].n), method, alpha}};
+    bp_params_t P2 = {norm_max_iter(max_iter_2, n), method, alpha};
+    const int need[2] = {logical_mode != 1, logical_mode != 0};
+    const double t1 = pz, t2 = pz + px, t3 = (pz + px) + py;
+    const int Pw = n + mx + mz;
+    const int64_t nu = ((int64_t)(num_rounds - 1) * reps + 1) * Pw;
+    const int64_t tlen = (int64_t)(num_rounds - 1) * reps * (mx + mz) + mx + mz;
+    oracle_counters_t tot;
+    memset(&tot, 0, sizeof(tot));
+    int rc = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads) reduction(| : rc)
+#endif
+    {
+        int tid = 0, nth = 1;
+#ifdef _OPENMP
+        tid = omp_get_thread_num(); nth = omp_get_num_threads();
+#endif
+        oracle_counters_t loc; memset(&loc, 0, sizeof(loc));
+        ws_f64 w64s[2], w64f[2]; ws_f32 w32s[2], w32f[2];
+        int mm = mx > mz ? mx : mz;
+        uint8_t *cur[2], *hist[2], *det = (uint8_t *)malloc((size_t)reps * mm + 1);
+        uint8_t *ser[2], *syn = (uint8_t *)malloc((size_t)mm + 1), *chk = (uint8_t *)malloc((size_t)mm + 1);
+        uint8_t *r = (uint8_t *)malloc((size_t)n);
+        for (int s = 0; s < 2; s++) {
+            cur[s] = (uint8_t *)malloc((size_t)n);
+            hist[s] = (uint8_t *)malloc((size_t)reps * m[s] + 1);
+            ser[s] = (uint8_t *)malloc((size_t)m[s] + 1);
+            if (precision == 32) {
+                if (ws_alloc_f32(&w32s[s], &GS[s]) || ws_alloc_f32(&w32f[s], &G2[s])) rc |= 1;
+                else { ws_priors_f32(&w32s[s], &GS[s], pst[s]); ws_priors_f32(&w32f[s], &G2[s], p2[s]); }
+            } else {
+                if (ws_alloc_f64(&w64s[s], &GS[s]) || ws_alloc_f64(&w64f[s], &G2[s])) rc |= 1;
+                else { ws_priors_f64(&w64s[s], &GS[s], pst[s]); ws_priors_f64(&w64f[s], &G2[s], p2[s]); }
+            }
+        }
+        int64_t lo = shot_count * tid / nth, hi = shot_count * (tid + 1) / nth;
+        for (int64_t b = lo; b < hi && !rc; b++) {
+            const uint64_t shot = shot_begin + (uint64_t)b;
+            uint8_t *tr = trace_out ? trace_out + b * tlen : NULL;
+#define U(idx) (uniforms ? uniforms[b * nu + (idx)] : oracle_uniform(seed, shot, (uint32_t)(idx), QLDPC_STREAM_PHEN))
+            memset(cur[0], 0, (size_t)n); memset(cur[1], 0, (size_t)n);
+            for (int rd = 0; rd + 1 < num_rounds; rd++) {
+                for (int j = 0; j < reps; j++) {
+                    const int64_t base = ((int64_t)rd * reps + j) * Pw;
+                    for (int p = 0; p < n; p++) {
+                        int c = classify(U(base + p), t1, t2, t3);
+                        cur[0][p] ^= (uint8_t)(c & 1); cur[1][p] ^= (uint8_t)(c >> 1);
+                    }
+                    for (int i = 0; i < mx; i++) ser[1][i] = U(base + n + i) < q;
+                    for (int i = 0; i < mz; i++) ser[0][i] = U(base + n + mx + i) < q;
+                    for (int s = 0; s < 2; s++) {  /* synd = h_ext @ [cur | serr] */
+                        csr_mulvec(hrp[s], hci[s], m[s], cur[s], syn);
+                        for (int i = 0; i < m[s]; i++) hist[s][j * m[s] + i] = syn[i] ^ ser[s][i];
+                    }
+                }
+                for (int s = 1; s >= 0; s--) {  /* decoder1_z then decoder1_x, :478-481 */
+                    const int R = reps * m[s];
+                    for (int k = 0; k < R; k++)  /* Z: consecutive differences; X: raw (quirk Q3) */
+                        det[k] = (s == 1 && k >= m[s]) ? (uint8_t)(hist[s][k] ^ hist[s][k - m[s]]) : hist[s][k];
+                    if (tr && need[s]) memcpy(tr, det, (size_t)R);  /* skipped sectors: bytes untouched */
+                    if (tr) tr += R;
+                    if (!need[s]) continue;
+                    int it, conv; const uint8_t *e;
+                    if (precision == 32) { conv = bp_run_f32(&GS[s], &PSs[s], &w32s[s], det, &it); e = w32s[s].dec; }
+                    else { conv = bp_run_f64(&GS[s], &PSs[s], &w64s[s], det, &it); e = w64s[s].dec; }
+                    loc.sector_decodes[s]++; loc.sector_iters[s] += it; loc.sector_nonconv[s] += !conv;
+                    const int w = n + m[s];
+                    for (int i = 0; i < reps; i++)  /* fold, src/Decoders_SpaceTime.py:218-223 */
+                        for (int p = 0; p < n; p++) cur[s][p] ^= e[i * w + p];
+                }
+            }
+            {   /* final perfect round, :483-529 */
+                const int64_t base = (int64_t)(num_rounds - 1) * reps * Pw;
+                for (int p = 0; p < n; p++) {
+                    int c = classify(U(base + p), t1, t2, t3);
+                    cur[0][p] ^= (uint8_t)(c & 1); cur[1][p] ^= (uint8_t)(c >> 1);
+                }
+            }
+            int fs[2] = {0, 0};
+            for (int s = 1; s >= 0; s--) {
+                csr_mulvec(hrp[s], hci[s], m[s], cur[s], syn);
+                if (tr && need[s]) memcpy(tr, syn, (size_t)m[s]);
+                if (tr) tr += m[s];
+                if (!need[s]) continue;
+                int it, conv; const uint8_t *e;
+                if (precision == 32) { conv = bp_run_f32(&G2[s], &P2, &w32f[s], syn, &it); e = w32f[s].dec; }
+                else { conv = bp_run_f64(&G2[s], &P2, &w64f[s], syn, &it); e = w64f[s].dec; }
+                loc.sector_decodes[s]++; loc.sector_iters[s] += it; loc.sector_nonconv[s] += !conv;
+                for (int p = 0; p < n; p++) r[p] = cur[s][p] ^ e[p];
+                csr_mulvec(hrp[s], hci[s], m[s], r, chk);
+                int f = 0;
+                for (int i = 0; i < m[s] && !f; i++) f = chk[i];
+                for (int l = 0; l < kk[s] && !f; l++) {
+                    uint8_t a = 0;
+                    for (int k = lrp[s][l]; k < lrp[s][l + 1]; k++) a ^= r[lci[s][k]];
+                    f = a;
+                }
+                fs[s] = f;
+                loc.sector_fail[s] += f;
+            }
+#undef U
+            int f = logical_mode == 0 ? fs[0] : logical_mode == 1 ? fs[1] : (fs[0] || fs[1]);
+            loc.shots++; loc.failures += f;
+            if (fail_out) fail_out[b] = (uint8_t)(fs[0] | (fs[1] << 1));
+        }
+        for (int s = 0; s < 2; s++) {
+            if (precision == 32) { ws_free_f32(&w32s[s]); ws_free_f32(&w32f[s]); }
+            else { ws_free_f64(&w64s[s]); ws_free_f64(&w64f[s]); }
+            free(cur[s]); free(hist[s]); free(ser[s]);
+        }
+        free(det); free(syn); free(chk); free(r);
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        {
+            tot.shots += loc.shots; tot.failures += loc.failures;
+            for (int s = 0; s < 2; s++) {
+                tot.sector_decodes[s] += loc.sector_decodes[s]; tot.sector_iters[s] += loc.sector_iters[s];
+                tot.sector_nonconv[s] += loc.sector_nonconv[s]; tot.sector_fail[s] += loc.sector_fail[s];
+            }
+        }
+    }
+    for (int s = 0; s < 2; s++) { graph_free(&G2[s]); graph_free(&GS[s]); free(srp[s]); free(sci[s]); }
+    if (out) *out = tot;
+    return rc ? -1 : 0;
+}

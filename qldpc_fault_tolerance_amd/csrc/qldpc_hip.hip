@@ -26,41 +26,14 @@
 
 #include "../../include/qldpc_hip.h"
 #include "variants.h"
+#include "runtime.h"
 
 using namespace qldpc;
+using namespace qldpc_rt;
+
+thread_local std::string qldpc_rt::g_err;
 
 namespace {
-
-thread_local std::string g_err;
-
-int set_err(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
-
-#define QLDPC_HIP(x)                                                                        \
-  do {                                                                                      \
-    hipError_t e_ = (x);                                                                    \
-    if (e_ != hipSuccess) return set_err(QLDPC_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-  int alloc(size_t b) {
-    bytes = b;
-    if (b == 0) return 0;
-    if (hipMalloc(&p, b) != hipSuccess) {
-      p = nullptr;
-      return set_err(QLDPC_ENOMEM, "hipMalloc failed");
-    }
-    return 0;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-  }
-};
 
 const int kVplSet[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12};
 constexpr int kLdsMax = 160 * 1024;
@@ -72,35 +45,6 @@ int env_int(const char* name, int dflt) {
 }
 
 }  // namespace
-
-struct qldpc_graph {
-  int device = 0;
-  int m = 0, n = 0, nnz = 0, max_row = 0, max_col = 0;
-  std::vector<int32_t> row_ptr, col_idx;
-  std::vector<std::vector<int32_t>> col_rows;  // rows of each column, ascending
-};
-
-struct qldpc_bp {
-  qldpc_graph* g = nullptr;
-  int engine = 2;
-  int max_iter = 0, method = 1, precision = 64;
-  double alpha = 0.625;
-  int TB = 64, VPL = 1, DMAX = 4, NS = 1;
-  int nch = 0;  // engine 2: 16-byte chunks per check row
-  int lds_bytes = 0, blocks_per_cu = 0, cus = 0;
-  std::vector<double> probs;
-  DevBuf vchk, llr;  // engine 1: packed u16 check ids; engines 2-4: edge words (check | slot<<16)
-  DevBuf rdeg;       // engine 4: u8 row degrees
-};
-
-struct qldpc_mc {
-  qldpc_bp* dec[2] = {nullptr, nullptr};
-  int kw[2] = {0, 0};
-  DevBuf lmask[2];
-  DevBuf counters;
-  int engine = 2, TB = 0, VPL = 0, DMAX = 0, NS = 1, precision = 64, lds_bytes = 0, blocks_per_cu = 0, cus = 0;
-  int mmax = 0, vslots = 0, img_bytes = 0;
-};
 
 // --------------------------------------------------------------- dispatch
 namespace {
@@ -248,7 +192,7 @@ extern "C" {
 
 int qldpc_abi_version(void) { return QLDPC_ABI_VERSION; }
 
-const char* qldpc_last_error(void) { return g_err.c_str(); }
+const char* qldpc_last_error(void) { return qldpc_rt::g_err.c_str(); }
 
 int qldpc_device_count(int* out) {
   if (!out) return set_err(QLDPC_EINVAL, "out is NULL");

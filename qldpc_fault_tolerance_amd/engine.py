@@ -157,6 +157,7 @@ class MCResult:
     err: np.ndarray | None = None
     corr: np.ndarray | None = None
     iters: np.ndarray | None = None
+    trace: np.ndarray | None = None
 
     @staticmethod
     def from_words(w: np.ndarray) -> "MCResult":
@@ -242,4 +243,86 @@ class DeviceMC:
         h = getattr(self, "handle", None)
         if h and _native._lib is not None:
             _native.lib().qldpc_mc_destroy(h)
+            self.handle = None
+
+
+class DevicePhenl:
+    """Phenomenological space-time shot loop of ``CodeSimulator_Phenon_SpaceTime`` on one GPU (``qldpc_phenl_*``).
+
+    ``st_x`` / ``st_z`` decode the X / Z detector histories on the space-time
+    graphs of hz / hx; ``dec2_x`` / ``dec2_z`` decode the perfect final round.
+    """
+
+    def __init__(self, code: CSSCode, st_x: DeviceBP, st_z: DeviceBP, dec2_x: DeviceBP, dec2_z: DeviceBP,
+                 num_rep: int, max_batch: int = 0):
+        self.code = code
+        self.num_rep = int(num_rep)
+        self.decoders = (st_x, st_z, dec2_x, dec2_z)
+        dev = dec2_x.graph.device
+        self.device = dev
+        self.lz = DeviceGraph(code.csr("lz"), device=dev)
+        self.lx = DeviceGraph(code.csr("lx"), device=dev)
+        h = ctypes.c_void_p()
+        _native.check(_native.lib().qldpc_phenl_create(
+            st_x.handle, st_z.handle, dec2_x.handle, dec2_z.handle, self.lz.handle, self.lx.handle, self.num_rep,
+            int(max_batch), ctypes.byref(h)), "qldpc_phenl_create")
+        self.handle = h
+
+    def trace_len(self, num_rounds: int) -> int:
+        v = ctypes.c_int64()
+        _native.check(_native.lib().qldpc_phenl_trace_len(self.handle, int(num_rounds), ctypes.byref(v)),
+                      "qldpc_phenl_trace_len")
+        return v.value
+
+    def uniforms_per_sample(self, num_rounds: int) -> int:
+        c = self.code
+        return ((num_rounds - 1) * self.num_rep + 1) * (c.N + c.hx.shape[0] + c.hz.shape[0])
+
+    def new_counters(self):
+        torch = _torch()
+        return torch.zeros(_native.COUNTER_WORDS, dtype=torch.int64, device=torch.device("cuda", self.device))
+
+    def launch(self, px, py, pz, q, seed, shot_begin, shot_count, num_rounds, logical_mode="Total", counters=None,
+               uniforms=None, fail=None, trace=None, stream=None):
+        torch = _torch()
+        if counters is None:
+            raise ValueError("counters buffer required")
+        mode = LOGICAL_MODES[logical_mode] if isinstance(logical_mode, str) else int(logical_mode)
+        s = stream if stream is not None else _stream_handle(torch, counters.device)
+
+        def ptr(t):
+            return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+        _native.check(_native.lib().qldpc_phenl_launch(
+            self.handle, float(px), float(py), float(pz), float(q), int(seed) & (2**64 - 1), int(shot_begin),
+            int(shot_count), int(num_rounds), mode, ptr(uniforms), ptr(counters), ptr(fail), ptr(trace), s),
+            "qldpc_phenl_launch")
+
+    def run(self, px, py, pz, q, seed, shot_begin, shot_count, num_rounds, logical_mode="Total", uniforms=None,
+            per_shot=False) -> MCResult:
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        S = int(shot_count)
+        cnt = self.new_counters()
+        u = None
+        if uniforms is not None:
+            u = torch.from_numpy(np.ascontiguousarray(uniforms, dtype=np.float64)).to(dev)
+            if tuple(u.shape) != (S, self.uniforms_per_sample(num_rounds)):
+                raise ValueError(f"uniforms must be [{S}, {self.uniforms_per_sample(num_rounds)}]")
+        f = tr = None
+        if per_shot:
+            f = torch.zeros(S, dtype=torch.uint8, device=dev)
+            tr = torch.zeros((S, self.trace_len(num_rounds)), dtype=torch.uint8, device=dev)
+        self.launch(px, py, pz, q, seed, shot_begin, S, num_rounds, logical_mode, cnt, u, f, tr)
+        torch.cuda.synchronize(dev)
+        res = MCResult.from_words(cnt.cpu().numpy())
+        if per_shot:
+            res.fail = f.cpu().numpy()
+            res.trace = tr.cpu().numpy()
+        return res
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _native._lib is not None:
+            _native.lib().qldpc_phenl_destroy(h)
             self.handle = None

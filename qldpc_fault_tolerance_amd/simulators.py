@@ -181,6 +181,133 @@ class CodeSimulator_DataError:
         return word_error_rate(error_count, num_run, self.K)
 
 
+class CodeSimulator_Phenon_SpaceTime:
+    """Phenomenological space-time simulator (``src/Simulators_SpaceTime.py:382-548``).
+
+    ``WordErrorRate(num_cycles, num_samples)`` returns ``(wer, None)`` with the
+    reference's per-cycle formula.  When decoder1_* are this engine's
+    :class:`~.decoders.ST_BP_Decoder_syndrome` and decoder2_* its
+    :class:`~.decoders.BPDecoder`, all samples run on the GPU
+    (``qldpc_phenl_launch``: bit-sliced ballot sampling and syndromes, batched
+    space-time BP, fold, final round, failure check), sharded over the
+    ``torch.distributed`` ranks with one counter all-reduce.  Other decoders run
+    the reference's per-sample ``_single_run`` loop.
+    """
+
+    def __init__(self, code=None, decoder1_x=None, decoder1_z=None, decoder2_x=None, decoder2_z=None,
+                 pauli_error_probs=(0.01, 0.01, 0.01), q=0, eval_logical_type="Total", num_rep=1, seed=None,
+                 max_batch=0):
+        self.code = code
+        self.hx_ext = np.hstack([code.hx, np.identity(np.shape(code.hx)[0])])
+        self.hz_ext = np.hstack([code.hz, np.identity(np.shape(code.hz)[0])])
+        self.decoder1_z, self.decoder1_x = decoder1_z, decoder1_x
+        self.decoder2_z, self.decoder2_x = decoder2_z, decoder2_x
+        self.N = code.N
+        self.K = code.K
+        self.channel_probs = list(pauli_error_probs)
+        self.synd_prob = q
+        self.min_logical_weight = self.N
+        self.eval_logical_type = eval_logical_type
+        self.num_rep = num_rep
+        self.seed = int(seed) if seed is not None else None
+        self.max_batch = int(max_batch)
+        self._shot_offset = 0
+        self._ph = None
+        self.last_result = None
+
+    # -- reference per-sample API (plugin path) --------------------------------
+    def _generate_error(self):
+        """``:405-442``: data error (3-way split), then hx-row and hz-row syndrome flips."""
+        N = self.N
+        u = np.array([random.random() for _ in range(N)])
+        ex, ez = pauli_split(u, self.channel_probs)
+        sz = np.array([random.random() < self.synd_prob for _ in range(self.hx_ext.shape[1] - N)], dtype=int)
+        sx = np.array([random.random() < self.synd_prob for _ in range(self.hz_ext.shape[1] - N)], dtype=int)
+        self.error_x_ext = np.concatenate([ex, sx])
+        self.error_z_ext = np.concatenate([ez, sz])
+        return self.error_x_ext, self.error_z_ext
+
+    def _single_run(self, num_rounds):
+        """``:444-529`` (Z detectors differenced, X raw: quirk Q3)."""
+        code = self.code
+        num_z_checks, num_qubits = code.hz.shape
+        num_x_checks = code.hx.shape[0]
+        cur_z, cur_x = np.zeros(num_qubits, dtype=int), np.zeros(num_qubits, dtype=int)
+        for _ in range(num_rounds - 1):
+            hist_z = np.zeros([self.num_rep, num_x_checks], dtype=int)
+            hist_x = np.zeros([self.num_rep, num_z_checks], dtype=int)
+            for j in range(self.num_rep):
+                ex_ext, ez_ext = self._generate_error()
+                cx = (np.concatenate([cur_x, np.zeros(num_z_checks, dtype=int)]) + ex_ext) % 2
+                cz = (np.concatenate([cur_z, np.zeros(num_x_checks, dtype=int)]) + ez_ext) % 2
+                hist_z[j] = (self.hx_ext @ cz % 2).astype(int)
+                hist_x[j] = (self.hz_ext @ cx % 2).astype(int)
+                cur_z, cur_x = cz[:num_qubits], cx[:num_qubits]
+            det_z = hist_z.copy()
+            det_z[1:] = (hist_z[:-1] + hist_z[1:]) % 2
+            cur_z = (cur_z + self.decoder1_z.decode(det_z)) % 2
+            cur_x = (cur_x + self.decoder1_x.decode(hist_x)) % 2
+        ex_ext, ez_ext = self._generate_error()
+        cur_x = (cur_x + ex_ext[:self.N]) % 2
+        cur_z = (cur_z + ez_ext[:self.N]) % 2
+        dz = self.decoder2_z.decode(code.hx @ cur_z % 2)
+        dx = self.decoder2_x.decode(code.hz @ cur_x % 2)
+        rx, rz = (cur_x + dx) % 2, (cur_z + dz) % 2
+        X_failure = int(((code.hz @ rx) % 2).any() or ((code.lz @ rx) % 2).any())
+        Z_failure = int(((code.hx @ rz) % 2).any() or ((code.lx @ rz) % 2).any())
+        assert self.eval_logical_type in ["X", "Z", "Total"]
+        if self.eval_logical_type == "X":
+            return X_failure
+        if self.eval_logical_type == "Z":
+            return Z_failure
+        return X_failure or Z_failure
+
+    # -- fused engine path ----------------------------------------------------
+    def _engine_parts(self):
+        from .decoders import ST_BP_Decoder_syndrome
+
+        d1 = (self.decoder1_x, self.decoder1_z)
+        if not all(isinstance(d, ST_BP_Decoder_syndrome) and d.num_rep == self.num_rep for d in d1):
+            return None
+        b2 = (_engine_bp(self.decoder2_x), _engine_bp(self.decoder2_z))
+        if any(b is None for b in b2):
+            return None
+        return d1[0].space_decoder, d1[1].space_decoder, b2[0], b2[1]
+
+    def fused_counts(self, num_rounds: int, num_samples: int):
+        """Run ``num_samples`` samples on the GPU; returns the all-reduced :class:`~.engine.MCResult`."""
+        parts = self._engine_parts()
+        if parts is None:
+            raise TypeError("fused path needs engine ST_BP_Decoder_syndrome (decoder1) and BPDecoder (decoder2)")
+        from .engine import DevicePhenl, MCResult, _torch
+
+        torch = _torch()
+        if self.seed is None:
+            self.seed = random.getrandbits(64)
+        if self._ph is None:
+            self._ph = DevicePhenl(self.code, *parts, num_rep=self.num_rep, max_batch=self.max_batch)
+        rank, ws = parallel.world()
+        b, c = parallel.shard_range(num_samples, rank, ws, begin=self._shot_offset)
+        self._shot_offset += int(num_samples)
+        px, py, pz = self.channel_probs
+        cnt = self._ph.new_counters()
+        self._ph.launch(px, py, pz, self.synd_prob, self.seed, b, c, num_rounds, self.eval_logical_type, cnt)
+        parallel.allreduce_counters(cnt)
+        torch.cuda.synchronize(cnt.device)
+        res = MCResult.from_words(cnt.cpu().numpy())
+        self.last_result = res
+        return res
+
+    def WordErrorRate(self, num_cycles: int, num_samples: int):
+        num_rounds = int((num_cycles - 1) / self.num_rep + 1)
+        if self._engine_parts() is not None:
+            error_count = self.fused_counts(num_rounds, num_samples).failures
+        else:
+            error_count = int(np.sum([self._single_run(num_rounds) for _ in range(num_samples)]))
+        total_num_cycles = (num_rounds - 1) * self.num_rep + 1
+        return word_error_rate_per_cycle(error_count, num_samples, self.K, total_num_cycles), None
+
+
 # -------------------------------------------------------------- code family
 
 
@@ -224,6 +351,62 @@ class CodeFamily:
         eval_wer_array = self.EvalWER(noise_model, eval_logical_type, eval_p_list, num_samples, num_cycles,
                                       data_synd_noise_ratio, circuit_type, circuit_error_params, if_plot=False)
         return ThresholdEst_extrapolation(eval_p_list, eval_wer_array, if_plot)
+
+
+class CodeFamily_SpaceTime:
+    """``src/Simulators_SpaceTime.py:1152-1309`` for the ``'data'`` and ``'phenl'`` noise models.
+
+    ``'phenl'`` builds decoder1 (space-time, ``num_rep``) and decoder2 exactly
+    as the reference (``:1189-1216``; p_data = eval_p, q = eval_p, Pauli
+    ``[eval_p/2]*3``) and runs :class:`CodeSimulator_Phenon_SpaceTime` (the
+    reference names an undefined ``CodeSimulator_SpaceTime`` there, quirk Q5).
+    Returns ``(eval_wer_list, eval_p_list_per_code)``; the reference leaves the
+    second value undefined for 'phenl' and this returns the p grid per code.
+    ``'circuit'`` needs stim (absent) and raises.
+    """
+
+    def __init__(self, code_list: list, decoder1_class, decoder2_class):
+        self.code_list = code_list
+        self.decoder1_class = decoder1_class
+        self.decoder2_class = decoder2_class
+
+    def EvalWER(self, noise_model: str, eval_logical_type: str, eval_p_list: list, num_samples: int, num_cycles=1,
+                num_rep=1, circuit_type="coloration", circuit_error_params=None, if_plot=True, if_adaptive=False,
+                adaptive_params=None):
+        assert noise_model in ["data", "phenl", "circuit"], "noise_model should be one of [data, phenl, circuit]"
+        assert eval_logical_type in ["X", "Z", "Total"], "eval_type should be one of [X, Y, Total]"
+        if noise_model == "circuit":
+            raise NotImplementedError("circuit-level noise needs stim's detector error models (absent; SURVEY.md §8f)")
+        eval_wer_list, eval_p_adapt_list = [], []
+        for eval_code in self.code_list:
+            per_code = []
+            for eval_p in eval_p_list:
+                p = eval_p * 3 / 2
+                pauli_error_probs = [p / 3, p / 3, p / 3]
+                if noise_model == "data":
+                    dx = self.decoder2_class.GetDecoder({"h": eval_code.hz, "p_data": eval_p})
+                    dz = self.decoder2_class.GetDecoder({"h": eval_code.hx, "p_data": eval_p})
+                    sim = CodeSimulator_DataError(code=eval_code, decoder_x=dx, decoder_z=dz,
+                                                  pauli_error_probs=pauli_error_probs,
+                                                  eval_logical_type=eval_logical_type)
+                    per_code.append(sim.WordErrorRate(num_samples)[0])
+                else:
+                    q = eval_p
+                    p_data, p_synd = p * 2 / 3, q
+                    d1x = self.decoder1_class.GetDecoder({"h": eval_code.hz, "p_data": p_data, "p_syndrome": p_synd,
+                                                          "num_rep": num_rep})
+                    d1z = self.decoder1_class.GetDecoder({"h": eval_code.hx, "p_data": p_data, "p_syndrome": p_synd,
+                                                          "num_rep": num_rep})
+                    d2x = self.decoder2_class.GetDecoder({"h": eval_code.hz, "p_data": p_data})
+                    d2z = self.decoder2_class.GetDecoder({"h": eval_code.hx, "p_data": p_data})
+                    sim = CodeSimulator_Phenon_SpaceTime(code=eval_code, decoder1_x=d1x, decoder1_z=d1z,
+                                                         decoder2_x=d2x, decoder2_z=d2z,
+                                                         pauli_error_probs=pauli_error_probs, q=q,
+                                                         eval_logical_type=eval_logical_type, num_rep=num_rep)
+                    per_code.append(sim.WordErrorRate(num_cycles=num_cycles, num_samples=num_samples)[0])
+            eval_wer_list.append(np.array(per_code))
+            eval_p_adapt_list.append(np.array(eval_p_list))
+        return eval_wer_list, eval_p_adapt_list
 
 
 def _plot_wer(code_list, eval_p_list, eval_wer_array, num_cycles):

@@ -88,6 +88,55 @@ def test_spacetime_wer_formula_matches_reference(gold):
         assert simulators.word_error_rate_per_cycle(int(nfail), int(num_samples), 17, total) == w
 
 
+def test_oracle_phenl_replays_reference_harness(gold, n225, oracle):
+    """A13: the oracle's CodeSimulator_Phenon_SpaceTime restatement, fed CPython's recorded uniforms, reproduces
+    the reference harness's detector histories (Z differenced, X raw: quirk Q3), final syndromes and failures."""
+    p = 0.02
+    r = oracle.phenl_run(n225, p / 2, p / 2, p / 2, p, 0, 0, 12, 3, 3, "Total", p_data=p, p_synd=p,
+                         uniforms=gold["phenst_u"], per_shot=True)
+    tr, m = r["trace"], n225.hz.shape[0]
+    body = tr[:, :2 * 2 * 3 * m].reshape(12, 2, 2, 3, m)
+    assert np.array_equal(body[:, :, 0].reshape(24, 3, m), gold["phenst_d1z_hist"])
+    assert np.array_equal(body[:, :, 1].reshape(24, 3, m), gold["phenst_d1x_hist"])
+    assert np.array_equal(tr[:, 12 * m:13 * m], gold["phenst_d2z_synd"])
+    assert np.array_equal(tr[:, 13 * m:], gold["phenst_d2x_synd"])
+    assert np.array_equal((r["fail"] != 0).astype(np.uint8), gold["phenst_fail"])
+
+
+def test_phenl_simulator_plugin_path_matches_oracle(gold, n225, oracle):
+    """The drop-in CodeSimulator_Phenon_SpaceTime._single_run (per-sample plugin path, CPython random) with
+    oracle-backed decoders draws and decides exactly like the reference harness."""
+    import random
+
+    p = 0.02
+
+    class OracleST:
+        def __init__(self, h):
+            self.h, self.csr = h, codes.space_time_csr(h, 3)
+            mh, nh = h.shape
+            self.probs = np.hstack([p * np.ones(nh), p * np.ones(mh)] * 3)
+
+        def decode(self, det):
+            e, _, _ = oracle.bp_decode_batch(self.csr, self.probs, 22, synd=np.asarray(det).reshape(1, -1))
+            return decoders.fold_space_time_correction(e[0], self.h.shape[1], self.h.shape[0], 3)
+
+    class OracleBP:
+        def __init__(self, h):
+            self.h = h
+
+        def decode(self, s):
+            return oracle.bp_decode_batch(self.h, p, 22, synd=np.asarray(s).reshape(1, -1))[0][0].astype(int)
+
+    sim = simulators.CodeSimulator_Phenon_SpaceTime(
+        code=n225, decoder1_x=OracleST(n225.hz), decoder1_z=OracleST(n225.hx), decoder2_x=OracleBP(n225.hz),
+        decoder2_z=OracleBP(n225.hx), pauli_error_probs=[p / 2] * 3, q=p, eval_logical_type="Total", num_rep=3)
+    flags = []
+    for s in range(12):
+        random.seed(9000 + s)
+        flags.append(int(sim._single_run(3)))
+    assert flags == gold["phenst_fail"].tolist()
+
+
 @pytest.mark.parametrize("t0", [1, 2, 3])
 def test_space_time_matrix_matches_reference(gold, n225, t0):
     """A10: GetSpaceTimeCheckMat (Decoders_SpaceTime.py:179-194)."""

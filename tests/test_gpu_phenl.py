@@ -1,0 +1,127 @@
+"""GPU parity of the phenomenological space-time shot loop (qldpc_phenl_*).
+
+Reference: CodeSimulator_Phenon_SpaceTime (src/Simulators_SpaceTime.py:382-548)
+with ST_BP_Decoder_syndrome (src/Decoders_SpaceTime.py:200-223) as decoder1.
+The golden case replays CPython's own random() stream (uniforms recorded by
+tests/golden/make_golden.py from the reference harness); the Philox cases
+compare against the oracle's restatement (oracle_phenl_run) bit for bit.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from qldpc_fault_tolerance_amd import codes, decoders, simulators
+from qldpc_fault_tolerance_amd.engine import DeviceBP, DevicePhenl
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_harness_n225.npz")
+
+
+def _phenl(code, p_data, p_synd, num_rep, precision, max_iter=None, max_batch=0):
+    n = code.N
+    mi = int(n / 10) if max_iter is None else max_iter
+    hz, hx = code.csr("hz"), code.csr("hx")
+    pst_x = np.hstack([p_data * np.ones(n), p_synd * np.ones(hz.m)] * num_rep)
+    pst_z = np.hstack([p_data * np.ones(n), p_synd * np.ones(hx.m)] * num_rep)
+    st_x = DeviceBP(codes.space_time_csr(code.hz, num_rep), pst_x, max_iter=mi, precision=precision)
+    st_z = DeviceBP(codes.space_time_csr(code.hx, num_rep), pst_z, max_iter=mi, precision=precision)
+    d2x = DeviceBP(hz, p_data * np.ones(n), max_iter=mi, precision=precision)
+    d2z = DeviceBP(hx, p_data * np.ones(n), max_iter=mi, precision=precision)
+    return DevicePhenl(code, st_x, st_z, d2x, d2z, num_rep=num_rep, max_batch=max_batch)
+
+
+def _split_trace(tr, num_rounds, num_rep, m):
+    """[S, trace_len] -> (z histories [S*(R-1), rep, m], x histories, final z synd [S, m], final x synd)."""
+    S = tr.shape[0]
+    R1 = num_rounds - 1
+    body = tr[:, :R1 * 2 * num_rep * m].reshape(S, R1, 2, num_rep, m)
+    fin = tr[:, R1 * 2 * num_rep * m:].reshape(S, 2, m)
+    return (body[:, :, 0].reshape(S * R1, num_rep, m), body[:, :, 1].reshape(S * R1, num_rep, m),
+            fin[:, 0], fin[:, 1])
+
+
+def test_phenl_replays_reference_harness(gpu):
+    """External CPython uniforms: detector histories, final syndromes and failures == the reference harness."""
+    g = np.load(GOLD)
+    code = codes.get_code("hgp_34_n225")
+    p = 0.02
+    ph = _phenl(code, p, p, 3, precision=64)
+    U = g["phenst_u"]
+    res = ph.run(p / 2, p / 2, p / 2, p, seed=0, shot_begin=0, shot_count=U.shape[0], num_rounds=3,
+                 logical_mode="Total", uniforms=U, per_shot=True)
+    hz_, hx_, fz, fx = _split_trace(res.trace, 3, 3, code.hz.shape[0])
+    assert np.array_equal(hz_, g["phenst_d1z_hist"])
+    assert np.array_equal(hx_, g["phenst_d1x_hist"])
+    assert np.array_equal(fz, g["phenst_d2z_synd"])
+    assert np.array_equal(fx, g["phenst_d2x_synd"])
+    assert np.array_equal((res.fail != 0).astype(np.uint8), g["phenst_fail"])
+    assert res.failures == int(g["phenst_fail"].sum()) and res.shots == U.shape[0]
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+@pytest.mark.parametrize("mode", ["Total", "X", "Z"])
+def test_phenl_philox_matches_oracle(gpu, oracle, precision, mode):
+    code = codes.get_code("hgp_34_n225")
+    p = 0.03
+    S, R, rep = 333, 4, 3  # 333: a ragged last sample word
+    ph = _phenl(code, p, p, rep, precision)
+    res = ph.run(p / 2, p / 2, p / 2, p, seed=77, shot_begin=1000, shot_count=S, num_rounds=R, logical_mode=mode,
+                 per_shot=True)
+    ref = oracle.phenl_run(code, p / 2, p / 2, p / 2, p, 77, 1000, S, R, rep, mode, p_data=p, p_synd=p,
+                           precision=precision, per_shot=True)
+    assert np.array_equal(res.trace, ref["trace"])
+    assert np.array_equal(res.fail, ref["fail"])
+    assert res.failures == ref["failures"] and res.shots == S
+    assert res.sector_decodes == ref["sector_decodes"]
+    assert res.sector_iters == ref["sector_iters"]
+    assert res.sector_nonconv == ref["sector_nonconv"]
+    assert res.sector_fail == ref["sector_fail"]
+
+
+def test_phenl_chunking_and_sharding_invariance(gpu):
+    """Counters do not depend on max_batch chunking or on how the sample range is split (per-sample RNG keys)."""
+    code = codes.get_code("hgp_34_n225")
+    p = 0.04
+    a = _phenl(code, p, p, 2, precision=32).run(p / 2, p / 2, p / 2, p, 5, 0, 1000, 3, per_shot=True)
+    b = _phenl(code, p, p, 2, precision=32, max_batch=192)
+    b1 = b.run(p / 2, p / 2, p / 2, p, 5, 0, 601, 3, per_shot=True)
+    b2 = b.run(p / 2, p / 2, p / 2, p, 5, 601, 399, 3, per_shot=True)
+    assert np.array_equal(a.fail, np.concatenate([b1.fail, b2.fail]))
+    assert np.array_equal(a.trace, np.concatenate([b1.trace, b2.trace]))
+    assert a.failures == b1.failures + b2.failures
+    assert a.sector_iters == [x + y for x, y in zip(b1.sector_iters, b2.sector_iters)]
+
+
+def test_phenl_n1225_space_time_graph(gpu, oracle):
+    """Config 5 graph (hgp_34_n1225_q3 stand-in, num_rep=3: ST graph 1764 x 5439) against the oracle, fp32."""
+    code = codes.get_code("hgp_34_n1225_q3")
+    p = 0.01
+    ph = _phenl(code, p, p, 3, precision=32)
+    S, R = 96, 3
+    res = ph.run(p / 2, p / 2, p / 2, p, 11, 0, S, R, per_shot=True)
+    ref = oracle.phenl_run(code, p / 2, p / 2, p / 2, p, 11, 0, S, R, 3, "Total", p_data=p, p_synd=p,
+                           precision=32, per_shot=True)
+    assert np.array_equal(res.trace, ref["trace"])
+    assert np.array_equal(res.fail, ref["fail"])
+    assert res.sector_iters == ref["sector_iters"]
+
+
+def test_phenl_simulator_dropin(gpu, oracle):
+    """CodeSimulator_Phenon_SpaceTime.WordErrorRate (fused path) == the per-cycle formula on the oracle's count."""
+    code = codes.get_code("hgp_34_n225")
+    eval_p = 0.02
+    c1 = decoders.ST_BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    c2 = decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    d1x = c1.GetDecoder({"h": code.hz, "p_data": eval_p, "p_syndrome": eval_p, "num_rep": 3})
+    d1z = c1.GetDecoder({"h": code.hx, "p_data": eval_p, "p_syndrome": eval_p, "num_rep": 3})
+    d2x = c2.GetDecoder({"h": code.hz, "p_data": eval_p})
+    d2z = c2.GetDecoder({"h": code.hx, "p_data": eval_p})
+    pp = eval_p / 2
+    sim = simulators.CodeSimulator_Phenon_SpaceTime(code=code, decoder1_x=d1x, decoder1_z=d1z, decoder2_x=d2x,
+                                                    decoder2_z=d2z, pauli_error_probs=[pp] * 3, q=eval_p,
+                                                    eval_logical_type="Total", num_rep=3, seed=99)
+    wer, none = sim.WordErrorRate(num_cycles=7, num_samples=500)  # num_rounds = 3
+    ref = oracle.phenl_run(code, pp, pp, pp, eval_p, 99, 0, 500, 3, 3, "Total", p_data=eval_p, p_synd=eval_p)
+    assert none is None
+    assert wer == simulators.word_error_rate_per_cycle(ref["failures"], 500, code.K, 7)
