@@ -258,6 +258,17 @@ int qldpc_graph_info(const qldpc_graph* g, int32_t* m, int32_t* n, int32_t* nnz,
 
 static int upload_llr(qldpc_bp* bp) {
   const int TB = bp->TB, VPL = bp->VPL, n = bp->g->n;
+  if (bp->engine == 5) {  // product-sum priors: ratio p / (1 - p), computed in double (oracle ws_priors)
+    std::vector<double> r64(n);
+    for (int j = 0; j < n; ++j) r64[j] = bp->probs[j] / (1.0 - bp->probs[j]);
+    if (bp->precision == 32) {
+      std::vector<float> r32(r64.begin(), r64.end());
+      QLDPC_HIP(hipMemcpy(bp->llr.p, r32.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    } else {
+      QLDPC_HIP(hipMemcpy(bp->llr.p, r64.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+    }
+    return 0;
+  }
   const size_t cnt = (size_t)VPL * TB;
   std::vector<double> l64(cnt, 1.0);
   for (int k = 0; k < VPL; ++k)
@@ -304,14 +315,72 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
     }
 }
 
+// Engine 5 (product-sum): the row-ordered / column-ordered products need the
+// plain CSR and CSC (edge ids in row-major order, rows ascending per column).
+static int create_ps(qldpc_graph* g, const double* channel_probs, int32_t max_iter, int32_t precision,
+                     qldpc_bp** out) {
+  auto* bp = new qldpc_bp();
+  bp->g = g;
+  bp->engine = 5;
+  bp->method = QLDPC_PRODUCT_SUM;
+  bp->precision = precision;
+  bp->max_iter = max_iter > 0 ? max_iter : g->n;
+  bp->alpha = 0;
+  bp->TB = 256;
+  bp->VPL = (g->n + 255) / 256;
+  bp->probs.assign(channel_probs, channel_probs + g->n);
+  auto fail = [&](int code) {
+    for (DevBuf* d : {&bp->llr, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp, &bp->ps_ce, &bp->ps_ws}) d->release();
+    delete bp;
+    return code;
+  };
+  const int E = g->nnz;
+  std::vector<int32_t> cp(g->n + 1, 0), ce;
+  ce.reserve(E);
+  for (int j = 0; j < g->n; ++j) {
+    for (int i : g->col_rows[j]) {
+      const int* b = g->col_idx.data() + g->row_ptr[i];
+      const int* e = g->col_idx.data() + g->row_ptr[i + 1];
+      ce.push_back((int32_t)(std::lower_bound(b, e, j) - g->col_idx.data()));
+    }
+    cp[j + 1] = (int32_t)ce.size();
+  }
+  int rc;
+  if ((rc = bp->ps_rp.alloc((size_t)(g->m + 1) * 4)) || (rc = bp->ps_ci.alloc((size_t)std::max(1, E) * 4)) ||
+      (rc = bp->ps_cp.alloc((size_t)(g->n + 1) * 4)) || (rc = bp->ps_ce.alloc((size_t)std::max(1, E) * 4)) ||
+      (rc = bp->llr.alloc((size_t)g->n * (precision == 32 ? 4 : 8))))
+    return fail(rc);
+  if (hipMemcpy(bp->ps_rp.p, g->row_ptr.data(), (size_t)(g->m + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      (E && hipMemcpy(bp->ps_ci.p, g->col_idx.data(), (size_t)E * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+      hipMemcpy(bp->ps_cp.p, cp.data(), cp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      (E && hipMemcpy(bp->ps_ce.p, ce.data(), (size_t)E * 4, hipMemcpyHostToDevice) != hipSuccess))
+    return fail(set_err(QLDPC_EHIP, "upload product-sum graph"));
+  if ((rc = upload_llr(bp))) return fail(rc);
+  // messages in LDS when 2E values fit in 96 KiB (>= 1 workgroup per CU with room), else in HBM
+  const bool lds_msgs = ps_lds_bytes(precision, g->m, g->n, E, true) <= 96 * 1024;
+  bp->lds_bytes = (int)ps_lds_bytes(precision, g->m, g->n, E, lds_msgs);
+  if (bp->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "graph too large for the product-sum engine"));
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ps_kernel(precision), bp->TB, bp->lds_bytes) != hipSuccess)
+    nb = 1;
+  bp->blocks_per_cu = std::max(1, nb);
+  if ((rc = device_cus(g->device, bp->cus))) return fail(rc);
+  bp->ps_grid = (long long)bp->blocks_per_cu * bp->cus;
+  if (!lds_msgs && (rc = bp->ps_ws.alloc((size_t)bp->ps_grid * 2 * E * (precision == 32 ? 4 : 8)))) return fail(rc);
+  *out = bp;
+  return 0;
+}
+
 int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_iter, int32_t bp_method,
                     double ms_scaling_factor, int32_t precision, int32_t vars_per_thread, int32_t min_col_slots,
                     qldpc_bp** out) {
   if (!g || !channel_probs || !out) return set_err(QLDPC_EINVAL, "NULL argument");
   if (precision != 32 && precision != 64) return set_err(QLDPC_EINVAL, "precision must be 32 or 64");
-  if (bp_method != QLDPC_MIN_SUM) return set_err(QLDPC_ENOTSUP, "GPU engine implements minimum_sum only");
-  if (g->max_col > 8 || min_col_slots > 8) return set_err(QLDPC_ENOTSUP, "column degree > 8");
+  if (bp_method != QLDPC_MIN_SUM && bp_method != QLDPC_PRODUCT_SUM)
+    return set_err(QLDPC_EINVAL, "bp_method must be 0 (product_sum) or 1 (minimum_sum)");
   QLDPC_HIP(hipSetDevice(g->device));
+  if (bp_method == QLDPC_PRODUCT_SUM) return create_ps(g, channel_probs, max_iter, precision, out);
+  if (g->max_col > 8 || min_col_slots > 8) return set_err(QLDPC_ENOTSUP, "column degree > 8");
   auto* bp = new qldpc_bp();
   bp->g = g;
   const int want_engine = env_int("QLDPC_ENGINE", 3);
@@ -399,9 +468,8 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
 
 int qldpc_bp_destroy(qldpc_bp* bp) {
   if (!bp) return 0;
-  bp->vchk.release();
-  bp->llr.release();
-  bp->rdeg.release();
+  for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp, &bp->ps_ce, &bp->ps_ws})
+    d->release();
   delete bp;
   return 0;
 }
@@ -471,6 +539,7 @@ int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, 
   if (!bp || (B > 0 && (!d_synd || !d_corr))) return set_err(QLDPC_EINVAL, "NULL argument");
   if (B == 0) return 0;
   QLDPC_HIP(hipSetDevice(bp->g->device));
+  if (bp->engine == 5) return ps_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
   const long long cap = (long long)bp->blocks_per_cu * bp->cus;
   if (bp->engine == 1) {
     DecArgs a;
@@ -527,6 +596,30 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
                     qldpc_mc** out) {
   if (!out || (!dec_x && !dec_z)) return set_err(QLDPC_EINVAL, "need at least one sector decoder");
   qldpc_bp* d0 = dec_x ? dec_x : dec_z;
+  const bool staged = (dec_x && dec_x->engine == 5) || (dec_z && dec_z->engine == 5) ||
+                      env_int("QLDPC_MC_STAGED", 0) == 1;
+  if (staged) {  // staged pipeline around decode_batch (staged.hip): any decoder pair
+    if (dec_x && dec_z && (dec_x->g->n != dec_z->g->n || dec_x->g->device != dec_z->g->device))
+      return set_err(QLDPC_EINVAL, "sector decoders differ in code length or device");
+    QLDPC_HIP(hipSetDevice(d0->g->device));
+    auto* mc = new qldpc_mc();
+    mc->dec[0] = dec_x;
+    mc->dec[1] = dec_z;
+    mc->engine = d0->engine;
+    mc->precision = d0->precision;
+    mc->TB = d0->TB;
+    mc->VPL = d0->VPL;
+    int rc = mc->counters.alloc(sizeof(qldpc_counters));
+    if (!rc) rc = staged_mc_prepare(mc, logical_x, logical_z);
+    if (rc) {
+      staged_mc_release(mc);
+      mc->counters.release();
+      delete mc;
+      return rc;
+    }
+    *out = mc;
+    return 0;
+  }
   if (dec_x && dec_z) {
     if (dec_x->g->n != dec_z->g->n) return set_err(QLDPC_EINVAL, "sector code lengths differ");
     if (dec_x->TB != dec_z->TB || dec_x->VPL != dec_z->VPL || dec_x->DMAX != dec_z->DMAX ||
@@ -590,6 +683,7 @@ int qldpc_mc_destroy(qldpc_mc* mc) {
   mc->lmask[0].release();
   mc->lmask[1].release();
   mc->counters.release();
+  staged_mc_release(mc);
   delete mc;
   return 0;
 }
@@ -613,7 +707,12 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     if (!need[q]) continue;
     if (!mc->dec[q]) return set_err(QLDPC_EINVAL, q == 0 ? "logical_mode needs the X sector (hz decoder)"
                                                           : "logical_mode needs the Z sector (hx decoder)");
-    if (!mc->lmask[q].p) return set_err(QLDPC_EINVAL, "sector has no logical operators");
+    if (!mc->staged && !mc->lmask[q].p) return set_err(QLDPC_EINVAL, "sector has no logical operators");
+  }
+  if (mc->staged) {
+    QLDPC_HIP(hipSetDevice((mc->dec[0] ? mc->dec[0] : mc->dec[1])->g->device));
+    return staged_mc_launch(mc, px, py, pz, seed, shot_begin, shot_count, logical_mode, d_uniforms, d_counters, d_fail,
+                            d_err, d_corr, d_iters, (hipStream_t)stream);
   }
   QLDPC_HIP(hipSetDevice((mc->dec[0] ? mc->dec[0] : mc->dec[1])->g->device));
   const long long cap = (long long)mc->blocks_per_cu * mc->cus;

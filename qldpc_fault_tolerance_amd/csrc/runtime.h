@@ -63,6 +63,9 @@ struct qldpc_bp {
   std::vector<double> probs;
   qldpc_rt::DevBuf vchk, llr;  // engine 1: packed u16 check ids; engines 2-4: edge words (check | slot<<16)
   qldpc_rt::DevBuf rdeg;       // engine 4: u8 row degrees
+  // engine 5 (product-sum, bp_ps.hip): CSR / CSC on the device, optional HBM message workspace
+  qldpc_rt::DevBuf ps_rp, ps_ci, ps_cp, ps_ce, ps_ws;
+  long long ps_grid = 0;
 };
 
 struct qldpc_mc {
@@ -72,5 +75,28 @@ struct qldpc_mc {
   qldpc_rt::DevBuf counters;
   int engine = 2, TB = 0, VPL = 0, DMAX = 0, NS = 1, precision = 64, lds_bytes = 0, blocks_per_cu = 0, cus = 0;
   int mmax = 0, vslots = 0, img_bytes = 0;
+  // staged pipeline (staged.hip): product-sum decoders, or QLDPC_MC_STAGED=1
+  bool staged = false;
+  long long sbatch = 0;
+  int sm[2] = {0, 0}, sk[2] = {0, 0};
+  qldpc_rt::DevBuf s_rp[2], s_ci[2], s_cur[2], s_failw[2], s_D, s_det, s_corr, s_iters, s_conv;
 };
 
+
+namespace qldpc_rt {
+
+// engine 5 (bp_ps.hip)
+size_t ps_lds_bytes(int precision, int m, int n, int E, bool lds_messages);
+const void* ps_kernel(int precision);
+int ps_decode_launch(const qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int32_t* iters, uint8_t* conv, int64_t B,
+                     hipStream_t stream);
+
+// staged data-error shot loop (staged.hip): bit-sliced sampling / syndromes /
+// checks around qldpc_bp_decode_batch, for decoders the fused kernels do not serve
+int staged_mc_prepare(qldpc_mc* mc, const qldpc_graph* logical_x, const qldpc_graph* logical_z);
+void staged_mc_release(qldpc_mc* mc);
+int staged_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed, uint64_t shot_begin,
+                     int64_t shot_count, int32_t logical_mode, const double* d_uniforms, void* d_counters,
+                     uint8_t* d_fail, uint8_t* d_err, uint8_t* d_corr, int32_t* d_iters, hipStream_t stream);
+
+}  // namespace qldpc_rt

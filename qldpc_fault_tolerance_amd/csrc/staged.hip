@@ -1,5 +1,10 @@
-// phenl.hip — phenomenological space-time shot loop on the GPU.
+// staged.hip — bit-sliced staged pipelines around the batched BP engine:
+//   (1) the phenomenological space-time shot loop (qldpc_phenl_*), and
+//   (2) the staged data-error shot loop behind qldpc_mc_launch for decoders the
+//       fused kernels do not serve (product-sum, engine 5) or when
+//       QLDPC_MC_STAGED=1 asks for it (A/B against the fused min-sum kernels).
 //
+// (1) in detail:
 // Replaces CodeSimulator_Phenon_SpaceTime._single_run / WordErrorRate
 // (src/Simulators_SpaceTime.py:421-548) for a batch of samples at once.  One
 // sample = (num_rounds - 1) noisy rounds of num_rep repetitions, each
@@ -42,10 +47,10 @@ namespace {
 constexpr uint32_t kStreamPhen = 0x51D50002u;
 constexpr int kTile = 256;  // threads per block of the layout kernels
 
-__device__ inline unsigned long long phen_k53(unsigned long long seed, unsigned long long shot, uint32_t idx) {
+__device__ inline unsigned long long phen_k53(unsigned long long seed, unsigned long long shot, uint32_t idx,
+                                              uint32_t tag) {
   uint32_t w0, w1;
-  philox4x32_10(idx, (uint32_t)shot, (uint32_t)(shot >> 32), kStreamPhen, (uint32_t)seed, (uint32_t)(seed >> 32),
-                w0, w1);
+  philox4x32_10(idx, (uint32_t)shot, (uint32_t)(shot >> 32), tag, (uint32_t)seed, (uint32_t)(seed >> 32), w0, w1);
   return ((unsigned long long)(w0 >> 5) << 26) | (unsigned long long)(w1 >> 6);
 }
 
@@ -59,6 +64,7 @@ struct SampleArgs {
   unsigned long long K1, K2, K3, Kq;  // ceil(t * 2^53) thresholds
   double t1, t2, t3, q;
   uint32_t base;                // (r·num_rep + j)·P
+  uint32_t tag;                 // Philox counter word 3: kStreamPhen, or kStreamData for the staged MC
   int n, m0, m1, W;
   long long count;              // samples in this chunk
 };
@@ -82,7 +88,7 @@ __global__ void __launch_bounds__(kTile) ph_sample(SampleArgs A) {
         bx = u < A.q;  // :425-431
       }
     } else {
-      const unsigned long long k = phen_k53(A.seed, A.shot_begin + (unsigned long long)gs, idx);
+      const unsigned long long k = phen_k53(A.seed, A.shot_begin + (unsigned long long)gs, idx, A.tag);
       if (p < A.n) {
         const uint32_t cls = (k < A.K1) ? 2u : (k < A.K2) ? 1u : (k < A.K3) ? 3u : 0u;
         bx = cls & 1u;
@@ -217,6 +223,20 @@ __global__ void __launch_bounds__(kTile) ph_iters(const int32_t* __restrict__ it
     atomicAdd(&cnt[kCntIters + q], sit);
     atomicAdd(&cnt[kCntNonconv + q], snc);
   }
+}
+
+// per-sample Pauli classes err[s][j] = x | z << 1 from the bit-sliced error words
+// grid: x = ceil(n / 256), y = word w
+__global__ void __launch_bounds__(kTile) ph_err_out(const unsigned long long* __restrict__ ex,
+                                                  const unsigned long long* __restrict__ ez, uint8_t* __restrict__ err,
+                                                  long long c0, int n, int W, long long count) {
+  const int j = blockIdx.x * kTile + threadIdx.x;
+  const int w = blockIdx.y;
+  if (j >= n) return;
+  const unsigned long long a = ex[(long long)j * W + w], b = ez[(long long)j * W + w];
+  const int nb = (int)std::min<long long>(64, count - (long long)w * 64);
+  for (int t = 0; t < nb; ++t)
+    err[(c0 + (long long)w * 64 + t) * n + j] = (uint8_t)(((a >> t) & 1ull) | (((b >> t) & 1ull) << 1));
 }
 
 unsigned long long ceil53(double t) {
@@ -372,6 +392,7 @@ int qldpc_phenl_launch(qldpc_phenl* P, double px, double py, double pz, double q
   SampleArgs A;
   std::memset(&A, 0, sizeof(A));
   A.uniforms = d_uniforms;
+  A.tag = kStreamPhen;
   A.nu = nu;
   A.seed = seed;
   A.shot_begin = shot_begin;
@@ -483,3 +504,137 @@ int qldpc_phenl_launch(qldpc_phenl* P, double px, double py, double pz, double q
 }
 
 }  // extern "C"
+
+// ===================================================== (2) staged data-error MC
+// CodeSimulator_DataError._single_run (src/Simulators.py:117-168) as a
+// pipeline: Philox sampling of both Pauli components with the fused kernels'
+// stream (kStreamData, ctr = (qubit, shot)) -> per needed sector: bit-sliced
+// H e, unpack, qldpc_bp_decode_batch, residual fold, [H; L] check -> tally.
+namespace qldpc_rt {
+
+constexpr long long kStagedBatch = 1 << 16;
+
+void staged_mc_release(qldpc_mc* mc) {
+  for (int q = 0; q < 2; ++q) {
+    mc->s_rp[q].release(); mc->s_ci[q].release(); mc->s_cur[q].release(); mc->s_failw[q].release();
+  }
+  for (DevBuf* d : {&mc->s_D, &mc->s_det, &mc->s_corr, &mc->s_iters, &mc->s_conv}) d->release();
+}
+
+int staged_mc_prepare(qldpc_mc* mc, const qldpc_graph* logical_x, const qldpc_graph* logical_z) {
+  const qldpc_graph* L[2] = {logical_x, logical_z};
+  const qldpc_bp* d0 = mc->dec[0] ? mc->dec[0] : mc->dec[1];
+  const int n = d0->g->n;
+  const long long B = kStagedBatch;
+  const size_t W = (size_t)(B / 64);
+  int mm = 1, rc;
+  for (int q = 0; q < 2; ++q) {
+    if ((rc = mc->s_cur[q].alloc((size_t)n * W * 8)) || (rc = mc->s_failw[q].alloc(W * 8))) return rc;
+    if (!mc->dec[q]) continue;
+    const qldpc_graph* h = mc->dec[q]->g;
+    if (!L[q]) return set_err(QLDPC_EINVAL, "sector has no logical operators");
+    std::vector<int32_t> rp(h->row_ptr), ci(h->col_idx);
+    for (int r = 0; r < L[q]->m; ++r) {
+      for (int e = L[q]->row_ptr[r]; e < L[q]->row_ptr[r + 1]; ++e) ci.push_back(L[q]->col_idx[e]);
+      rp.push_back((int32_t)ci.size());
+    }
+    mc->sm[q] = h->m;
+    mc->sk[q] = L[q]->m;
+    mm = std::max(mm, h->m);
+    if ((rc = mc->s_rp[q].alloc(rp.size() * 4)) || (rc = mc->s_ci[q].alloc(std::max<size_t>(4, ci.size() * 4))))
+      return rc;
+    QLDPC_HIP(hipMemcpy(mc->s_rp[q].p, rp.data(), rp.size() * 4, hipMemcpyHostToDevice));
+    if (!ci.empty()) QLDPC_HIP(hipMemcpy(mc->s_ci[q].p, ci.data(), ci.size() * 4, hipMemcpyHostToDevice));
+  }
+  if ((rc = mc->s_D.alloc((size_t)mm * W * 8)) || (rc = mc->s_det.alloc((size_t)mm * B)) ||
+      (rc = mc->s_corr.alloc((size_t)n * B)) || (rc = mc->s_iters.alloc((size_t)B * 4)) ||
+      (rc = mc->s_conv.alloc((size_t)B)))
+    return rc;
+  mc->sbatch = B;
+  mc->staged = true;
+  return 0;
+}
+
+int staged_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed, uint64_t shot_begin,
+                     int64_t shot_count, int32_t logical_mode, const double* d_uniforms, void* d_counters,
+                     uint8_t* d_fail, uint8_t* d_err, uint8_t* d_corr, int32_t* d_iters, hipStream_t st) {
+  const bool need[2] = {logical_mode != 1, logical_mode != 0};
+  const qldpc_bp* d0 = mc->dec[0] ? mc->dec[0] : mc->dec[1];
+  const int n = d0->g->n;
+  auto* cnt = static_cast<unsigned long long*>(d_counters);
+  const double t1 = pz, t2 = pz + px, t3 = (pz + px) + py;
+  SampleArgs A;
+  std::memset(&A, 0, sizeof(A));
+  A.uniforms = d_uniforms;
+  A.tag = kStreamData;
+  A.nu = n;
+  A.seed = seed;
+  A.shot_begin = shot_begin;
+  A.t1 = t1; A.t2 = t2; A.t3 = t3;
+  A.K1 = ceil53(t1); A.K2 = ceil53(t2); A.K3 = ceil53(t3);
+  A.n = n;
+  A.base = 0;
+  for (long long c0 = 0; c0 < shot_count; c0 += mc->sbatch) {
+    const long long B = std::min<long long>(mc->sbatch, shot_count - c0);
+    const int W = (int)((B + 63) / 64);
+    A.c0 = c0;
+    A.count = B;
+    A.W = W;
+    const dim3 wgrid((W + kTile - 1) / kTile);
+    for (int q = 0; q < 2; ++q) {
+      A.cur[q] = static_cast<unsigned long long*>(mc->s_cur[q].p);
+      QLDPC_HIP(hipMemsetAsync(mc->s_cur[q].p, 0, (size_t)n * W * 8, st));
+      QLDPC_HIP(hipMemsetAsync(mc->s_failw[q].p, 0, (size_t)W * 8, st));
+    }
+    hipLaunchKernelGGL(ph_sample, dim3((unsigned)((B + kTile - 1) / kTile), (unsigned)n), dim3(kTile), 0, st, A);
+    QLDPC_HIP(hipGetLastError());
+    if (d_err) {
+      hipLaunchKernelGGL(ph_err_out, dim3((unsigned)((n + kTile - 1) / kTile), (unsigned)W), dim3(kTile), 0, st,
+                         static_cast<const unsigned long long*>(mc->s_cur[0].p),
+                         static_cast<const unsigned long long*>(mc->s_cur[1].p), d_err, c0, n, W, B);
+      QLDPC_HIP(hipGetLastError());
+    }
+    for (int q = 0; q < 2; ++q) {
+      if (!need[q]) continue;
+      const int m = mc->sm[q];
+      auto* cur = static_cast<unsigned long long*>(mc->s_cur[q].p);
+      hipLaunchKernelGGL(ph_syndrome, dim3(wgrid.x, (unsigned)m), dim3(kTile), 0, st,
+                         static_cast<const int32_t*>(mc->s_rp[q].p), static_cast<const int32_t*>(mc->s_ci[q].p), cur,
+                         nullptr, nullptr, static_cast<unsigned long long*>(mc->s_D.p), W, 0, -1);
+      QLDPC_HIP(hipGetLastError());
+      hipLaunchKernelGGL(ph_unpack, dim3((unsigned)((m + kTile - 1) / kTile), (unsigned)W), dim3(kTile), 0, st,
+                         static_cast<const unsigned long long*>(mc->s_D.p), static_cast<uint8_t*>(mc->s_det.p),
+                         nullptr, 0, 0, c0, m, W, B);
+      QLDPC_HIP(hipGetLastError());
+      int rc = qldpc_bp_decode_batch(mc->dec[q], static_cast<const uint8_t*>(mc->s_det.p),
+                                     static_cast<uint8_t*>(mc->s_corr.p), static_cast<int32_t*>(mc->s_iters.p),
+                                     static_cast<uint8_t*>(mc->s_conv.p), B, st);
+      if (rc) return rc;
+      hipLaunchKernelGGL(ph_iters, dim3((unsigned)((B + kTile - 1) / kTile)), dim3(kTile), 0, st,
+                         static_cast<const int32_t*>(mc->s_iters.p), static_cast<const uint8_t*>(mc->s_conv.p), cnt, q,
+                         B);
+      QLDPC_HIP(hipGetLastError());
+      if (d_corr)
+        QLDPC_HIP(hipMemcpy2DAsync(d_corr + (c0 * 2 + q) * n, (size_t)2 * n, mc->s_corr.p, (size_t)n, (size_t)n,
+                                   (size_t)B, hipMemcpyDeviceToDevice, st));
+      if (d_iters)
+        QLDPC_HIP(hipMemcpy2DAsync(d_iters + c0 * 2 + q, 8, mc->s_iters.p, 4, 4, (size_t)B, hipMemcpyDeviceToDevice,
+                                   st));
+      hipLaunchKernelGGL(ph_fold, dim3((unsigned)((n + kTile - 1) / kTile), (unsigned)W), dim3(kTile), 0, st,
+                         static_cast<const uint8_t*>(mc->s_corr.p), cur, n, W, 1, n, n, B);
+      QLDPC_HIP(hipGetLastError());
+      hipLaunchKernelGGL(ph_check, dim3(wgrid.x, (unsigned)(m + mc->sk[q])), dim3(kTile), 0, st,
+                         static_cast<const int32_t*>(mc->s_rp[q].p), static_cast<const int32_t*>(mc->s_ci[q].p), cur,
+                         static_cast<unsigned long long*>(mc->s_failw[q].p), W);
+      QLDPC_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(ph_tally, wgrid, dim3(kTile), 0, st,
+                       need[0] ? static_cast<const unsigned long long*>(mc->s_failw[0].p) : nullptr,
+                       need[1] ? static_cast<const unsigned long long*>(mc->s_failw[1].p) : nullptr, cnt, d_fail, c0,
+                       W, B, logical_mode);
+    QLDPC_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+}  // namespace qldpc_rt

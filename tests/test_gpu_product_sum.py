@@ -1,0 +1,117 @@
+"""GPU parity of engine 5 (product-sum BP, bp_method="product_sum") and of the staged shot loop.
+
+Product-sum restates ldpc 0.1.x bp_decode_prob_ratios (oracle bp_ps_*): ordered
+products per row and per column with NaN guards, so the bar is bit-exact
+corrections / iteration counts / convergence flags in fp64 and fp32.  The
+staged data-error shot loop (bit-sliced ballot sampling + XOR-word syndromes +
+batched BP + [H; L] check) serves product-sum decoders in DeviceMC and, with
+QLDPC_MC_STAGED=1, min-sum decoders too: it must reproduce the fused kernels'
+per-shot results exactly (same Philox stream).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from qldpc_fault_tolerance_amd import codes, decoders, simulators
+from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceMC
+
+pytestmark = pytest.mark.gpu
+
+
+def _sample_synd(H, p, B, seed):
+    rng = np.random.default_rng(seed)
+    e = (rng.random((B, H.shape[1])) < p).astype(np.uint8)
+    return (e.astype(np.int64) @ H.T.astype(np.int64) % 2).astype(np.uint8)
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+@pytest.mark.parametrize("name", ["hgp_34_n225", "GenBicycleA2", "LP_Matg8_L30_Dmin20", "hgp_34_n1600"])
+def test_product_sum_decode_matches_oracle(gpu, oracle, precision, name):
+    code = codes.get_code(name)
+    H = code.hz
+    n = code.N
+    mi = int(n / 10)
+    for p in (0.02, 0.08):
+        B = 300 if n < 1500 else 120
+        synd = _sample_synd(H, p, B, seed=int(p * 1000) + precision)
+        dec = DeviceBP(H, p * np.ones(n), max_iter=mi, bp_method="product_sum", precision=precision)
+        assert dec.geometry()["engine"] == 5
+        corr, iters, conv = dec.decode_batch(synd)
+        ocorr, oiters, oconv = oracle.bp_decode_batch(H, p, mi, "product_sum", 0.0, synd, precision)
+        assert np.array_equal(iters, oiters), (name, p)
+        assert np.array_equal(conv, oconv), (name, p)
+        assert np.array_equal(corr, ocorr.astype(np.int64)), (name, p)
+
+
+def test_product_sum_hbm_messages(gpu, oracle):
+    """fp64 on the n1225 space-time graph (E = 15,288): messages exceed the LDS budget and live in HBM."""
+    code = codes.get_code("hgp_34_n1225_q3")
+    st = codes.space_time_csr(code.hx, 3)
+    p = 0.01
+    probs = np.hstack([p * np.ones(code.N), p * np.ones(code.hx.shape[0])] * 3)
+    synd = _sample_synd(st.to_dense(), p, 48, seed=5)
+    dec = DeviceBP(st, probs, max_iter=122, bp_method="product_sum", precision=64)
+    corr, iters, conv = dec.decode_batch(synd)
+    ocorr, oiters, oconv = oracle.bp_decode_batch(st, probs, 122, "product_sum", 0.0, synd, 64)
+    assert np.array_equal(iters, oiters) and np.array_equal(conv, oconv)
+    assert np.array_equal(corr, ocorr.astype(np.int64))
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+def test_product_sum_mc_matches_oracle(gpu, oracle, precision):
+    code = codes.get_code("hgp_34_n225")
+    n = code.N
+    p = 0.04
+    px = py = pz = p / 2
+    dx = DeviceBP(code.hz, p * np.ones(n), max_iter=22, bp_method="product_sum", precision=precision)
+    dz = DeviceBP(code.hx, p * np.ones(n), max_iter=22, bp_method="product_sum", precision=precision)
+    mc = DeviceMC(code, dx, dz)
+    S = 1000
+    res = mc.run(px, py, pz, seed=3, shot_begin=500, shot_count=S, logical_mode="Total", per_shot=True)
+    ref = oracle.mc_run(code, px, py, pz, seed=3, shot_begin=500, shot_count=S, logical_mode="Total", max_iter=22,
+                        bp_method="product_sum", precision=precision, per_shot=True)
+    assert np.array_equal(res.err, ref["err"])
+    assert np.array_equal(res.iters, ref["iters"])
+    assert np.array_equal(res.corr, ref["corr"])
+    assert np.array_equal(res.fail, ref["fail"])
+    assert res.failures == ref["failures"] and res.shots == S
+    assert res.sector_iters == ref["sector_iters"] and res.sector_nonconv == ref["sector_nonconv"]
+
+
+@pytest.mark.parametrize("mode", ["Total", "X"])
+def test_staged_min_sum_equals_fused(gpu, monkeypatch, mode):
+    """QLDPC_MC_STAGED=1: the staged pipeline reproduces the fused min-sum kernel shot for shot."""
+    code = codes.get_code("hgp_34_n1600")
+    n = code.N
+    p = 0.05
+    dx = DeviceBP(code.hz, p * np.ones(n), max_iter=160, precision=32)
+    dz = DeviceBP(code.hx, p * np.ones(n), max_iter=160, precision=32, vars_per_thread=dx.geometry()["vars_per_thread"])
+    fused = DeviceMC(code, dx, dz).run(p / 2, p / 2, p / 2, 17, 0, 700, mode, per_shot=True)
+    monkeypatch.setenv("QLDPC_MC_STAGED", "1")
+    staged = DeviceMC(code, dx, dz).run(p / 2, p / 2, p / 2, 17, 0, 700, mode, per_shot=True)
+    assert np.array_equal(fused.err, staged.err)
+    assert np.array_equal(fused.fail, staged.fail)
+    need = [0, 1] if mode == "Total" else [0]
+    for q in need:
+        assert np.array_equal(fused.corr[:, q], staged.corr[:, q])
+        assert np.array_equal(fused.iters[:, q], staged.iters[:, q])
+    assert fused.failures == staged.failures
+    assert fused.sector_iters == staged.sector_iters
+    assert np.array_equal(fused.iter_hist, staged.iter_hist)
+
+
+def test_product_sum_simulator_dropin(gpu, oracle):
+    """BP_Decoder_Class(bp_method='product_sum') in CodeSimulator_DataError runs on the GPU (staged path)."""
+    code = codes.get_code("hgp_34_n225")
+    p = 0.05
+    cls = decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="product_sum", ms_scaling_factor=0.0)
+    dx = cls.GetDecoder({"h": code.hz, "p_data": p})
+    dz = cls.GetDecoder({"h": code.hx, "p_data": p})
+    pp = p / 2
+    sim = simulators.CodeSimulator_DataError(code=code, decoder_x=dx, decoder_z=dz, pauli_error_probs=[pp] * 3,
+                                             eval_logical_type="Total", seed=4321)
+    wer, eb = sim.WordErrorRate(2000)
+    ref = oracle.mc_run(code, pp, pp, pp, seed=4321, shot_begin=0, shot_count=2000, logical_mode="Total",
+                        probs_x=p, probs_z=p, max_iter=22, bp_method="product_sum", precision=64)
+    assert (wer, eb) == simulators.word_error_rate(ref["failures"], 2000, code.K)
