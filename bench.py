@@ -89,7 +89,7 @@ def kernel_name(dec):
     t = "float" if dec.precision == 32 else "double"
     dmax = 4 if dec.graph.info()["max_col_deg"] <= 4 else 8
     if g["engine"] >= 3:
-        return f"qldpc::rmc_kernel<{t}, {dmax}, {g['vars_per_thread']}, {g['engine']}>"
+        return f"qldpc::rmc_kernel<{t}, {dmax}, {g['vars_per_thread']}, {g['engine']}, {g['degree3_slots']}>"
     return f"qldpc::smc_kernel<{t}, {dmax}, 1> (engine {g['engine']})"
 
 

@@ -178,9 +178,15 @@ int qldpc_bp_geometry(const qldpc_bp *bp, int32_t *threads, int32_t *vars_per_th
 
 /* Kernel engine serving a decoder: 3 = register-resident variables (default
  * when the graph fits: column degree <= 4, <= 8 variables per thread, image
- * < 64 KiB), 2 = streamed variables, 1 = LDS-atomic check state.  QLDPC_ENGINE
- * in the environment selects 1 or 2 explicitly. */
+ * < 64 KiB), 2 = streamed variables, 1 = LDS-atomic check state, 4 = engine 3
+ * with c2v computed by the check phase, 5 = product-sum (bp_method 0).
+ * QLDPC_ENGINE in the environment selects 1, 2 or 4 explicitly. */
 int qldpc_bp_engine(const qldpc_bp *bp, int32_t *engine);
+
+/* Engine 3: leading variable slots per thread that hold only variables of
+ * column degree <= 3 (variables are host-sorted by degree; those slots skip the
+ * 4th edge slot at compile time).  0 for the other engines and for fp64. */
+int qldpc_bp_degree3_slots(const qldpc_bp *bp, int32_t *d3k);
 
 #ifdef __cplusplus
 }

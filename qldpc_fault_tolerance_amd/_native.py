@@ -20,7 +20,7 @@ EXPORTED = [
     "qldpc_graph_info", "qldpc_bp_create", "qldpc_bp_destroy", "qldpc_bp_set_channel_probs",
     "qldpc_bp_decode_batch", "qldpc_mc_create", "qldpc_mc_destroy", "qldpc_mc_launch", "qldpc_mc_run",
     "qldpc_bp_geometry", "qldpc_bp_engine", "qldpc_phenl_create", "qldpc_phenl_destroy",
-    "qldpc_phenl_trace_len", "qldpc_phenl_launch",
+    "qldpc_phenl_trace_len", "qldpc_phenl_launch", "qldpc_bp_degree3_slots",
 ]
 
 
@@ -92,6 +92,8 @@ def _declare(L):
     L.qldpc_bp_geometry.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 4
     L.qldpc_bp_engine.restype = ctypes.c_int
     L.qldpc_bp_engine.argtypes = [_vp, ctypes.POINTER(_i32)]
+    L.qldpc_bp_degree3_slots.restype = ctypes.c_int
+    L.qldpc_bp_degree3_slots.argtypes = [_vp, ctypes.POINTER(_i32)]
     L.qldpc_phenl_create.restype = ctypes.c_int
     L.qldpc_phenl_create.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _pp]
     L.qldpc_phenl_destroy.restype = ctypes.c_int

@@ -53,6 +53,15 @@ __host__ __device__ inline size_t r_lds_bytes(int img, int chunk) {
   return (size_t)img + 2 * a16((size_t)((chunk + 31) / 32) * 4) + 8 * 12;
 }
 
+// Engine-3 check-state entry CS[i+1] of check i ({m1 | parity<<sign, m2}; CS[0]
+// = the missing-edge dummy).  A pre-scaled 16-byte float variant {m1|par,
+// alpha*m2, alpha*m1} saves two VALU ops per edge but measured 15 % slower
+// (ds_read_b128 gathers, +VGPRs): the gather bandwidth, not VALU, binds.
+template <typename T>
+struct CSEntry {
+  using type = Pair<T>;
+};
+
 template <typename T>
 __device__ inline T& lds_at(unsigned char* smem, uint32_t off) {
   return *reinterpret_cast<T*>(smem + off);
@@ -102,7 +111,7 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
       else
         R.ea[k][t] = (echk(e) * (uint32_t)(2 * sizeof(T))) | (va << 16);
     }
-    R.L[k] = (k * TB + tid < S.n) ? llr[k * TB + tid] : (T)1;
+    R.L[k] = (S.perm[k * TB + tid] >= 0) ? llr[k * TB + tid] : (T)1;
   }
 }
 
@@ -133,25 +142,87 @@ __device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
 
 // Variable phase (one flooding iteration's column pass).  Returns decision bits.
 // F bit0 holds (H x)_i for the current decisions: only variables whose decision
-// flipped since the previous iteration (xprev) xor their checks.
-template <typename T, int DMAX, int VPL>
-__device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, uint32_t fdelta, T alpha,
-                                 uint32_t xprev, bool last_live) {
+// flipped since the previous iteration (xprev) xor their checks.  Slots k < D3K
+// (compile time) hold variables of column degree <= 3 (host-sorted), so their
+// 4th edge slot is skipped entirely (no gather, no arithmetic, no store).
+template <typename T, int DMAX, int VPL, int ND>
+__device__ inline void r_gather(unsigned char* smem, const RState<T, DMAX, VPL>& R, int k,
+                                typename CSEntry<T>::type (&pn)[DMAX],
+                                typename FT<T>::U (&on)[DMAX]) {
+  constexpr bool KV = RState<T, DMAX, VPL>::kKeepV;
+#pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    pn[t] = lds_at<typename CSEntry<T>::type>(smem, R.ea[k][t] & 0xFFFFu);
+    if (!KV) on[t] = FT<T>::bits(lds_at<T>(smem, R.ea[k][t] >> 16));
+  }
+}
+
+template <typename T, int DMAX, int VPL, int ND>
+__device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL>& R, int k,
+                                 const typename CSEntry<T>::type (&pr)[DMAX],
+                                 const typename FT<T>::U (&o)[DMAX], uint32_t fdelta, T alpha, bool xprev) {
   using U = typename FT<T>::U;
   constexpr U kS = FT<T>::kSign;
   constexpr bool KV = RState<T, DMAX, VPL>::kKeepV;
-  r_launder(R);
-  uint32_t xbits = 0;
-  Pair<T> pn[DMAX];
-  U on[DMAX];
+  T c[ND];
 #pragma unroll
-  for (int t = 0; t < DMAX; ++t) {
-    pn[t] = lds_at<Pair<T>>(smem, R.ea[0][t] & 0xFFFFu);
-    if (!KV) on[t] = FT<T>::bits(lds_at<T>(smem, R.ea[0][t] >> 16));
+  for (int t = 0; t < ND; ++t) {
+    const U a = pr[t].a;
+    const U d = a ^ o[t];
+    // min over the other edges: m2 if this edge holds m1 (|own| == m1), else m1;
+    // sign = parity of the others and the syndrome = sign bit of d
+    // (m2 carries no sign bit, so masking after the select is the same value;
+    // masking `a` before it trips an instruction-selection crash in this LLVM)
+    const U sel = (((d & ~kS) == 0) ? pr[t].b : a) & ~kS;
+    c[t] = FT<T>::val(FT<T>::bits(FT<T>::val(sel) * alpha) ^ (d & kS));
+  }
+  // ldpc column pass: forward partial sums from the prior, then backward
+  T f[ND];
+  T acc = R.L[k];
+#pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    f[t] = acc;
+    acc = acc + c[t];
+  }
+  const bool x = acc <= (T)0;
+  T b = c[ND - 1];
+  U nv[ND];
+  nv[ND - 1] = canon2<T>(f[ND - 1]);
+#pragma unroll
+  for (int t = ND - 2; t >= 0; --t) {
+    nv[t] = canon2<T>(f[t] + b);
+    if (t > 0) b = b + c[t];
   }
 #pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    lds_at<U>(smem, R.ea[k][t] >> 16) = nv[t];
+    if (KV) R.ov[KV ? k : 0][KV ? t : 0] = nv[t];
+  }
+  if (x != xprev) {
+#pragma unroll
+    for (int t = 0; t < ND; ++t)
+      atomicXor(&lds_at<uint32_t>(smem, ((R.ea[k][t] & 0xFFFFu) >> (sizeof(T) == 4 ? 1 : 2)) + fdelta), 1u);
+  }
+  return x;
+}
+
+template <typename T, int DMAX, int VPL, int D3K>
+__device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, uint32_t fdelta, T alpha,
+                                 uint32_t xprev, bool last_live) {
+  using U = typename FT<T>::U;
+  constexpr bool KV = RState<T, DMAX, VPL>::kKeepV;
+  constexpr int N3 = DMAX == 4 ? 3 : DMAX;
+  r_launder(R);
+  uint32_t xbits = 0;
+  typename CSEntry<T>::type pn[DMAX];
+  U on[DMAX];
+  if (0 < D3K)
+    r_gather<T, DMAX, VPL, N3>(smem, R, 0, pn, on);
+  else
+    r_gather<T, DMAX, VPL, DMAX>(smem, R, 0, pn, on);
+#pragma unroll
   for (int k = 0; k < VPL; ++k) {
-    Pair<T> pr[DMAX];
+    typename CSEntry<T>::type pr[DMAX];
     U o[DMAX];
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
@@ -159,52 +230,16 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, u
       o[t] = KV ? R.ov[KV ? k : 0][KV ? t : 0] : on[t];
     }
     if (k + 1 < VPL) {  // next variable's gathers go out before this one's arithmetic
-#pragma unroll
-      for (int t = 0; t < DMAX; ++t) {
-        pn[t] = lds_at<Pair<T>>(smem, R.ea[k + 1][t] & 0xFFFFu);
-        if (!KV) on[t] = FT<T>::bits(lds_at<T>(smem, R.ea[k + 1][t] >> 16));
-      }
+      if (k + 1 < D3K)
+        r_gather<T, DMAX, VPL, N3>(smem, R, k + 1, pn, on);
+      else
+        r_gather<T, DMAX, VPL, DMAX>(smem, R, k + 1, pn, on);
     }
     if (k == VPL - 1 && !last_live) break;  // every lane of this wave holds padding
-    T c[DMAX];
-#pragma unroll
-    for (int t = 0; t < DMAX; ++t) {
-      const U a = pr[t].a;
-      const U d = a ^ o[t];
-      // min over the other edges: m2 if this edge holds m1 (|own| == m1), else m1
-      // (m2 carries no sign bit, so masking after the select is the same value;
-      // masking `a` before it trips an instruction-selection crash in this LLVM)
-      const U sel = (((d & ~kS) == 0) ? pr[t].b : a) & ~kS;
-      c[t] = FT<T>::val(FT<T>::bits(FT<T>::val(sel) * alpha) ^ (d & kS));
-    }
-    // ldpc column pass: forward partial sums from the prior, then backward
-    T f[DMAX];
-    T acc = R.L[k];
-#pragma unroll
-    for (int t = 0; t < DMAX; ++t) {
-      f[t] = acc;
-      acc = acc + c[t];
-    }
-    const bool x = acc <= (T)0;
+    const bool xp = ((xprev >> k) & 1u) != 0;
+    const bool x = k < D3K ? r_var_one<T, DMAX, VPL, N3>(smem, R, k, pr, o, fdelta, alpha, xp)
+                           : r_var_one<T, DMAX, VPL, DMAX>(smem, R, k, pr, o, fdelta, alpha, xp);
     xbits |= (x ? 1u : 0u) << k;
-    T b = c[DMAX - 1];
-    U nv[DMAX];
-    nv[DMAX - 1] = canon2<T>(f[DMAX - 1]);
-#pragma unroll
-    for (int t = DMAX - 2; t >= 0; --t) {
-      nv[t] = canon2<T>(f[t] + b);
-      if (t > 0) b = b + c[t];
-    }
-#pragma unroll
-    for (int t = 0; t < DMAX; ++t) {
-      lds_at<U>(smem, R.ea[k][t] >> 16) = nv[t];
-      if (KV) R.ov[KV ? k : 0][KV ? t : 0] = nv[t];
-    }
-    if (x != (((xprev >> k) & 1u) != 0)) {
-#pragma unroll
-      for (int t = 0; t < DMAX; ++t)
-        atomicXor(&lds_at<uint32_t>(smem, ((R.ea[k][t] & 0xFFFFu) >> (sizeof(T) == 4 ? 1 : 2)) + fdelta), 1u);
-    }
   }
   return xbits;
 }
@@ -213,7 +248,7 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, u
 // tests (H x)_i == s_i (F bit0).  Clears F and rebuilds CS from the rows.
 template <typename T, bool FIRST>
 __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int nch, int tid, int TB,
-                              uint32_t& sbits) {
+                              uint32_t& sbits, T alpha_next) {
   using U = typename FT<T>::U;
   using VT = typename V16<T>::type;
   constexpr int NV = V16<T>::N;
@@ -251,10 +286,11 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
         px ^= xb;
       }
     }
-    Pair<T> st;
+    (void)alpha_next;
+    typename CSEntry<T>::type st;
     st.a = m1 | (px & kS);
     st.b = m2;
-    lds_at<Pair<T>>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
+    lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
   }
   return mism;
 }
@@ -412,7 +448,7 @@ __device__ inline int c_check_any(unsigned char* smem, const RLayout& Ly, int m,
 }
 
 // One sector pass over `cn` shots (chunk-relative), one decode in flight.
-template <typename T, int DMAX, int VPL, bool MC, int ENG>
+template <typename T, int DMAX, int VPL, bool MC, int ENG, int D3K>
 __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned char* smem, const RLayout& Ly,
                        int vslots, int mmax, uint32_t* failmap, unsigned long long* cnt, const SMcArgs* A,
                        const SDecArgs* D, int tid, int TB) {
@@ -459,8 +495,8 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         const unsigned long long gshot = A->shot_begin + (unsigned long long)sl;
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
-          const int j = k * TB + tidl;
-          if (j < n) {
+          const int j = S.perm[k * TB + tidl];
+          if (j >= 0) {
             uint32_t cls;
             if (A->uniforms) {
               const double u = A->uniforms[sl * (long long)n + j];
@@ -516,7 +552,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     if constexpr (ENG == 4)
       c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     else
-      r_check<T, true>(smem, Ly, m, nch, tid, TB, sb);
+      r_check<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     __syncthreads();
     if (tid < 10) lred[tid] = 0;  // lred read above (before the barrier); flags[0..1] start clear
     // ---------------------------------------------------------- iterations
@@ -533,9 +569,11 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         mism = c_check_any<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha);
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
-        xb = r_var<T, DMAX, VPL>(smem, R, fdelta, alpha, xb, last_live);
+        xb = r_var<T, DMAX, VPL, D3K>(smem, R, fdelta, alpha, xb, last_live);
         __syncthreads();
-        mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb);
+        // check state for iteration it + 1 (float: pre-scaled by its alpha)
+        const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
+        mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha_next);
       }
       if (__any(mism) && (tid & 63) == 0) flags[it & 1] = 1u;
       __syncthreads();
@@ -554,7 +592,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
           if ((r >> k) & 1u) {
-            const int j = k * TB + tidl;
+            const int j = S.perm[k * TB + tidl];
 #pragma unroll
             for (int w = 0; w < 4; ++w)
               if (w < S.kw) acc[w] ^= S.lmask[(long long)j * S.kw + w];
@@ -569,15 +607,15 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       if (A->corr) {
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
-          const int j = k * TB + tidl;
-          if (j < n) A->corr[(sl * 2 + q) * (long long)n + j] = (uint8_t)((xb >> k) & 1u);
+          const int j = S.perm[k * TB + tidl];
+          if (j >= 0) A->corr[(sl * 2 + q) * (long long)n + j] = (uint8_t)((xb >> k) & 1u);
         }
       }
     } else {
 #pragma unroll
       for (int k = 0; k < VPL; ++k) {
-        const int j = k * TB + tidl;
-        if (j < n) D->corr[sl * (long long)n + j] = (uint8_t)((xb >> k) & 1u);
+        const int j = S.perm[k * TB + tidl];
+        if (j >= 0) D->corr[sl * (long long)n + j] = (uint8_t)((xb >> k) & 1u);
       }
     }
     pshot = sh;
@@ -587,7 +625,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   __syncthreads();  // image reused by the next pass
 }
 
-template <typename T, int DMAX, int VPL, int ENG>
+template <typename T, int DMAX, int VPL, int ENG, int D3K>
 __global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
@@ -610,7 +648,7 @@ __global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
     for (int qi = 0; qi < A.nsec; ++qi) {
       const SSector S = pick_ssector(A, qi);
       const int q = qi == 0 ? A.sec_id0 : A.sec_id1;
-      r_pass<T, DMAX, VPL, true, ENG>(S, q, c0, cn, smem, Ly, A.vslots, A.mmax, q == 0 ? fm0 : fm1, cnt, &A, nullptr,
+      r_pass<T, DMAX, VPL, true, ENG, D3K>(S, q, c0, cn, smem, Ly, A.vslots, A.mmax, q == 0 ? fm0 : fm1, cnt, &A, nullptr,
                                  tid, TB);
     }
     // combine the sectors per shot (eval_logical_type, src/Simulators.py:162-168)
@@ -629,7 +667,7 @@ __global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
   if (tid < kCntHist && cnt[tid]) atomicAdd(&A.counters[tid], cnt[tid]);
 }
 
-template <typename T, int DMAX, int VPL, int ENG>
+template <typename T, int DMAX, int VPL, int ENG, int D3K>
 __global__ __launch_bounds__(kMaxThreadsS) void rdec_kernel(SDecArgs D) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
@@ -639,7 +677,7 @@ __global__ __launch_bounds__(kMaxThreadsS) void rdec_kernel(SDecArgs D) {
   for (long long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const long long c0 = ch * CH;
     const int cn = (int)(D.B - c0 < CH ? D.B - c0 : CH);
-    r_pass<T, DMAX, VPL, false, ENG>(D.sec, 0, c0, cn, smem, Ly, D.vslots, D.mmax, nullptr, nullptr, nullptr, &D, tid,
+    r_pass<T, DMAX, VPL, false, ENG, D3K>(D.sec, 0, c0, cn, smem, Ly, D.vslots, D.mmax, nullptr, nullptr, nullptr, &D, tid,
                                 TB);
   }
 }

@@ -59,14 +59,14 @@ SVariant get_svariant(int precision, int dmax, int ns) {
   return dmax == 4 ? get_svariant_f64_d4(ns) : get_svariant_f64_d8(ns);
 }
 
-SVariant get_rvariant(int engine, int precision, int vpl) {
+SVariant get_rvariant(int engine, int precision, int vpl, int d3k) {
   if (engine == 4) return precision == 32 ? get_r4variant_f32(vpl) : get_r4variant_f64(vpl);
-  return precision == 32 ? get_rvariant_f32(vpl) : get_rvariant_f64(vpl);
+  return precision == 32 ? get_rvariant_f32(vpl, d3k) : get_rvariant_f64(vpl);
 }
 
 // Slot-family kernels of an engine (2, 3 or 4).
-SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl) {
-  return engine >= 3 ? get_rvariant(engine, precision, vpl) : get_svariant(precision, dmax, ns);
+SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k) {
+  return engine >= 3 ? get_rvariant(engine, precision, vpl, d3k) : get_svariant(precision, dmax, ns);
 }
 
 int round_up(int x, int a) { return (x + a - 1) / a * a; }
@@ -273,8 +273,8 @@ static int upload_llr(qldpc_bp* bp) {
   std::vector<double> l64(cnt, 1.0);
   for (int k = 0; k < VPL; ++k)
     for (int t = 0; t < TB; ++t) {
-      const int j = k * TB + t;
-      if (j < n) l64[(size_t)k * TB + t] = std::log((1.0 - bp->probs[j]) / bp->probs[j]);  // glibc log, as Cython
+      const int j = bp->slot_var.empty() ? (k * TB + t < n ? k * TB + t : -1) : bp->slot_var[(size_t)k * TB + t];
+      if (j >= 0) l64[(size_t)k * TB + t] = std::log((1.0 - bp->probs[j]) / bp->probs[j]);  // glibc log, as Cython
     }
   if (bp->precision == 32) {
     std::vector<float> l32(cnt);
@@ -286,30 +286,70 @@ static int upload_llr(qldpc_bp* bp) {
   return 0;
 }
 
-// Engine-2 edge table: for variable j = k*TB + t and its d-th check i (rows
-// ascending), the word ((i + 1) | slot<<16) where slot is j's position in row i
-// of the row-major V image (after the 16-byte sink), with the 16-byte chunks of
-// row i XOR-swizzled so that consecutive rows read by consecutive lanes hit
-// distinct LDS banks.  Missing edges are the word 0 (dummies, bp_slot.h).
+// Engine-2/3 edge table: for slot (k, t) holding variable j = slot_var[k*TB+t]
+// and its d-th check i (rows ascending), the word ((i + 1) | slot<<16) where
+// slot is the position of edge (i, j) in row i of the row-major V image (after
+// the 16-byte sink), with the 16-byte chunks of row i XOR-swizzled so that
+// consecutive rows read by consecutive lanes hit distinct LDS banks.  Missing
+// edges are the word 0 (dummies, bp_slot.h).
+//
+// Where an edge sits inside its row is free (the check phase takes an
+// order-independent min / second min / parity), so with `vbase_dw` >= 0 (engine
+// 3, fp32: dword offset of V in the image) the positions are chosen greedily,
+// per v2c store instruction of the variable phase (slot (k, t), 32-lane half
+// wave), to spread its 32 stores over the 32 banks: at most 2 per bank, which
+// ds_write_b32 absorbs for free (MI355X_MICROARCH.md §LDS).  vbase_dw < 0
+// keeps the ascending-column order (engine 4 relies on it).
 static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
-                             std::vector<uint32_t>& out) {
+                             const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1) {
   const int nv = 16 / tsize;  // messages per 16-byte chunk
   const int rw = nch * nv;
   const int swz_mask = (nch == 2) ? 1 : (nch == 4) ? 3 : 0;
   const int swz_shift = (nch == 2) ? 3 : 2;
+  auto phys = [&](int i, int ls) { return nv + i * rw + ((ls / nv) ^ ((i >> swz_shift) & swz_mask)) * nv + ls % nv; };
+  // logical slot of every edge (CSR order); default = ascending column position
+  std::vector<int> lslot(g->nnz);
+  for (int i = 0; i < g->m; ++i)
+    for (int e = g->row_ptr[i]; e < g->row_ptr[i + 1]; ++e) lslot[e] = e - g->row_ptr[i];
+  auto edge_of = [&](int i, int j) {
+    const int32_t* b = g->col_idx.data() + g->row_ptr[i];
+    const int32_t* e = g->col_idx.data() + g->row_ptr[i + 1];
+    return (int)(std::lower_bound(b, e, (int32_t)j) - g->col_idx.data());
+  };
+  if (vbase_dw >= 0 && tsize == 4 && rw <= 32) {
+    std::vector<uint32_t> used(g->m, 0u);
+    for (int k = 0; k < VPL; ++k)
+      for (int d = 0; d < DM; ++d)
+        for (int h0 = 0; h0 < TB; h0 += 32) {
+          int cnt[32] = {0};
+          for (int t = h0; t < h0 + 32 && t < TB; ++t) {
+            const int j = slot_var[(size_t)k * TB + t];
+            if (j < 0 || d >= (int)g->col_rows[j].size()) continue;
+            const int i = g->col_rows[j][d];
+            int best = -1, bc = 1 << 30;
+            for (int ls = 0; ls < rw; ++ls) {
+              if ((used[i] >> ls) & 1u) continue;
+              const int c = cnt[(vbase_dw + phys(i, ls)) & 31];
+              if (c < bc) {
+                bc = c;
+                best = ls;
+              }
+            }
+            used[i] |= 1u << best;
+            cnt[(vbase_dw + phys(i, best)) & 31]++;
+            lslot[edge_of(i, j)] = best;
+          }
+        }
+  }
   out.assign((size_t)VPL * DM * TB, kNoEdgeS);
   for (int k = 0; k < VPL; ++k)
     for (int t = 0; t < TB; ++t) {
-      const int j = k * TB + t;
-      if (j >= g->n) continue;
+      const int j = slot_var[(size_t)k * TB + t];
+      if (j < 0) continue;
       const auto& rows = g->col_rows[j];
       for (int d = 0; d < (int)rows.size(); ++d) {
         const int i = rows[d];
-        const int32_t* b = g->col_idx.data() + g->row_ptr[i];
-        const int32_t* e = g->col_idx.data() + g->row_ptr[i + 1];
-        const int pos = (int)(std::lower_bound(b, e, (int32_t)j) - b);
-        const int chunk = (pos / nv) ^ ((i >> swz_shift) & swz_mask);
-        const int slot = nv + i * rw + chunk * nv + pos % nv;
+        const int slot = phys(i, lslot[edge_of(i, j)]);
         out[((size_t)k * DM + d) * TB + t] = (uint32_t)(i + 1) | ((uint32_t)slot << 16);
       }
     }
@@ -395,6 +435,7 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
     bp->vchk.release();
     bp->llr.release();
     bp->rdeg.release();
+    bp->perm.release();
     delete bp;
     return code;
   };
@@ -443,14 +484,44 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
       bp->lds_bytes = (int)slot_lds_bytes(bp->NS, img, kChunkMax);
     }
     if (bp->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB (use precision 32)"));
-    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, vchk);
-    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL).dec_k;
+    // slot -> variable map: identity, or (engine 3) degree <= 3 variables first
+    const int TB = bp->TB, VPL = bp->VPL;
+    std::vector<int32_t> order;
+    order.reserve(g->n);
+    const bool sort3 = bp->engine == 3 && DM == 4 && env_int("QLDPC_DEGSORT", 1) != 0;
+    for (int pass = 0; pass < (sort3 ? 2 : 1); ++pass)
+      for (int j = 0; j < g->n; ++j)
+        if (!sort3 || ((int)g->col_rows[j].size() <= 3) == (pass == 0)) order.push_back(j);
+    bp->slot_var.assign((size_t)VPL * TB, -1);
+    for (int j = 0; j < g->n; ++j) bp->slot_var[j] = order[j];
+    bp->d3k = 0;
+    if (sort3)
+      for (int k = 0; k < VPL; ++k) {
+        bool ok = true;
+        for (int t = 0; t < TB && ok; ++t) {
+          const int j = bp->slot_var[(size_t)k * TB + t];
+          ok = j < 0 || (int)g->col_rows[j].size() <= 3;
+        }
+        if (!ok) break;
+        bp->d3k = k + 1;
+      }
+    const int vbase_dw = (bp->engine == 3 && env_int("QLDPC_BANKOPT", 1) != 0)
+                             ? (int)(r_layout(3, vslots2, g->m, tsize).v / 4)
+                             : -1;
+    if (precision != 32) bp->d3k = 0;  // fp64 engine-3 kernels are built with D3K = 0 only
+    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw);
+    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k).dec_k;
   }
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
   if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)bp->VPL * bp->TB * tsize))) return fail(rc);
   if (hipMemcpy(bp->vchk.p, vchk.data(), vchk.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return fail(set_err(QLDPC_EHIP, "upload edge table"));
   if ((rc = upload_llr(bp))) return fail(rc);
+  if (!bp->slot_var.empty()) {
+    if ((rc = bp->perm.alloc(bp->slot_var.size() * 4))) return fail(rc);
+    if (hipMemcpy(bp->perm.p, bp->slot_var.data(), bp->slot_var.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(set_err(QLDPC_EHIP, "upload slot map"));
+  }
   if (bp->engine == 4) {
     std::vector<uint8_t> deg(std::max(1, g->m));
     for (int i = 0; i < g->m; ++i) deg[i] = (uint8_t)(g->row_ptr[i + 1] - g->row_ptr[i]);
@@ -468,7 +539,8 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
 
 int qldpc_bp_destroy(qldpc_bp* bp) {
   if (!bp) return 0;
-  for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp, &bp->ps_ce, &bp->ps_ws})
+  for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp, &bp->ps_ce,
+                    &bp->ps_ws})
     d->release();
   delete bp;
   return 0;
@@ -478,6 +550,12 @@ int qldpc_bp_set_channel_probs(qldpc_bp* bp, const double* channel_probs) {
   if (!bp || !channel_probs) return set_err(QLDPC_EINVAL, "NULL argument");
   bp->probs.assign(channel_probs, channel_probs + bp->g->n);
   return upload_llr(bp);
+}
+
+int qldpc_bp_degree3_slots(const qldpc_bp* bp, int32_t* d3k) {
+  if (!bp || !d3k) return set_err(QLDPC_EINVAL, "NULL argument");
+  *d3k = bp->engine == 3 ? bp->d3k : 0;
+  return 0;
 }
 
 int qldpc_bp_engine(const qldpc_bp* bp, int32_t* engine) {
@@ -515,6 +593,8 @@ static SSector ssector_of(const qldpc_bp* bp, const unsigned long long* lmask, i
   s.llr = bp->llr.p;
   s.lmask = lmask;
   s.rdeg = static_cast<const uint8_t*>(bp->rdeg.p);
+  s.perm = static_cast<const int32_t*>(bp->perm.p);
+  s.d3k = bp->d3k;
   s.m = bp->g->m;
   s.n = bp->g->n;
   s.kw = kw;
@@ -567,7 +647,7 @@ int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, 
     a.chunk = chunk_for(B, cap, bp->NS);
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
-    SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL);
+    SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;
@@ -645,6 +725,8 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   mc->TB = d0->TB;
   mc->VPL = d0->VPL;
   mc->DMAX = d0->DMAX;
+  // one kernel serves both sectors: only slots that hold degree <= 3 variables in both skip slot 4
+  mc->d3k = std::min(dec_x ? dec_x->d3k : 1 << 20, dec_z ? dec_z->d3k : 1 << 20);
   mc->precision = d0->precision;
   mc->mmax = std::max(dec_x ? dec_x->g->m : 0, dec_z ? dec_z->g->m : 0);
   const void* kern;
@@ -665,7 +747,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
       mc->NS = choose_ns(mc->img_bytes);
       mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
     }
-    kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL).mc_k;
+    kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k).mc_k;
   }
   if (mc->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB"));
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
@@ -763,7 +845,7 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.fail = d_fail; a.err = d_err; a.corr = d_corr; a.iters = d_iters;
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
-    SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL);
+    SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k);
     QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;

@@ -63,6 +63,11 @@ struct qldpc_bp {
   std::vector<double> probs;
   qldpc_rt::DevBuf vchk, llr;  // engine 1: packed u16 check ids; engines 2-4: edge words (check | slot<<16)
   qldpc_rt::DevBuf rdeg;       // engine 4: u8 row degrees
+  // engines 3/4: variable of each (k, t) slot (-1 = padding).  Engine 3 sorts
+  // degree <= 3 variables first so that slots k < d3k skip the 4th edge slot.
+  std::vector<int32_t> slot_var;
+  qldpc_rt::DevBuf perm;
+  int d3k = 0;
   // engine 5 (product-sum, bp_ps.hip): CSR / CSC on the device, optional HBM message workspace
   qldpc_rt::DevBuf ps_rp, ps_ci, ps_cp, ps_ce, ps_ws;
   long long ps_grid = 0;
@@ -75,6 +80,7 @@ struct qldpc_mc {
   qldpc_rt::DevBuf counters;
   int engine = 2, TB = 0, VPL = 0, DMAX = 0, NS = 1, precision = 64, lds_bytes = 0, blocks_per_cu = 0, cus = 0;
   int mmax = 0, vslots = 0, img_bytes = 0;
+  int d3k = 0;  // engine 3: compile-time degree-3 slot count of the kernel (min over sectors)
   // staged pipeline (staged.hip): product-sum decoders, or QLDPC_MC_STAGED=1
   bool staged = false;
   long long sbatch = 0;

@@ -34,7 +34,10 @@ Variant get_variant_f32_d4(int vpl);
 Variant get_variant_f32_d8(int vpl);
 Variant get_variant_f64_d4(int vpl);
 Variant get_variant_f64_d8(int vpl);
-SVariant get_rvariant_f32(int vpl);
+SVariant get_rvariant_f32(int vpl, int d3k);  // kern_r_f32_{a,b,c}.hip by VPL range
+SVariant get_rvariant_f32_a(int vpl, int d3k);
+SVariant get_rvariant_f32_b(int vpl, int d3k);
+SVariant get_rvariant_f32_c(int vpl, int d3k);
 SVariant get_rvariant_f64(int vpl);
 SVariant get_r4variant_f32(int vpl);
 SVariant get_r4variant_f64(int vpl);
@@ -103,34 +106,50 @@ SVariant pick_sns(int ns) {
   }
 }
 
-template <typename T, int VPL, int ENG>
+template <typename T, int VPL, int ENG, int D3K>
 hipError_t rlaunch_dec(dim3 g, dim3 b, size_t lds, hipStream_t s, const SDecArgs& a) {
-  hipLaunchKernelGGL((rdec_kernel<T, 4, VPL, ENG>), g, b, lds, s, a);
+  hipLaunchKernelGGL((rdec_kernel<T, 4, VPL, ENG, D3K>), g, b, lds, s, a);
   return hipGetLastError();
 }
-template <typename T, int VPL, int ENG>
+template <typename T, int VPL, int ENG, int D3K>
 hipError_t rlaunch_mc(dim3 g, dim3 b, size_t lds, hipStream_t s, const SMcArgs& a) {
-  hipLaunchKernelGGL((rmc_kernel<T, 4, VPL, ENG>), g, b, lds, s, a);
+  hipLaunchKernelGGL((rmc_kernel<T, 4, VPL, ENG, D3K>), g, b, lds, s, a);
   return hipGetLastError();
 }
-template <typename T, int VPL, int ENG>
+template <typename T, int VPL, int ENG, int D3K>
 SVariant make_rvariant() {
-  return SVariant{&rlaunch_dec<T, VPL, ENG>, &rlaunch_mc<T, VPL, ENG>,
-                  reinterpret_cast<const void*>(&rdec_kernel<T, 4, VPL, ENG>),
-                  reinterpret_cast<const void*>(&rmc_kernel<T, 4, VPL, ENG>)};
+  return SVariant{&rlaunch_dec<T, VPL, ENG, D3K>, &rlaunch_mc<T, VPL, ENG, D3K>,
+                  reinterpret_cast<const void*>(&rdec_kernel<T, 4, VPL, ENG, D3K>),
+                  reinterpret_cast<const void*>(&rmc_kernel<T, 4, VPL, ENG, D3K>)};
 }
+// D3K = 0 only (fp64 and engine 4)
 template <typename T, int ENG>
 SVariant pick_rvpl(int vpl) {
   switch (vpl) {
-    case 1: return make_rvariant<T, 1, ENG>();
-    case 2: return make_rvariant<T, 2, ENG>();
-    case 3: return make_rvariant<T, 3, ENG>();
-    case 4: return make_rvariant<T, 4, ENG>();
-    case 5: return make_rvariant<T, 5, ENG>();
-    case 6: return make_rvariant<T, 6, ENG>();
-    case 7: return make_rvariant<T, 7, ENG>();
-    case 8: return make_rvariant<T, 8, ENG>();
+    case 1: return make_rvariant<T, 1, ENG, 0>();
+    case 2: return make_rvariant<T, 2, ENG, 0>();
+    case 3: return make_rvariant<T, 3, ENG, 0>();
+    case 4: return make_rvariant<T, 4, ENG, 0>();
+    case 5: return make_rvariant<T, 5, ENG, 0>();
+    case 6: return make_rvariant<T, 6, ENG, 0>();
+    case 7: return make_rvariant<T, 7, ENG, 0>();
+    case 8: return make_rvariant<T, 8, ENG, 0>();
     default: return SVariant{nullptr, nullptr, nullptr, nullptr};
+  }
+}
+// every D3K in 0..VPL for one VPL
+template <typename T, int VPL, int ENG>
+SVariant pick_rd3k(int d3k) {
+  switch (d3k < 0 ? 0 : d3k > VPL ? VPL : d3k) {
+    case 0: return make_rvariant<T, VPL, ENG, 0>();
+    case 1: return make_rvariant<T, VPL, ENG, (1 <= VPL ? 1 : 0)>();
+    case 2: return make_rvariant<T, VPL, ENG, (2 <= VPL ? 2 : 0)>();
+    case 3: return make_rvariant<T, VPL, ENG, (3 <= VPL ? 3 : 0)>();
+    case 4: return make_rvariant<T, VPL, ENG, (4 <= VPL ? 4 : 0)>();
+    case 5: return make_rvariant<T, VPL, ENG, (5 <= VPL ? 5 : 0)>();
+    case 6: return make_rvariant<T, VPL, ENG, (6 <= VPL ? 6 : 0)>();
+    case 7: return make_rvariant<T, VPL, ENG, (7 <= VPL ? 7 : 0)>();
+    default: return make_rvariant<T, VPL, ENG, (8 <= VPL ? 8 : 0)>();
   }
 }
 #endif

@@ -108,6 +108,9 @@ class DeviceBP:
         _native.check(_native.lib().qldpc_bp_engine(self.handle, ctypes.byref(e)), "bp_engine")
         g = dict(zip(["threads", "vars_per_thread", "lds_bytes", "blocks_per_cu"], [x.value for x in v]))
         g["engine"] = e.value
+        d = ctypes.c_int32()
+        _native.check(_native.lib().qldpc_bp_degree3_slots(self.handle, ctypes.byref(d)), "bp_degree3_slots")
+        g["degree3_slots"] = d.value
         return g
 
     def decode_batch_device(self, synd_dev, corr_dev, iters_dev=None, conv_dev=None, stream=None):

@@ -29,4 +29,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_$c" -o p -- \
     python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > "$O/pmc_$c.json" 2> "$O/pmc_$c.err" || exit 1
 done
+step sq-counters
+timeout -k 10 400 bash "$R/tools/pmc_passes.sh" "gpurun_out/$TAG/sq" hgp_34_n1600 0.06 65536 > "$O/sq.log" 2>&1 || { tail "$O/sq.log"; exit 1; }
 echo "done $TAG"
