@@ -482,6 +482,17 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
       const int img = (int)slot_img_bytes(vslots2, g->m, tsize);
       bp->NS = choose_ns(img);
       bp->lds_bytes = (int)slot_lds_bytes(bp->NS, img, kChunkMax);
+      // big images leave room for few workgroups per CU: widen the workgroup so
+      // the CU still holds >= 16 waves (ST n1225 fp32: 1 x 1024 threads, 2x the
+      // samples/s of 1 x 256, bench.py --workload phenl)
+      const int bpc = std::max(1, kLdsMax / std::max(1, bp->lds_bytes));
+      if (vars_per_thread <= 0 && env_int("QLDPC_TB", 0) <= 0 && bpc * bp->TB / 64 < 16) {
+        const int tb = std::min(kMaxThreadsS, round_up((16 + bpc - 1) / bpc * 64, 64));
+        if (tb > bp->TB) {
+          bp->TB = tb;
+          bp->VPL = (g->n + tb - 1) / tb;
+        }
+      }
     }
     if (bp->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB (use precision 32)"));
     // slot -> variable map: identity, or (engine 3) degree <= 3 variables first
