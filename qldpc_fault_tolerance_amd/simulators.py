@@ -181,6 +181,139 @@ class CodeSimulator_DataError:
         return word_error_rate(error_count, num_run, self.K)
 
 
+def word_error_rate_phenl(error_count: int, num_samples: int, K: int, num_rounds: int):
+    """``CodeSimulator_Phenon.WordErrorRate`` arithmetic (``src/Simulators.py:329-358``)."""
+    assert int(num_rounds) % 2 == 1
+    ler = error_count / num_samples
+    ler_q = 1.0 - (1 - ler) ** (1 / K)
+    if ler_q <= 0.5:
+        return (1.0 - (1 - 2 * ler_q) ** (1 / num_rounds)) / 2
+    return (1.0 + (-1 + 2 * ler_q) ** (1 / num_rounds)) / 2
+
+
+class CodeSimulator_Phenon:
+    """Single-shot phenomenological simulator (``src/Simulators.py:189-381``).
+
+    Each noisy round decodes the extended syndrome ``[h | I]·[e | s_err]`` with
+    decoder1 (``BP_Decoder_Class`` with ``p_syndrome``, or ``FirstMinBPDecoder``
+    in the notebooks), then a perfect round is decoded by decoder2.  This is the
+    space-time loop with ``num_rep = 1`` (``GetSpaceTimeCheckMat(h, 1) = [h | I]``,
+    same draw order), so when decoder1_* are engine :class:`~.decoders.BPDecoder`
+    objects on ``[h | I]`` and decoder2_* engine ``BPDecoder`` objects, every
+    sample runs on the GPU (``qldpc_phenl_launch``).  Other decoders (e.g.
+    ``FirstMinBPDecoder``) run the reference's per-sample loop.
+    """
+
+    def __init__(self, code=None, decoder1_x=None, decoder1_z=None, decoder2_x=None, decoder2_z=None,
+                 pauli_error_probs=(0.01, 0.01, 0.01), q=0, eval_logical_type="Total", seed=None, max_batch=0):
+        self.code = code
+        self.hx_ext = np.hstack([code.hx, np.identity(np.shape(code.hx)[0])])
+        self.hz_ext = np.hstack([code.hz, np.identity(np.shape(code.hz)[0])])
+        self.decoder1_z, self.decoder1_x = decoder1_z, decoder1_x
+        self.decoder2_z, self.decoder2_x = decoder2_z, decoder2_x
+        self.N = code.N
+        self.K = code.K
+        self.channel_probs = list(pauli_error_probs)
+        self.synd_prob = q
+        self.error_x = np.zeros(self.N).astype(int)
+        self.error_z = np.zeros(self.N).astype(int)
+        self.min_logical_weight = self.N
+        self.eval_logical_type = eval_logical_type
+        self.seed = int(seed) if seed is not None else None
+        self.max_batch = int(max_batch)
+        self._shot_offset = 0
+        self._ph = None
+        self.last_result = None
+
+    def _generate_error(self):
+        """``:211-250``: data error (3-way split), then hx-row and hz-row syndrome flips."""
+        N = self.N
+        u = np.array([random.random() for _ in range(N)])
+        ex, ez = pauli_split(u, self.channel_probs)
+        sz = np.array([random.random() < self.synd_prob for _ in range(self.hx_ext.shape[1] - N)], dtype=int)
+        sx = np.array([random.random() < self.synd_prob for _ in range(self.hz_ext.shape[1] - N)], dtype=int)
+        self.error_x_ext = np.concatenate([ex, sx])
+        self.error_z_ext = np.concatenate([ez, sz])
+        return self.error_x_ext, self.error_z_ext
+
+    def _single_run(self, num_rounds):
+        """``:252-327``."""
+        code = self.code
+        N = self.N
+        mx, mz = code.hx.shape[0], code.hz.shape[0]
+        cz = np.zeros(N + mx, dtype=int)
+        cx = np.zeros(N + mz, dtype=int)
+        for _ in range(num_rounds - 1):
+            ex_ext, ez_ext = self._generate_error()
+            cx = (np.concatenate([cx[:N], np.zeros(mz, dtype=int)]) + ex_ext) % 2
+            cz = (np.concatenate([cz[:N], np.zeros(mx, dtype=int)]) + ez_ext) % 2
+            dz = np.asarray(self.decoder1_z.decode((self.hx_ext @ cz % 2).astype(int)))
+            dx = np.asarray(self.decoder1_x.decode((self.hz_ext @ cx % 2).astype(int)))
+            cx = (cx + dx.astype(int)) % 2
+            cz = (cz + dz.astype(int)) % 2
+        ex_ext, ez_ext = self._generate_error()
+        cur_x = ((cx + ex_ext) % 2)[:N]
+        cur_z = ((cz + ez_ext) % 2)[:N]
+        dz = self.decoder2_z.decode(code.hx @ cur_z % 2)
+        dx = self.decoder2_x.decode(code.hz @ cur_x % 2)
+        rx, rz = (cur_x + dx) % 2, (cur_z + dz) % 2
+        X_failure = int(((code.hz @ rx) % 2).any() or ((code.lz @ rx) % 2).any())
+        Z_failure = int(((code.hx @ rz) % 2).any() or ((code.lx @ rz) % 2).any())
+        assert self.eval_logical_type in ["X", "Z", "Total"]
+        if self.eval_logical_type == "X":
+            return X_failure
+        if self.eval_logical_type == "Z":
+            return Z_failure
+        return X_failure or Z_failure
+
+    def _engine_parts(self):
+        from .decoders import BPDecoder
+
+        d1 = (self.decoder1_x, self.decoder1_z)
+        if not all(isinstance(d, BPDecoder) for d in d1):
+            return None
+        b2 = (_engine_bp(self.decoder2_x), _engine_bp(self.decoder2_z))
+        if any(b is None for b in b2):
+            return None
+        return d1[0].decoder, d1[1].decoder, b2[0], b2[1]
+
+    def fused_counts(self, num_rounds: int, num_samples: int):
+        parts = self._engine_parts()
+        if parts is None:
+            raise TypeError("fused path needs engine BPDecoder instances (decoder1 on [h | I], decoder2 on h)")
+        from .engine import DevicePhenl, MCResult, _torch
+
+        torch = _torch()
+        if self.seed is None:
+            self.seed = random.getrandbits(64)
+        if self._ph is None:
+            self._ph = DevicePhenl(self.code, *parts, num_rep=1, max_batch=self.max_batch)
+        rank, ws = parallel.world()
+        b, c = parallel.shard_range(num_samples, rank, ws, begin=self._shot_offset)
+        self._shot_offset += int(num_samples)
+        px, py, pz = self.channel_probs
+        cnt = self._ph.new_counters()
+        self._ph.launch(px, py, pz, self.synd_prob, self.seed, b, c, num_rounds, self.eval_logical_type, cnt)
+        parallel.allreduce_counters(cnt)
+        torch.cuda.synchronize(cnt.device)
+        res = MCResult.from_words(cnt.cpu().numpy())
+        self.last_result = res
+        return res
+
+    def _count(self, num_rounds, num_samples):
+        if self._engine_parts() is not None:
+            return self.fused_counts(num_rounds, num_samples).failures
+        return int(np.sum([self._single_run(num_rounds) for _ in range(num_samples)]))
+
+    def WordErrorRate(self, num_rounds: int, num_samples: int):
+        error_count = self._count(num_rounds, num_samples)
+        return word_error_rate_phenl(error_count, num_samples, self.K, num_rounds), None
+
+    def WordErrorProbability(self, num_rounds: int, num_samples: int):
+        """``:360-381`` (the A8 formulas on the end-of-run failure count)."""
+        return word_error_rate(self._count(num_rounds, num_samples), num_samples, self.K)
+
+
 class CodeSimulator_Phenon_SpaceTime:
     """Phenomenological space-time simulator (``src/Simulators_SpaceTime.py:382-548``).
 
@@ -312,7 +445,7 @@ class CodeSimulator_Phenon_SpaceTime:
 
 
 class CodeFamily:
-    """``src/Simulators.py:746-963`` (code-capacity ``'data'`` noise model)."""
+    """``src/Simulators.py:746-963`` (``'data'`` and ``'phenl'`` noise models; ``'circuit'`` needs stim)."""
 
     def __init__(self, code_list: list, decoder1_class, decoder2_class):
         self.code_list = code_list
@@ -323,14 +456,27 @@ class CodeFamily:
                 data_synd_noise_ratio=1, circuit_type="coloration", circuit_error_params=None, if_plot=True):
         assert noise_model in ["data", "phenl", "circuit"], "noise_model should be one of [data, phenl, circuit]"
         assert eval_logical_type in ["X", "Z", "Total"], "eval_type should be one of [X, Y, Total]"
-        if noise_model != "data":
-            raise NotImplementedError(f"noise_model={noise_model!r}: the engine covers the code-capacity path "
-                                      "(phenomenological: CodeSimulator_Phenon_SpaceTime; circuit level needs stim)")
+        if noise_model == "circuit":
+            raise NotImplementedError("circuit-level noise needs stim's circuits / detector error models (absent)")
         eval_wer_list = []
         for eval_code in self.code_list:
             for eval_p in eval_p_list:
                 p = eval_p * 3 / 2
                 pauli_error_probs = [p / 3, p / 3, p / 3]  # src/Simulators.py:763-764
+                if noise_model == "phenl":  # src/Simulators.py:779-809
+                    q = eval_p
+                    p_data, p_synd = p * 2 / 3, q
+                    hx_ext = np.hstack([eval_code.hx, np.identity(np.shape(eval_code.hx)[0])])
+                    hz_ext = np.hstack([eval_code.hz, np.identity(np.shape(eval_code.hz)[0])])
+                    d1x = self.decoder1_class.GetDecoder({"h": hz_ext, "p_data": p_data, "p_syndrome": p_synd})
+                    d1z = self.decoder1_class.GetDecoder({"h": hx_ext, "p_data": p_data, "p_syndrome": p_synd})
+                    d2x = self.decoder2_class.GetDecoder({"h": eval_code.hz, "p_data": p_data})
+                    d2z = self.decoder2_class.GetDecoder({"h": eval_code.hx, "p_data": p_data})
+                    sim = CodeSimulator_Phenon(code=eval_code, decoder1_x=d1x, decoder1_z=d1z, decoder2_x=d2x,
+                                               decoder2_z=d2z, pauli_error_probs=pauli_error_probs, q=q,
+                                               eval_logical_type=eval_logical_type)
+                    eval_wer_list.append(sim.WordErrorRate(num_rounds=num_cycles, num_samples=num_samples)[0])
+                    continue
                 decoder_x = self.decoder2_class.GetDecoder({"h": eval_code.hz, "p_data": eval_p})
                 decoder_z = self.decoder2_class.GetDecoder({"h": eval_code.hx, "p_data": eval_p})
                 sim = CodeSimulator_DataError(code=eval_code, decoder_x=decoder_x, decoder_z=decoder_z,

@@ -2,7 +2,8 @@
 
 Run in the build container only (``/root/reference`` is not on the GPU box):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py          # reference_harness_n225.npz
+    python tests/golden/make_golden.py phen     # reference_harness_phen_n225.npz
 
 The reference modules import third-party packages that are absent here
 (``graph_tools``, ``ldpc``, ``bposd``, ``stim``, …), so empty stub
@@ -229,5 +230,75 @@ def main():
     print("wrote", os.path.join(HERE, "reference_harness_n225.npz"), len(out), "arrays")
 
 
+def main_phen():
+    """Single-shot phenomenological simulator (CodeSimulator_Phenon, src/Simulators.py:189-381) and
+    FirstMinBPDecoder (src/Decoders.py:49-74) -> tests/golden/reference_harness_phen_n225.npz."""
+    install_stubs()
+    import Decoders
+    import Simulators
+
+    Simulators.parmap = lambda f, X, nprocs=1: [f(x) for x in X]
+    code = codes.get_code("hgp_34_n225")
+    n, mx, mz = code.N, code.hx.shape[0], code.hz.shape[0]
+    out = {}
+
+    class Capture:
+        def __init__(self, inner):
+            self.inner, self.seen = inner, []
+
+        def decode(self, x):
+            self.seen.append(np.array(x, dtype=np.uint8))
+            return self.inner.decode(x)
+
+    p = 0.02
+    cls = Decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    hx_ext = np.hstack([code.hx, np.identity(mx)])
+    hz_ext = np.hstack([code.hz, np.identity(mz)])
+    d1x = Capture(cls.GetDecoder({"h": hz_ext, "p_data": p, "p_syndrome": p}))
+    d1z = Capture(cls.GetDecoder({"h": hx_ext, "p_data": p, "p_syndrome": p}))
+    d2x = Capture(cls.GetDecoder({"h": code.hz, "p_data": p}))
+    d2z = Capture(cls.GetDecoder({"h": code.hx, "p_data": p}))
+    out["phen_factory_max_iter_arg"] = np.array([d1x.inner.max_iter, d2x.inner.max_iter], dtype=np.float64)
+    sim = Simulators.CodeSimulator_Phenon(code=code, decoder1_x=d1x, decoder1_z=d1z, decoder2_x=d2x,
+                                          decoder2_z=d2z, pauli_error_probs=[p / 2] * 3, q=p,
+                                          eval_logical_type="Total")
+    num_rounds = 3
+    n_u = num_rounds * (n + mx + mz)
+    flags, U = [], []
+    for s in range(16):
+        random.seed(7000 + s)
+        flags.append(int(sim._single_run(num_rounds)))
+        random.seed(7000 + s)
+        U.append([random.random() for _ in range(n_u)])
+    out["phen_fail"] = np.array(flags, dtype=np.uint8)
+    out["phen_u"] = np.array(U)
+    out["phen_d1z_synd"] = np.array(d1z.seen)
+    out["phen_d1x_synd"] = np.array(d1x.seen)
+    out["phen_d2z_synd"] = np.array(d2z.seen)
+    out["phen_d2x_synd"] = np.array(d2x.seen)
+    # WordErrorRate / WordErrorProbability formulas (:329-381) on injected failure counts
+    cases = []
+    for num_rounds_, num_samples, nfail in [(3, 100, 9), (5, 400, 77), (1, 50, 50)]:
+        sim2 = Simulators.CodeSimulator_Phenon(code=code, pauli_error_probs=[p / 2] * 3, q=p)
+        for fn in ("WordErrorRate", "WordErrorProbability"):
+            fl = [1] * nfail + [0] * (num_samples - nfail)
+            sim2._single_run = (lambda num_rounds, it=iter(fl): next(it))
+            w, eb = getattr(sim2, fn)(num_rounds_, num_samples)
+            cases.append([num_rounds_, num_samples, nfail, 0 if fn == "WordErrorRate" else 1, w,
+                          np.nan if eb is None else eb])
+    out["phen_wer_cases"] = np.array(cases, dtype=np.float64)
+    # FirstMinBPDecoder: repeated max_iter=1 BP with the syndrome-weight stopping rule
+    rng = np.random.default_rng(11)
+    fm = Decoders.FirstMinBPDecoder(hz_ext, np.hstack([p * np.ones(n), p * np.ones(mz)]), 20, "minimum_sum", 0.625)
+    S = (rng.random((24, mz)) < 0.06).astype(np.uint8)
+    out["firstmin_synd"] = S
+    out["firstmin_corr"] = np.array([fm.decode(s.astype(float)) for s in S], dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "reference_harness_phen_n225.npz"), **out)
+    print("wrote", os.path.join(HERE, "reference_harness_phen_n225.npz"), len(out), "arrays")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "phen":
+        main_phen()
+    else:
+        main()

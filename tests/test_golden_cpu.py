@@ -209,3 +209,61 @@ def test_oracle_mc_shard_invariance(n225, oracle):
         tot = parts[0][key]
         tot = tot + parts[1][key] if not isinstance(tot, list) else [x + y for x, y in zip(tot, parts[1][key])]
         assert tot == whole[key], key
+
+
+# ---------------------------------------------------------------- single-shot phenomenological (§8f rank 1)
+@pytest.fixture(scope="module")
+def phen_gold():
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_harness_phen_n225.npz"))
+
+
+def test_oracle_phen_single_shot_replays_reference(phen_gold, n225, oracle):
+    """CodeSimulator_Phenon (src/Simulators.py:189-327) = the space-time loop at num_rep = 1: the oracle's
+    restatement fed CPython's recorded uniforms reproduces the reference's decoder inputs and failures."""
+    p, m = 0.02, n225.hz.shape[0]
+    r = oracle.phenl_run(n225, p / 2, p / 2, p / 2, p, 0, 0, 16, 3, 1, "Total", p_data=p, p_synd=p,
+                         uniforms=phen_gold["phen_u"], per_shot=True)
+    body = r["trace"][:, :2 * 2 * m].reshape(16, 2, 2, m)
+    assert np.array_equal(body[:, :, 0].reshape(32, m), phen_gold["phen_d1z_synd"])
+    assert np.array_equal(body[:, :, 1].reshape(32, m), phen_gold["phen_d1x_synd"])
+    assert np.array_equal(r["trace"][:, 4 * m:5 * m], phen_gold["phen_d2z_synd"])
+    assert np.array_equal(r["trace"][:, 5 * m:], phen_gold["phen_d2x_synd"])
+    assert np.array_equal((r["fail"] != 0).astype(np.uint8), phen_gold["phen_fail"])
+
+
+def test_phen_single_shot_plugin_path(phen_gold, n225, oracle):
+    """The drop-in CodeSimulator_Phenon._single_run (CPython random, oracle-backed BP decoders) == reference."""
+    import random
+
+    p = 0.02
+
+    class OracleBP:
+        def __init__(self, h, probs):
+            self.h, self.probs = h, probs
+
+        def decode(self, s):
+            return oracle.bp_decode_batch(self.h, self.probs, 22, synd=np.asarray(s).reshape(1, -1))[0][0].astype(int)
+
+    mx, mz, n = n225.hx.shape[0], n225.hz.shape[0], n225.N
+    ext = lambda h: np.hstack([h, np.identity(h.shape[0])])  # noqa: E731
+    sim = simulators.CodeSimulator_Phenon(
+        code=n225, decoder1_x=OracleBP(ext(n225.hz), np.hstack([p * np.ones(n), p * np.ones(mz)])),
+        decoder1_z=OracleBP(ext(n225.hx), np.hstack([p * np.ones(n), p * np.ones(mx)])),
+        decoder2_x=OracleBP(n225.hz, p), decoder2_z=OracleBP(n225.hx, p), pauli_error_probs=[p / 2] * 3, q=p)
+    flags = []
+    for s in range(16):
+        random.seed(7000 + s)
+        flags.append(int(sim._single_run(3)))
+    assert flags == phen_gold["phen_fail"].tolist()
+    # BP_Decoder_Class with p_syndrome: max_iter = (n_ext - m)/ratio = n/ratio (src/Decoders.py:154-162)
+    assert list(phen_gold["phen_factory_max_iter_arg"]) == [n / 10, n / 10]
+
+
+def test_phen_wer_formulas_match_reference(phen_gold):
+    """WordErrorRate (:329-358) and WordErrorProbability (:360-381) of CodeSimulator_Phenon."""
+    for num_rounds, num_samples, nfail, which, w, eb in phen_gold["phen_wer_cases"]:
+        if int(which) == 0:
+            assert simulators.word_error_rate_phenl(int(nfail), int(num_samples), 17, int(num_rounds)) == w
+        else:
+            w2, eb2 = simulators.word_error_rate(int(nfail), int(num_samples), 17)
+            assert w2 == w and ((eb2 == eb) or (np.isnan(eb2) and np.isnan(eb)))

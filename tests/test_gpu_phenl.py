@@ -125,3 +125,62 @@ def test_phenl_simulator_dropin(gpu, oracle):
     ref = oracle.phenl_run(code, pp, pp, pp, eval_p, 99, 0, 500, 3, 3, "Total", p_data=eval_p, p_synd=eval_p)
     assert none is None
     assert wer == simulators.word_error_rate_per_cycle(ref["failures"], 500, code.K, 7)
+
+
+# ------------------------------------------------ single-shot phenomenological (CodeSimulator_Phenon, num_rep = 1)
+PHEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_harness_phen_n225.npz")
+
+
+def _phen_dropin(code, p, seed=None, precision=64):
+    cls = decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625,
+                                    precision=precision)
+    ext = lambda h: np.hstack([h, np.identity(h.shape[0])])  # noqa: E731
+    d1x = cls.GetDecoder({"h": ext(code.hz), "p_data": p, "p_syndrome": p})
+    d1z = cls.GetDecoder({"h": ext(code.hx), "p_data": p, "p_syndrome": p})
+    d2x = cls.GetDecoder({"h": code.hz, "p_data": p})
+    d2z = cls.GetDecoder({"h": code.hx, "p_data": p})
+    return simulators.CodeSimulator_Phenon(code=code, decoder1_x=d1x, decoder1_z=d1z, decoder2_x=d2x,
+                                           decoder2_z=d2z, pauli_error_probs=[p / 2] * 3, q=p,
+                                           eval_logical_type="Total", seed=seed)
+
+
+def test_phen_single_shot_replays_reference_harness(gpu):
+    """CodeSimulator_Phenon on the GPU (DevicePhenl, num_rep=1) replays the reference harness bit for bit."""
+    g = np.load(PHEN)
+    code = codes.get_code("hgp_34_n225")
+    p, m = 0.02, code.hz.shape[0]
+    sim = _phen_dropin(code, p)
+    from qldpc_fault_tolerance_amd.engine import DevicePhenl
+
+    ph = DevicePhenl(code, *sim._engine_parts(), num_rep=1)
+    res = ph.run(p / 2, p / 2, p / 2, p, 0, 0, 16, 3, "Total", uniforms=g["phen_u"], per_shot=True)
+    body = res.trace[:, :4 * m].reshape(16, 2, 2, m)
+    assert np.array_equal(body[:, :, 0].reshape(32, m), g["phen_d1z_synd"])
+    assert np.array_equal(body[:, :, 1].reshape(32, m), g["phen_d1x_synd"])
+    assert np.array_equal(res.trace[:, 4 * m:5 * m], g["phen_d2z_synd"])
+    assert np.array_equal(res.trace[:, 5 * m:], g["phen_d2x_synd"])
+    assert np.array_equal((res.fail != 0).astype(np.uint8), g["phen_fail"])
+
+
+def test_phen_single_shot_dropin_matches_oracle(gpu, oracle):
+    code = codes.get_code("hgp_34_n225")
+    p = 0.02
+    sim = _phen_dropin(code, p, seed=2024)
+    wer, none = sim.WordErrorRate(5, 700)
+    ref = oracle.phenl_run(code, p / 2, p / 2, p / 2, p, 2024, 0, 700, 5, 1, "Total", p_data=p, p_synd=p)
+    assert none is None
+    assert wer == simulators.word_error_rate_phenl(ref["failures"], 700, code.K, 5)
+    assert sim.last_result.sector_iters == ref["sector_iters"]
+
+
+def test_firstmin_decoder_matches_reference_fixture(gpu):
+    """FirstMinBPDecoder (src/Decoders.py:49-74) over the engine == the reference class on the oracle BP."""
+    g = np.load(PHEN)
+    code = codes.get_code("hgp_34_n225")
+    p = 0.02
+    hz_ext = np.hstack([code.hz, np.identity(code.hz.shape[0])])
+    fm = decoders.FirstMinBPDecoder(hz_ext, np.hstack([p * np.ones(code.N), p * np.ones(code.hz.shape[0])]), 20,
+                                    "minimum_sum", 0.625)
+    out = fm.decode_batch(g["firstmin_synd"])
+    assert np.array_equal(out.astype(np.uint8), g["firstmin_corr"])
+    assert np.array_equal(fm.decode(g["firstmin_synd"][3]).astype(np.uint8), g["firstmin_corr"][3])
