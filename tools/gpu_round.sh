@@ -29,6 +29,12 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_$c" -o p -- \
     python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > "$O/pmc_$c.json" 2> "$O/pmc_$c.err" || exit 1
 done
+step phenl
+timeout -k 10 300 python3 "$R/bench.py" --workload phenl --p 0.005 --shots 65536 --steps 3 --warmup 1 > "$O/bench_phenl.json" 2> "$O/bench_phenl.err" || { tail "$O/bench_phenl.err"; exit 1; }
+cat "$O/bench_phenl.json"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_phenl" -o run -- \
+  python3 "$R/bench.py" --workload phenl --p 0.005 --shots 65536 --steps 1 --warmup 1 > "$O/bench_phenl_trace.json" 2> "$O/bench_phenl_trace.err" || exit 1
+
 step sq-counters
 timeout -k 10 400 bash "$R/tools/pmc_passes.sh" "gpurun_out/$TAG/sq" hgp_34_n1600 0.06 65536 > "$O/sq.log" 2>&1 || { tail "$O/sq.log"; exit 1; }
 echo "done $TAG"
