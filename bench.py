@@ -91,7 +91,8 @@ def kernel_name(dec):
     """Name of the fused MC kernel the decoder's geometry selects (as rocprofv3 reports it)."""
     g = dec.geometry()
     t = "float" if dec.precision == 32 else "double"
-    dmax = 4 if dec.graph.info()["max_col_deg"] <= 4 else 8
+    mc = dec.graph.info()["max_col_deg"]
+    dmax = 4 if mc <= 4 else (mc if g["engine"] == 3 and mc <= 6 and dec.precision == 32 else 8)
     if g["engine"] >= 3:
         return f"qldpc::rmc_kernel<{t}, {dmax}, {g['vars_per_thread']}, {g['engine']}, {g['degree3_slots']}>"
     return f"qldpc::smc_kernel<{t}, {dmax}, 1> (engine {g['engine']})"

@@ -211,7 +211,7 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, u
                                  uint32_t xprev, bool last_live) {
   using U = typename FT<T>::U;
   constexpr bool KV = RState<T, DMAX, VPL>::kKeepV;
-  constexpr int N3 = DMAX == 4 ? 3 : DMAX;
+  constexpr int N3 = DMAX > 3 ? 3 : DMAX;  // low-degree slots use 3 edge slots
   r_launder(R);
   uint32_t xbits = 0;
   typename CSEntry<T>::type pn[DMAX];

@@ -59,14 +59,16 @@ SVariant get_svariant(int precision, int dmax, int ns) {
   return dmax == 4 ? get_svariant_f64_d4(ns) : get_svariant_f64_d8(ns);
 }
 
-SVariant get_rvariant(int engine, int precision, int vpl, int d3k) {
+SVariant get_rvariant(int engine, int precision, int vpl, int d3k, int dmax) {
   if (engine == 4) return precision == 32 ? get_r4variant_f32(vpl) : get_r4variant_f64(vpl);
+  if (precision == 32 && dmax == 5) return get_rvariant_f32_d5(vpl, d3k);
+  if (precision == 32 && dmax == 6) return get_rvariant_f32_d6(vpl, d3k);
   return precision == 32 ? get_rvariant_f32(vpl, d3k) : get_rvariant_f64(vpl);
 }
 
 // Slot-family kernels of an engine (2, 3 or 4).
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k) {
-  return engine >= 3 ? get_rvariant(engine, precision, vpl, d3k) : get_svariant(precision, dmax, ns);
+  return engine >= 3 ? get_rvariant(engine, precision, vpl, d3k, dmax) : get_svariant(precision, dmax, ns);
 }
 
 int round_up(int x, int a) { return (x + a - 1) / a * a; }
@@ -147,7 +149,7 @@ int choose_sgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
 // nonzero if engine 3 cannot take the graph (the caller falls back to engine 2).
 constexpr int kMaxVplR = 8;
 constexpr int kPrefVplR = 7;
-int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
+int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL, int pref = kPrefVplR, int vmax = kMaxVplR) {
   const int forced_tb = env_int("QLDPC_TB", 0);
   if (requested_vpl > 0) {
     VPL = requested_vpl;
@@ -157,10 +159,10 @@ int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL) {
     VPL = (n + TB - 1) / TB;
   } else {
     TB = 64;
-    while (TB < kMaxThreadsS && ((n + TB - 1) / TB > kPrefVplR || (m + TB - 1) / TB > 32)) TB *= 2;
+    while (TB < kMaxThreadsS && ((n + TB - 1) / TB > pref || (m + TB - 1) / TB > 32)) TB *= 2;
     VPL = (n + TB - 1) / TB;
   }
-  if (TB > kMaxThreadsS || TB < 64 || VPL < 1 || VPL > kMaxVplR || (m + TB - 1) / TB > 32) return 1;
+  if (TB > kMaxThreadsS || TB < 64 || VPL < 1 || VPL > vmax || (m + TB - 1) / TB > 32) return 1;
   return 0;
 }
 
@@ -429,7 +431,11 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
   bp->method = bp_method;
   bp->alpha = ms_scaling_factor;
   bp->precision = precision;
-  bp->DMAX = std::max(g->max_col, (int)min_col_slots) <= 4 ? 4 : 8;
+  const int colmax = std::max(g->max_col, (int)min_col_slots);
+  bp->DMAX = colmax <= 4 ? 4 : 8;
+  // engine 3 also takes fp32 graphs with column degree 5-6 (lifted-product codes), exact slot count
+  if (bp->engine == 3 && precision == 32 && colmax > 4 && colmax <= 6 && env_int("QLDPC_E3_D56", 1) != 0)
+    bp->DMAX = colmax;
   bp->probs.assign(channel_probs, channel_probs + g->n);
   auto fail = [&](int code) {
     bp->vchk.release();
@@ -440,7 +446,7 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
     return code;
   };
   const int tsize = precision == 32 ? 4 : 8;
-  const int DM = bp->DMAX;
+  int DM = bp->DMAX;
   std::vector<uint32_t> vchk;
   const void* kern = nullptr;
   int rc;
@@ -467,10 +473,14 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
     bp->nch = bp->engine == 4 ? 8 * tsize / 16 : (std::max(1, g->max_row) * tsize + 15) / 16;
     const int vslots = (1 + g->m * bp->nch) * (16 / tsize);
     if (vslots >= 0xFFFF) return fail(set_err(QLDPC_ENOTSUP, "V image exceeds 65535 message slots"));
-    if (bp->engine >= 3 && (DM != 4 || choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL) ||
+    // degree-5/6 variables hold 2.5x the registers of degree-4 ones: fewer per thread
+    const int pref = DM == 4 ? kPrefVplR : 4, vmax = DM == 4 ? kMaxVplR : 5;
+    if (bp->engine >= 3 && ((DM != 4 && !(bp->engine == 3 && (DM == 5 || DM == 6))) ||
+                            choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL, pref, vmax) ||
                             !r_fits(bp->engine, vslots, g->m, tsize))) {
       bp->engine = 2;  // graph outside the register engines' envelope
       bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
+      if (DM == 5 || DM == 6) bp->DMAX = DM = 8;  // engine 2 kernels come in 4 and 8 slots
     }
     const int vslots2 = (1 + g->m * bp->nch) * (16 / tsize);
     if (bp->engine >= 3) {
@@ -499,7 +509,7 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
     const int TB = bp->TB, VPL = bp->VPL;
     std::vector<int32_t> order;
     order.reserve(g->n);
-    const bool sort3 = bp->engine == 3 && DM == 4 && env_int("QLDPC_DEGSORT", 1) != 0;
+    const bool sort3 = bp->engine == 3 && DM >= 4 && env_int("QLDPC_DEGSORT", 1) != 0;
     for (int pass = 0; pass < (sort3 ? 2 : 1); ++pass)
       for (int j = 0; j < g->n; ++j)
         if (!sort3 || ((int)g->col_rows[j].size() <= 3) == (pass == 0)) order.push_back(j);

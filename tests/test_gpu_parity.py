@@ -51,7 +51,7 @@ def test_decode_adaptive_alpha_matches_oracle(gpu, oracle):
 
 
 @pytest.mark.parametrize("precision", [64, 32])
-@pytest.mark.parametrize("name", ["hgp_34_n225", "hgp_34_n1600"])
+@pytest.mark.parametrize("name", ["hgp_34_n225", "hgp_34_n1600", "LP_Matg8_L30_Dmin20", "GenBicycleA4"])
 def test_mc_per_shot_matches_oracle(gpu, oracle, precision, name):
     from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceMC
 
@@ -62,6 +62,8 @@ def test_mc_per_shot_matches_oracle(gpu, oracle, precision, name):
     px = py = pz = p / 2
     dx = DeviceBP(code.hz, (px + py) * np.ones(n), max_iter=mi, precision=precision)
     dz = DeviceBP(code.hx, (pz + py) * np.ones(n), max_iter=mi, precision=precision)
+    if precision == 32:  # the register engine serves every config graph in fp32 (column degree <= 6)
+        assert dx.geometry()["engine"] == 3
     mc = DeviceMC(code, dx, dz)
     S = 300 if n > 1000 else 1500
     res = mc.run(px, py, pz, seed=0x51D5EED0, shot_begin=12345, shot_count=S, logical_mode="Total", per_shot=True)
