@@ -35,6 +35,15 @@
 
 namespace qldpc {
 
+// Engine ids of this file: 3, 4, and 13 = engine 3 with dword-scaled edge
+// addresses (images of 64-256 KiB: the space-time graphs).
+constexpr int eng_base(int E) { return E % 10; }
+constexpr int eng_sh(int E) { return E >= 10 ? 2 : 0; }
+template <int ENG>
+__device__ inline uint32_t ea_cs(uint32_t ea) { return (ea & 0xFFFFu) << eng_sh(ENG); }
+template <int ENG>
+__device__ inline uint32_t ea_v(uint32_t ea) { return (ea >> 16) << eng_sh(ENG); }
+
 struct RLayout {
   uint32_t v, f, sink, lred, total;  // byte offsets (engine 3: CS at 0; engine 4: V at 0)
 };
@@ -91,7 +100,7 @@ __device__ inline uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
 template <typename T, int DMAX, int VPL, int ENG = 3>
 struct RState {
   using U = typename FT<T>::U;
-  static constexpr bool kKeepV = ENG == 3 && sizeof(T) == 4;  // own v2c in VGPRs (engine 3, float)
+  static constexpr bool kKeepV = eng_base(ENG) == 3 && sizeof(T) == 4;  // own v2c in VGPRs (engine 3, float)
   uint32_t ea[VPL][DMAX];
   T L[VPL];
   U ov[kKeepV ? VPL : 1][kKeepV ? DMAX : 1];
@@ -106,10 +115,10 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
     for (int t = 0; t < DMAX; ++t) {
       const uint32_t e = S.edges[(k * DMAX + t) * TB + tid];
       const uint32_t va = Ly.v + eslot(e) * (uint32_t)sizeof(T);
-      if (ENG == 4)
+      if (eng_base(ENG) == 4)
         R.ea[k][t] = e == kNoEdgeS ? (Ly.v | (Ly.sink << 16)) : (va | (va << 16));
       else
-        R.ea[k][t] = (echk(e) * (uint32_t)(2 * sizeof(T))) | (va << 16);
+        R.ea[k][t] = ((echk(e) * (uint32_t)(2 * sizeof(T))) >> eng_sh(ENG)) | ((va >> eng_sh(ENG)) << 16);
     }
     R.L[k] = (S.perm[k * TB + tid] >= 0) ? llr[k * TB + tid] : (T)1;
   }
@@ -125,8 +134,8 @@ struct FMap {
 };
 template <typename T, int ENG>
 __device__ inline uint32_t f_addr(uint32_t ea, const FMap& M) {
-  if (ENG == 4) return M.fbase + 4u * (uint32_t)((int)((ea & 0xFFFFu) - M.rstart) >> M.rsh);
-  return ((ea & 0xFFFFu) >> (sizeof(T) == 4 ? 1 : 2)) + M.fbase;
+  if (eng_base(ENG) == 4) return M.fbase + 4u * (uint32_t)((int)((ea & 0xFFFFu) - M.rstart) >> M.rsh);
+  return (ea_cs<ENG>(ea) >> (sizeof(T) == 4 ? 1 : 2)) + M.fbase;
 }
 
 // Opaque redefinition of the edge words (no instruction): without it the
@@ -145,25 +154,25 @@ __device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
 // flipped since the previous iteration (xprev) xor their checks.  Slots k < D3K
 // (compile time) hold variables of column degree <= 3 (host-sorted), so their
 // 4th edge slot is skipped entirely (no gather, no arithmetic, no store).
-template <typename T, int DMAX, int VPL, int ND>
-__device__ inline void r_gather(unsigned char* smem, const RState<T, DMAX, VPL>& R, int k,
+template <typename T, int DMAX, int VPL, int ND, int ENG>
+__device__ inline void r_gather(unsigned char* smem, const RState<T, DMAX, VPL, ENG>& R, int k,
                                 typename CSEntry<T>::type (&pn)[DMAX],
                                 typename FT<T>::U (&on)[DMAX]) {
-  constexpr bool KV = RState<T, DMAX, VPL>::kKeepV;
+  constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
-    pn[t] = lds_at<typename CSEntry<T>::type>(smem, R.ea[k][t] & 0xFFFFu);
-    if (!KV) on[t] = FT<T>::bits(lds_at<T>(smem, R.ea[k][t] >> 16));
+    pn[t] = lds_at<typename CSEntry<T>::type>(smem, ea_cs<ENG>(R.ea[k][t]));
+    if (!KV) on[t] = FT<T>::bits(lds_at<T>(smem, ea_v<ENG>(R.ea[k][t])));
   }
 }
 
-template <typename T, int DMAX, int VPL, int ND>
-__device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL>& R, int k,
+template <typename T, int DMAX, int VPL, int ND, int ENG>
+__device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, int k,
                                  const typename CSEntry<T>::type (&pr)[DMAX],
                                  const typename FT<T>::U (&o)[DMAX], uint32_t fdelta, T alpha, bool xprev) {
   using U = typename FT<T>::U;
   constexpr U kS = FT<T>::kSign;
-  constexpr bool KV = RState<T, DMAX, VPL>::kKeepV;
+  constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
   T c[ND];
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
@@ -195,31 +204,31 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL>& R, i
   }
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
-    lds_at<U>(smem, R.ea[k][t] >> 16) = nv[t];
+    lds_at<U>(smem, ea_v<ENG>(R.ea[k][t])) = nv[t];
     if (KV) R.ov[KV ? k : 0][KV ? t : 0] = nv[t];
   }
   if (x != xprev) {
 #pragma unroll
     for (int t = 0; t < ND; ++t)
-      atomicXor(&lds_at<uint32_t>(smem, ((R.ea[k][t] & 0xFFFFu) >> (sizeof(T) == 4 ? 1 : 2)) + fdelta), 1u);
+      atomicXor(&lds_at<uint32_t>(smem, (ea_cs<ENG>(R.ea[k][t]) >> (sizeof(T) == 4 ? 1 : 2)) + fdelta), 1u);
   }
   return x;
 }
 
-template <typename T, int DMAX, int VPL, int D3K>
-__device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, uint32_t fdelta, T alpha,
+template <typename T, int DMAX, int VPL, int D3K, int ENG>
+__device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, uint32_t fdelta, T alpha,
                                  uint32_t xprev, bool last_live) {
   using U = typename FT<T>::U;
-  constexpr bool KV = RState<T, DMAX, VPL>::kKeepV;
+  constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
   constexpr int N3 = DMAX > 3 ? 3 : DMAX;  // low-degree slots use 3 edge slots
   r_launder(R);
   uint32_t xbits = 0;
   typename CSEntry<T>::type pn[DMAX];
   U on[DMAX];
   if (0 < D3K)
-    r_gather<T, DMAX, VPL, N3>(smem, R, 0, pn, on);
+    r_gather<T, DMAX, VPL, N3, ENG>(smem, R, 0, pn, on);
   else
-    r_gather<T, DMAX, VPL, DMAX>(smem, R, 0, pn, on);
+    r_gather<T, DMAX, VPL, DMAX, ENG>(smem, R, 0, pn, on);
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     typename CSEntry<T>::type pr[DMAX];
@@ -231,14 +240,14 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL>& R, u
     }
     if (k + 1 < VPL) {  // next variable's gathers go out before this one's arithmetic
       if (k + 1 < D3K)
-        r_gather<T, DMAX, VPL, N3>(smem, R, k + 1, pn, on);
+        r_gather<T, DMAX, VPL, N3, ENG>(smem, R, k + 1, pn, on);
       else
-        r_gather<T, DMAX, VPL, DMAX>(smem, R, k + 1, pn, on);
+        r_gather<T, DMAX, VPL, DMAX, ENG>(smem, R, k + 1, pn, on);
     }
     if (k == VPL - 1 && !last_live) break;  // every lane of this wave holds padding
     const bool xp = ((xprev >> k) & 1u) != 0;
-    const bool x = k < D3K ? r_var_one<T, DMAX, VPL, N3>(smem, R, k, pr, o, fdelta, alpha, xp)
-                           : r_var_one<T, DMAX, VPL, DMAX>(smem, R, k, pr, o, fdelta, alpha, xp);
+    const bool x = k < D3K ? r_var_one<T, DMAX, VPL, N3, ENG>(smem, R, k, pr, o, fdelta, alpha, xp)
+                           : r_var_one<T, DMAX, VPL, DMAX, ENG>(smem, R, k, pr, o, fdelta, alpha, xp);
     xbits |= (x ? 1u : 0u) << k;
   }
   return xbits;
@@ -423,12 +432,12 @@ __device__ inline void r_fill(const SSector& S, unsigned char* smem, const RLayo
   VT* V4 = reinterpret_cast<VT*>(smem + Ly.v);
   const VT s = V16<T>::splat(FT<T>::val(FT<T>::kSent));
   // engine 4: the first chunk is the zero chunk missing edges read
-  for (int i = tid; i < vslots / V16<T>::N; i += TB) V4[i] = (ENG == 4 && i == 0) ? V16<T>::splat((T)0) : s;
+  for (int i = tid; i < vslots / V16<T>::N; i += TB) V4[i] = (eng_base(ENG) == 4 && i == 0) ? V16<T>::splat((T)0) : s;
   uint32_t* F = reinterpret_cast<uint32_t*>(smem + Ly.f);
-  for (int i = tid; i <= mmax; i += TB) F[i] = (ENG == 4 && i >= 1 && i <= S.m) ? ((uint32_t)S.rdeg[i - 1] << 16) : 0u;
+  for (int i = tid; i <= mmax; i += TB) F[i] = (eng_base(ENG) == 4 && i >= 1 && i <= S.m) ? ((uint32_t)S.rdeg[i - 1] << 16) : 0u;
   uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);
   if (tid < 10) lred[tid] = 0;  // lred[0..7], flags[0..1]
-  if (ENG == 3 && tid == 0) {
+  if (eng_base(ENG) == 3 && tid == 0) {
     Pair<T> z;
     z.a = 0;
     z.b = 0;
@@ -459,7 +468,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   r_load<T, DMAX, VPL, ENG>(S, R, Ly, tid, TB);
   r_fill<T, ENG>(S, smem, Ly, vslots, mmax, tid, TB);
   FMap M;
-  M.fbase = ENG == 4 ? Ly.f + 4u : Ly.f;
+  M.fbase = eng_base(ENG) == 4 ? Ly.f + 4u : Ly.f;
   M.rstart = Ly.v + 16u;
   M.rsh = 4 + __builtin_ctz((unsigned)nch);
   const uint32_t fdelta = Ly.f;
@@ -485,7 +494,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         const U cl = canon2<T>(R.L[k]);
 #pragma unroll
         for (int t = 0; t < DMAX; ++t) {
-          lds_at<U>(smem, R.ea[k][t] >> 16) = cl;
+          lds_at<U>(smem, ea_v<ENG>(R.ea[k][t])) = cl;
           if (KV) R.ov[KV ? k : 0][KV ? t : 0] = cl;
         }
       }
@@ -518,7 +527,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         const uint8_t* srow = D->synd + (c0 + sh) * (long long)m;
         for (int i = tidl; i < m; i += TB) {
           uint32_t& F = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
-          F = (ENG == 4 ? (F & 0xFFFF0000u) : 0u) | ((uint32_t)(srow[i] & 1u) << 1);
+          F = (eng_base(ENG) == 4 ? (F & 0xFFFF0000u) : 0u) | ((uint32_t)(srow[i] & 1u) << 1);
         }
       }
     }
@@ -549,7 +558,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     }
     if (!have) break;
     // ---------------------------------------------------------- first check pass (CS / c2v from priors)
-    if constexpr (ENG == 4)
+    if constexpr (eng_base(ENG) == 4)
       c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     else
       r_check<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
@@ -561,7 +570,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     uint32_t xb = 0;
     while (true) {
       int mism;
-      if constexpr (ENG == 4) {
+      if constexpr (eng_base(ENG) == 4) {
         xb = c_var<T, DMAX, VPL>(smem, R, M, last_live);
         __syncthreads();
         // c2v for iteration it + 1 (wasted if this one converged)
@@ -569,7 +578,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         mism = c_check_any<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha);
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
-        xb = r_var<T, DMAX, VPL, D3K>(smem, R, fdelta, alpha, xb, last_live);
+        xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live);
         __syncthreads();
         // check state for iteration it + 1 (float: pre-scaled by its alpha)
         const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
@@ -631,7 +640,7 @@ __global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = A.chunk;
   const int fw = (CH + 31) / 32;
-  const RLayout Ly = r_layout(ENG, A.vslots, A.mmax, (int)sizeof(T));
+  const RLayout Ly = r_layout(eng_base(ENG), A.vslots, A.mmax, (int)sizeof(T));
   uint32_t* fm0 = reinterpret_cast<uint32_t*>(smem + Ly.total);
   uint32_t* fm1 = fm0 + ((fw + 3) & ~3);
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(fm1 + ((fw + 3) & ~3));
@@ -672,7 +681,7 @@ __global__ __launch_bounds__(kMaxThreadsS) void rdec_kernel(SDecArgs D) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = D.chunk;
-  const RLayout Ly = r_layout(ENG, D.vslots, D.mmax, (int)sizeof(T));
+  const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T));
   const long long nchunks = (D.B + CH - 1) / CH;
   for (long long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const long long c0 = ch * CH;

@@ -67,7 +67,9 @@ SVariant get_rvariant(int engine, int precision, int vpl, int d3k, int dmax) {
 }
 
 // Slot-family kernels of an engine (2, 3 or 4).
-SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k) {
+SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0) {
+  if (engine == 3 && ea_shift == 2)
+    return (precision == 32 && dmax == 4) ? get_rvariant_f32_big(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
   return engine >= 3 ? get_rvariant(engine, precision, vpl, d3k, dmax) : get_svariant(precision, dmax, ns);
 }
 
@@ -167,9 +169,11 @@ int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL, int pre
 }
 
 // Engines 3 and 4 address their image with 16-bit byte offsets.
-bool r_fits(int eng, int vslots, int mmax, int tsize) {
+// Engines 3 and 4 address their image with 16-bit byte offsets; engine 3 with
+// dword-scaled offsets (kernel id 13, ea_shift 2) reaches 256 KiB.
+bool r_fits(int eng, int vslots, int mmax, int tsize, int ea_shift = 0) {
   const RLayout L = r_layout(eng, vslots, mmax, tsize);
-  return L.lred <= 65536u && r_lds_bytes((int)L.total, kChunkMax) <= (size_t)kLdsMax;
+  return L.lred <= (65536u << ea_shift) && r_lds_bytes((int)L.total, kChunkMax) <= (size_t)kLdsMax;
 }
 
 // Slots per workgroup: QLDPC_NS, else 1 (independent workgroups interleave
@@ -475,9 +479,14 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
     if (vslots >= 0xFFFF) return fail(set_err(QLDPC_ENOTSUP, "V image exceeds 65535 message slots"));
     // degree-5/6 variables hold 2.5x the registers of degree-4 ones: fewer per thread
     const int pref = DM == 4 ? kPrefVplR : 4, vmax = DM == 4 ? kMaxVplR : 5;
+    // images of 64-256 KiB (space-time graphs): engine 3 with dword-scaled addresses (fp32, 4 slots)
+    if (bp->engine == 3 && precision == 32 && DM == 4 && !r_fits(3, vslots, g->m, tsize) &&
+        r_fits(3, vslots, g->m, tsize, 2) && env_int("QLDPC_E3_BIG", 1) != 0)
+      bp->ea_shift = 2;
     if (bp->engine >= 3 && ((DM != 4 && !(bp->engine == 3 && (DM == 5 || DM == 6))) ||
                             choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL, pref, vmax) ||
-                            !r_fits(bp->engine, vslots, g->m, tsize))) {
+                            !r_fits(bp->engine, vslots, g->m, tsize, bp->ea_shift))) {
+      bp->ea_shift = 0;
       bp->engine = 2;  // graph outside the register engines' envelope
       bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
       if (DM == 5 || DM == 6) bp->DMAX = DM = 8;  // engine 2 kernels come in 4 and 8 slots
@@ -531,7 +540,7 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
                              : -1;
     if (precision != 32) bp->d3k = 0;  // fp64 engine-3 kernels are built with D3K = 0 only
     build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw);
-    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k).dec_k;
+    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift).dec_k;
   }
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
   if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)bp->VPL * bp->TB * tsize))) return fail(rc);
@@ -668,7 +677,7 @@ int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, 
     a.chunk = chunk_for(B, cap, bp->NS);
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
-    SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k);
+    SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;
@@ -746,6 +755,9 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   mc->TB = d0->TB;
   mc->VPL = d0->VPL;
   mc->DMAX = d0->DMAX;
+  mc->ea_shift = std::max(dec_x ? dec_x->ea_shift : 0, dec_z ? dec_z->ea_shift : 0);
+  if (dec_x && dec_z && dec_x->ea_shift != dec_z->ea_shift)
+    return fail(set_err(QLDPC_EINVAL, "sector decoders use different LDS address scales"));
   // one kernel serves both sectors: only slots that hold degree <= 3 variables in both skip slot 4
   mc->d3k = std::min(dec_x ? dec_x->d3k : 1 << 20, dec_z ? dec_z->d3k : 1 << 20);
   mc->precision = d0->precision;
@@ -760,7 +772,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
       if (d) mc->vslots = std::max(mc->vslots, (1 + d->g->m * d->nch) * (16 / tsize));
     mc->img_bytes = (int)slot_img_bytes(mc->vslots, mc->mmax, tsize);
     if (mc->engine >= 3) {
-      if (!r_fits(mc->engine, mc->vslots, mc->mmax, tsize))
+      if (!r_fits(mc->engine, mc->vslots, mc->mmax, tsize, mc->ea_shift))
         return fail(set_err(QLDPC_ENOTSUP, "sector images exceed the register engines' 64 KiB addressing (QLDPC_ENGINE=2)"));
       mc->NS = 1;
       mc->lds_bytes = (int)r_lds_bytes((int)r_layout(mc->engine, mc->vslots, mc->mmax, tsize).total, kChunkMax);
@@ -768,7 +780,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
       mc->NS = choose_ns(mc->img_bytes);
       mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
     }
-    kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k).mc_k;
+    kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift).mc_k;
   }
   if (mc->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB"));
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
@@ -866,7 +878,7 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.fail = d_fail; a.err = d_err; a.corr = d_corr; a.iters = d_iters;
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
-    SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k);
+    SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift);
     QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;

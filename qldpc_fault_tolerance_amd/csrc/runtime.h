@@ -68,6 +68,7 @@ struct qldpc_bp {
   std::vector<int32_t> slot_var;
   qldpc_rt::DevBuf perm;
   int d3k = 0;
+  int ea_shift = 0;  // engine 3: 2 = dword-scaled LDS addresses in the edge words (images > 64 KiB)
   // engine 5 (product-sum, bp_ps.hip): CSR / CSC on the device, optional HBM message workspace
   qldpc_rt::DevBuf ps_rp, ps_ci, ps_cp, ps_ce, ps_ws;
   long long ps_grid = 0;
@@ -81,6 +82,7 @@ struct qldpc_mc {
   int engine = 2, TB = 0, VPL = 0, DMAX = 0, NS = 1, precision = 64, lds_bytes = 0, blocks_per_cu = 0, cus = 0;
   int mmax = 0, vslots = 0, img_bytes = 0;
   int d3k = 0;  // engine 3: compile-time degree-3 slot count of the kernel (min over sectors)
+  int ea_shift = 0;
   // staged pipeline (staged.hip): product-sum decoders, or QLDPC_MC_STAGED=1
   bool staged = false;
   long long sbatch = 0;

@@ -38,6 +38,7 @@ SVariant get_rvariant_f32(int vpl, int d3k);  // kern_r_f32_{a,b,c}.hip by VPL r
 SVariant get_rvariant_f32_a(int vpl, int d3k);
 SVariant get_rvariant_f32_b(int vpl, int d3k);
 SVariant get_rvariant_f32_c(int vpl, int d3k);
+SVariant get_rvariant_f32_big(int vpl, int d3k);  // kern_r_f32_big.hip: images of 64-256 KiB
 SVariant get_rvariant_f32_d5(int vpl, int d3k);  // kern_r_f32_d56.hip: column degree 5
 SVariant get_rvariant_f32_d6(int vpl, int d3k);  //                      column degree 6
 SVariant get_rvariant_f64(int vpl);

@@ -98,6 +98,7 @@ def test_phenl_n1225_space_time_graph(gpu, oracle):
     code = codes.get_code("hgp_34_n1225_q3")
     p = 0.01
     ph = _phenl(code, p, p, 3, precision=32)
+    assert ph.decoders[0].geometry()["engine"] == 3  # register engine with dword-scaled LDS addresses
     S, R = 96, 3
     res = ph.run(p / 2, p / 2, p / 2, p, 11, 0, S, R, per_shot=True)
     ref = oracle.phenl_run(code, p / 2, p / 2, p / 2, p, 11, 0, S, R, 3, "Total", p_data=p, p_synd=p,
