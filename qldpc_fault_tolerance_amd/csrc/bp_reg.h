@@ -279,20 +279,37 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
     }
     U m1 = FT<T>::kSent, m2 = FT<T>::kSent;
     U px = s ? kS : (U)0;
-    for (int c = 0; c < nch; ++c) {
-      const VT v = row[c];
+    if constexpr (sizeof(U) == 4) {
+      // float min / median with |x| source modifiers: on non-negative, non-NaN
+      // floats the float order is the bit order and v_med3_f32 returns one of its
+      // inputs unchanged, so this is the integer min / second min of |v2c| bits
+      // with the masking folded into the instructions
+      float f1 = FT<T>::val(m1), f2 = FT<T>::val(m2);
+      for (int c = 0; c < nch; ++c) {
+        const VT v = row[c];
 #pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        const U xb = FT<T>::bits(V16<T>::get(v, k));
-        const U a = xb & ~kS;
-        if constexpr (sizeof(U) == 4) {
-          m2 = med3u(m1, m2, a);  // m1 <= m2 holds, so the median is the new second minimum
-        } else {
+        for (int k = 0; k < NV; ++k) {
+          const float x = V16<T>::get(v, k);
+          f2 = __builtin_amdgcn_fmed3f(f1, f2, __builtin_fabsf(x));  // f1 <= f2: the new second minimum
+          // v_min_f32 with the |x| modifier (as a builtin, LLVM would add a canonicalize)
+          asm("v_min_f32 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
+          px ^= FT<T>::bits(x);
+        }
+      }
+      m1 = FT<T>::bits(f1);
+      m2 = FT<T>::bits(f2);
+    } else {
+      for (int c = 0; c < nch; ++c) {
+        const VT v = row[c];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          const U xb = FT<T>::bits(V16<T>::get(v, k));
+          const U a = xb & ~kS;
           const U hi = m1 > a ? m1 : a;
           m2 = m2 < hi ? m2 : hi;
+          m1 = m1 < a ? m1 : a;
+          px ^= xb;
         }
-        m1 = m1 < a ? m1 : a;
-        px ^= xb;
       }
     }
     (void)alpha_next;
