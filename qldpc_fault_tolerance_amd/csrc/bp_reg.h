@@ -87,6 +87,10 @@ __device__ inline typename FT<T>::U canon2(T v) {
   return b | ((b - (U)1) & ~b & FT<T>::kSign);
 }
 
+// x is +0 or -0 (v_cmp_class_*: class bits 5 = -0, 6 = +0)
+__device__ inline bool is_zero(float x) { return __builtin_amdgcn_classf(x, 0x60); }
+__device__ inline bool is_zero(double x) { return __builtin_amdgcn_class(x, 0x60); }
+
 // median of three (the backend selects v_med3_u32 for this pattern)
 __device__ inline uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
@@ -181,8 +185,22 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     // min over the other edges: m2 if this edge holds m1 (|own| == m1), else m1;
     // sign = parity of the others and the syndrome = sign bit of d
     // (m2 carries no sign bit, so masking after the select is the same value;
-    // masking `a` before it trips an instruction-selection crash in this LLVM)
-    const U sel = (((d & ~kS) == 0) ? pr[t].b : a) & ~kS;
+    // masking `a` before it trips an instruction-selection crash in this LLVM).
+    // |d| == 0 is tested with v_cmp_class (+-0 only): one instruction instead of
+    // mask + compare (bit patterns of any class, denormals and NaNs included).
+    U sel;
+    if constexpr (sizeof(T) == 4) {
+      // v_cmp_class (+-0) feeding v_cndmask; LLVM would rewrite the class test as
+      // mask + integer compare.  s_nop 1: the VALU-writes-VCC -> VALU-reads-VCC
+      // hazard the compiler itself pads on gfx950.
+      asm("v_cmp_class_f32 vcc, %1, %2\n\ts_nop 1\n\tv_cndmask_b32 %0, %3, %4, vcc"
+          : "=v"(sel)
+          : "v"(d), "v"(0x60u), "v"(a), "v"(pr[t].b)
+          : "vcc");
+      sel &= ~kS;
+    } else {
+      sel = (is_zero(FT<T>::val(d)) ? pr[t].b : a) & ~kS;
+    }
     c[t] = FT<T>::val(FT<T>::bits(FT<T>::val(sel) * alpha) ^ (d & kS));
   }
   // ldpc column pass: forward partial sums from the prior, then backward
