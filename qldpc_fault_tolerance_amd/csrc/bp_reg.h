@@ -311,8 +311,12 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
           f2 = __builtin_amdgcn_fmed3f(f1, f2, __builtin_fabsf(x));  // f1 <= f2: the new second minimum
           // v_min_f32 with the |x| modifier (as a builtin, LLVM would add a canonicalize)
           asm("v_min_f32 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
-          px ^= FT<T>::bits(x);
         }
+        // parity of the chunk's sign bits: two three-input xors (v_bitop3 0x96 = a^b^c)
+        uint32_t p01, p23;
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(p01) : "v"((uint32_t)px), "v"(FT<T>::bits(v.x)), "v"(FT<T>::bits(v.y)));
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(p23) : "v"(p01), "v"(FT<T>::bits(v.z)), "v"(FT<T>::bits(v.w)));
+        px = p23;
       }
       m1 = FT<T>::bits(f1);
       m2 = FT<T>::bits(f2);
