@@ -172,13 +172,27 @@ class CodeSimulator_DataError:
         self.last_result = res
         return res
 
-    def WordErrorRate(self, num_run: int):
+    def _batch_failures(self, n: int) -> int:
         ok, _, _ = self._engine_ready()
         if ok:
-            error_count = self.fused_counts(num_run).failures
-        else:
-            error_count = int(np.sum([self._single_run() for _ in range(num_run)]))
-        return word_error_rate(error_count, num_run, self.K)
+            return self.fused_counts(n).failures
+        return int(np.sum([self._single_run() for _ in range(n)]))
+
+    def WordErrorRate(self, num_run: int):
+        return word_error_rate(self._batch_failures(num_run), num_run, self.K)
+
+    def WordErrorRate_TargetFailure(self, target_failures: int, batch_size: int, max_batches: int):
+        """Adaptive sampling (the reference's ``WordErrorRate_TargetFailure``,
+        src/Simulators_SpaceTime.py:1051-1077): batches of ``batch_size`` shots until
+        ``target_failures`` failures or ``max_batches``; returns ``(wer, total_samples)``.
+        Each batch's count is all-reduced, so every rank stops at the same batch."""
+        total, fails = 0, 0
+        for _ in range(int(max_batches)):
+            fails += self._batch_failures(batch_size)
+            total += int(batch_size)
+            if fails >= target_failures:
+                break
+        return word_error_rate(fails, total, self.K)[0], total
 
 
 def word_error_rate_phenl(error_count: int, num_samples: int, K: int, num_rounds: int):
@@ -431,14 +445,29 @@ class CodeSimulator_Phenon_SpaceTime:
         self.last_result = res
         return res
 
+    def _batch_failures(self, num_rounds: int, n: int) -> int:
+        if self._engine_parts() is not None:
+            return self.fused_counts(num_rounds, n).failures
+        return int(np.sum([self._single_run(num_rounds) for _ in range(n)]))
+
     def WordErrorRate(self, num_cycles: int, num_samples: int):
         num_rounds = int((num_cycles - 1) / self.num_rep + 1)
-        if self._engine_parts() is not None:
-            error_count = self.fused_counts(num_rounds, num_samples).failures
-        else:
-            error_count = int(np.sum([self._single_run(num_rounds) for _ in range(num_samples)]))
+        error_count = self._batch_failures(num_rounds, num_samples)
         total_num_cycles = (num_rounds - 1) * self.num_rep + 1
         return word_error_rate_per_cycle(error_count, num_samples, self.K, total_num_cycles), None
+
+    def WordErrorRate_TargetFailure(self, num_cycles: int, target_failures: int, batch_size: int, max_batches: int):
+        """Adaptive sampling (src/Simulators_SpaceTime.py:1051-1077) on this simulator:
+        batches until ``target_failures`` or ``max_batches``; returns ``(wer, total_samples)``."""
+        num_rounds = int((num_cycles - 1) / self.num_rep + 1)
+        total, fails = 0, 0
+        for _ in range(int(max_batches)):
+            fails += self._batch_failures(num_rounds, batch_size)
+            total += int(batch_size)
+            if fails >= target_failures:
+                break
+        total_num_cycles = (num_rounds - 1) * self.num_rep + 1
+        return word_error_rate_per_cycle(fails, total, self.K, total_num_cycles), total
 
 
 # -------------------------------------------------------------- code family

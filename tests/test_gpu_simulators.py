@@ -107,3 +107,24 @@ def test_fp32_decoded_vectors_agree_with_fp64(gpu, oracle):
     both = conv & ov
     agree_conv = np.mean([np.array_equal(corr[i], oc[i]) for i in np.flatnonzero(both)])
     assert agree_conv >= 0.999, agree_conv
+
+
+def test_target_failure_adaptive_sampling(gpu, oracle):
+    """WordErrorRate_TargetFailure (src/Simulators_SpaceTime.py:1051-1077): stops at the first batch reaching the
+    target; the estimate is the A8 formula on the oracle's count over exactly the samples drawn."""
+    code = codes.get_code("hgp_34_n225")
+    p = 0.05
+    cls = decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    dx = cls.GetDecoder({"h": code.hz, "p_data": p})
+    dz = cls.GetDecoder({"h": code.hx, "p_data": p})
+    pp = p / 2
+    sim = simulators.CodeSimulator_DataError(code=code, decoder_x=dx, decoder_z=dz, pauli_error_probs=[pp] * 3,
+                                             eval_logical_type="Total", seed=77)
+    wer, total = sim.WordErrorRate_TargetFailure(target_failures=150, batch_size=100, max_batches=50)
+    ref = oracle.mc_run(code, pp, pp, pp, seed=77, shot_begin=0, shot_count=total, logical_mode="Total",
+                        probs_x=p, probs_z=p, max_iter=22, precision=64)
+    assert ref["failures"] >= 150
+    prev = oracle.mc_run(code, pp, pp, pp, seed=77, shot_begin=0, shot_count=total - 100, logical_mode="Total",
+                         probs_x=p, probs_z=p, max_iter=22, precision=64)
+    assert prev["failures"] < 150  # it stopped at the first batch that reached the target
+    assert wer == simulators.word_error_rate(ref["failures"], total, code.K)[0]
