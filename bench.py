@@ -194,10 +194,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
+    # one rank per GPU; QLDPC_SHARE_GPU=1 lets ranks share the visible GPUs (multi-rank rehearsal on a
+    # one-GPU box, with QLDPC_DIST_BACKEND=gloo since RCCL refuses two ranks on one device)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % ndev if os.environ.get("QLDPC_SHARE_GPU") == "1" else local)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("QLDPC_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     if a.workload == "phenl":
         return phenl_main(a, torch, dist, world, rank, dev)
@@ -213,11 +220,11 @@ def main():
     need_x, need_z = a.logical != "Z", a.logical != "X"
     # decoders as EvalWER builds them: p_data = eval_p on hz (X errors) and hx (Z errors)
     dx = DeviceBP(code.hz, p * np.ones(n), max_iter=max_iter, bp_method="minimum_sum", ms_scaling_factor=0.625,
-                  precision=a.precision, device=local) if need_x else None
+                  precision=a.precision, device=dev.index) if need_x else None
     # the Z-sector decoder takes the X sector's geometry (one fused kernel serves both)
     vpl = dx.geometry()["vars_per_thread"] if dx is not None and not os.environ.get("QLDPC_TB") else 0
     dz = DeviceBP(code.hx, p * np.ones(n), max_iter=max_iter, bp_method="minimum_sum", ms_scaling_factor=0.625,
-                  precision=a.precision, device=local, vars_per_thread=vpl) if need_z else None
+                  precision=a.precision, device=dev.index, vars_per_thread=vpl) if need_z else None
     mc = DeviceMC(code, dx, dz)
     S = int(a.shots)
     stream = torch.cuda.current_stream(dev)

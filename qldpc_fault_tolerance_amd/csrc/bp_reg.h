@@ -685,7 +685,16 @@ __global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(fm1 + ((fw + 3) & ~3));
   if (tid < kCntHist) cnt[tid] = 0;
   const long long nchunks = (A.shot_count + CH - 1) / CH;
-  for (long long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+  // chunks come from a queue (A.work): a workgroup that drew short decodes takes more
+  // chunks, so the launch does not wait on the unluckiest static share
+  __shared__ long long s_next;
+  long long ch = blockIdx.x;
+  if (A.work) {
+    if (tid == 0) s_next = (long long)atomicAdd(A.work, 1u);
+    __syncthreads();
+    ch = s_next;
+  }
+  for (; ch < nchunks;) {
     const long long c0 = ch * CH;
     const int cn = (int)(A.shot_count - c0 < CH ? A.shot_count - c0 : CH);
     for (int i = tid; i < fw; i += TB) {
@@ -708,8 +717,12 @@ __global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
       if (A.fail) A.fail[c0 + j] = (uint8_t)(fx | (fz << 1));
     }
     if (nf) atomicAdd(&cnt[kCntFail], nf);
-    if (tid == 0) cnt[kCntShots] += (unsigned long long)cn;
+    if (tid == 0) {
+      cnt[kCntShots] += (unsigned long long)cn;
+      if (A.work) s_next = (long long)atomicAdd(A.work, 1u);
+    }
     __syncthreads();
+    ch = A.work ? s_next : ch + gridDim.x;
   }
   __syncthreads();
   if (tid < kCntHist && cnt[tid]) atomicAdd(&A.counters[tid], cnt[tid]);

@@ -64,6 +64,7 @@ struct SMcArgs {
   uint8_t* err;
   uint8_t* corr;
   int* iters;
+  unsigned int* work;  // engine 3: chunk queue head (zeroed per launch), NULL = static chunk striding
 };
 
 struct SDecArgs {

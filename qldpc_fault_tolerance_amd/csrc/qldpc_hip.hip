@@ -743,6 +743,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
     mc->lmask[0].release();
     mc->lmask[1].release();
     mc->counters.release();
+    mc->work.release();
     delete mc;
     return code;
   };
@@ -788,7 +789,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, mc->TB, mc->lds_bytes) != hipSuccess) nb = 1;
   mc->blocks_per_cu = std::max(1, nb);
   mc->cus = d0->cus;
-  if ((rc = mc->counters.alloc(sizeof(qldpc_counters)))) return fail(rc);
+  if ((rc = mc->counters.alloc(sizeof(qldpc_counters))) || (rc = mc->work.alloc(16))) return fail(rc);
   *out = mc;
   return 0;
 }
@@ -798,6 +799,7 @@ int qldpc_mc_destroy(qldpc_mc* mc) {
   mc->lmask[0].release();
   mc->lmask[1].release();
   mc->counters.release();
+  mc->work.release();
   staged_mc_release(mc);
   delete mc;
   return 0;
@@ -870,6 +872,12 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.img_bytes = mc->img_bytes;
     const long long want = grid_blocks > 0 ? grid_blocks : cap;
     a.chunk = chunk_for(shot_count, want, mc->NS);
+    // engine 3: chunks from a queue, ~8 per workgroup (no tail behind the slowest static share)
+    if (mc->engine >= 3 && mc->work.p && env_int("QLDPC_DYN", 1) != 0) {
+      a.chunk = (int)std::max<long long>(8, std::min<long long>(kChunkMax, shot_count / (want * 8)));
+      QLDPC_HIP(hipMemsetAsync(mc->work.p, 0, 4, (hipStream_t)stream));
+      a.work = static_cast<unsigned int*>(mc->work.p);
+    }
     a.t1 = t1; a.t2 = t2; a.t3 = t3;
     a.K1 = ceil_2p53(t1); a.K2 = ceil_2p53(t2); a.K3 = ceil_2p53(t3);
     a.seed = seed; a.shot_begin = shot_begin; a.shot_count = shot_count;
