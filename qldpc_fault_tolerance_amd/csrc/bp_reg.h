@@ -735,11 +735,25 @@ __global__ __launch_bounds__(kMaxThreadsS) void rdec_kernel(SDecArgs D) {
   const int CH = D.chunk;
   const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T));
   const long long nchunks = (D.B + CH - 1) / CH;
-  for (long long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+  __shared__ long long s_next;
+  long long ch = blockIdx.x;
+  if (D.work) {
+    if (tid == 0) s_next = (long long)atomicAdd(D.work, 1u);
+    __syncthreads();
+    ch = s_next;
+  }
+  while (ch < nchunks) {
     const long long c0 = ch * CH;
     const int cn = (int)(D.B - c0 < CH ? D.B - c0 : CH);
     r_pass<T, DMAX, VPL, false, ENG, D3K>(D.sec, 0, c0, cn, smem, Ly, D.vslots, D.mmax, nullptr, nullptr, nullptr, &D, tid,
                                 TB);
+    if (D.work) {  // r_pass ends with a barrier: every thread has read s_next
+      if (tid == 0) s_next = (long long)atomicAdd(D.work, 1u);
+      __syncthreads();
+      ch = s_next;
+    } else {
+      ch += gridDim.x;
+    }
   }
 }
 

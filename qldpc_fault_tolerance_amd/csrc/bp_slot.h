@@ -75,6 +75,7 @@ struct SDecArgs {
   uint8_t* conv;
   long long B;
   int mmax, vslots, img_bytes, chunk;
+  unsigned int* work;  // engine 3: chunk queue head (zeroed per launch), NULL = static chunk striding
 };
 
 template <typename T> struct V16;

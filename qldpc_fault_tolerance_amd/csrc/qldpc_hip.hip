@@ -569,8 +569,8 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
 
 int qldpc_bp_destroy(qldpc_bp* bp) {
   if (!bp) return 0;
-  for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp, &bp->ps_ce,
-                    &bp->ps_ws})
+  for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->work, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp,
+                    &bp->ps_ce, &bp->ps_ws})
     d->release();
   delete bp;
   return 0;
@@ -675,6 +675,13 @@ int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, 
     a.vslots = (1 + bp->g->m * bp->nch) * (16 / tsize);
     a.img_bytes = (int)slot_img_bytes(a.vslots, a.mmax, tsize);
     a.chunk = chunk_for(B, cap, bp->NS);
+    a.work = nullptr;
+    if (bp->engine >= 3 && env_int("QLDPC_DYN", 1) != 0) {  // chunk queue, ~8 chunks per workgroup
+      if (!bp->work.p && bp->work.alloc(16)) return QLDPC_ENOMEM;
+      a.chunk = (int)std::max<long long>(1, std::min<long long>(kChunkMax, B / (cap * 8)));
+      QLDPC_HIP(hipMemsetAsync(bp->work.p, 0, 4, (hipStream_t)stream));
+      a.work = static_cast<unsigned int*>(bp->work.p);
+    }
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
     SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift);

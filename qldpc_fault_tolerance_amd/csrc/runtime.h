@@ -63,6 +63,7 @@ struct qldpc_bp {
   std::vector<double> probs;
   qldpc_rt::DevBuf vchk, llr;  // engine 1: packed u16 check ids; engines 2-4: edge words (check | slot<<16)
   qldpc_rt::DevBuf rdeg;       // engine 4: u8 row degrees
+  qldpc_rt::DevBuf work;       // engine 3 decode_batch: chunk-queue head
   // engines 3/4: variable of each (k, t) slot (-1 = padding).  Engine 3 sorts
   // degree <= 3 variables first so that slots k < d3k skip the 4th edge slot.
   std::vector<int32_t> slot_var;
