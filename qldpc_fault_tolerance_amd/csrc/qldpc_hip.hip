@@ -676,9 +676,9 @@ int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, 
     a.img_bytes = (int)slot_img_bytes(a.vslots, a.mmax, tsize);
     a.chunk = chunk_for(B, cap, bp->NS);
     a.work = nullptr;
-    if (bp->engine >= 3 && env_int("QLDPC_DYN", 1) != 0) {  // chunk queue, ~8 chunks per workgroup
+    if (bp->engine >= 3 && env_int("QLDPC_DYN", 1) != 0) {  // chunk queue, ~64 chunks per workgroup
       if (!bp->work.p && bp->work.alloc(16)) return QLDPC_ENOMEM;
-      a.chunk = (int)std::max<long long>(1, std::min<long long>(kChunkMax, B / (cap * 8)));
+      a.chunk = (int)std::max<long long>(1, std::min<long long>(kChunkMax, B / (cap * std::max(1, env_int("QLDPC_DYN_PER", 64)))));
       QLDPC_HIP(hipMemsetAsync(bp->work.p, 0, 4, (hipStream_t)stream));
       a.work = static_cast<unsigned int*>(bp->work.p);
     }
@@ -879,9 +879,10 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.img_bytes = mc->img_bytes;
     const long long want = grid_blocks > 0 ? grid_blocks : cap;
     a.chunk = chunk_for(shot_count, want, mc->NS);
-    // engine 3: chunks from a queue, ~8 per workgroup (no tail behind the slowest static share)
+    // engine 3: chunks from a queue, ~64 per workgroup (no tail behind the slowest static share)
     if (mc->engine >= 3 && mc->work.p && env_int("QLDPC_DYN", 1) != 0) {
-      a.chunk = (int)std::max<long long>(8, std::min<long long>(kChunkMax, shot_count / (want * 8)));
+      const int per = std::max(1, env_int("QLDPC_DYN_PER", 64));  // measured plateau 64-128 (n1600)
+      a.chunk = (int)std::max<long long>(1, std::min<long long>(kChunkMax, shot_count / (want * per)));
       QLDPC_HIP(hipMemsetAsync(mc->work.p, 0, 4, (hipStream_t)stream));
       a.work = static_cast<unsigned int*>(mc->work.p);
     }
