@@ -104,6 +104,41 @@ int qldpc_bp_decode_batch(qldpc_bp *bp, const uint8_t *d_synd, uint8_t *d_corr, 
                           uint8_t *d_conv, int64_t B, void *stream);
 
 /*
+ * Soft-output BP for BP+OSD (src/Decoders.py:26-41: `bposd_decoder` runs
+ * ldpc's BP, then OSD on its final `log_prob_ratios` when BP did not converge).
+ * qldpc_bp_create_soft builds a min-sum decoder on engine 1 (the kernel that
+ * can write posteriors); qldpc_bp_decode_batch_soft is qldpc_bp_decode_batch
+ * plus d_post: double [B][n] = the last iteration's posterior log-probability
+ * ratios (ldpc's log_prob_ratios; exact fp32 values widened in fp32 mode).
+ */
+int qldpc_bp_create_soft(qldpc_graph *g, const double *channel_probs, int32_t max_iter, double ms_scaling_factor,
+                         int32_t precision, qldpc_bp **out);
+int qldpc_bp_decode_batch_soft(qldpc_bp *bp, const uint8_t *d_synd, uint8_t *d_corr, int32_t *d_iters,
+                               uint8_t *d_conv, double *d_post, int64_t B, void *stream);
+
+/*
+ * Ordered-statistics decoding (the OSD half of `bposd_decoder(h,
+ * channel_probs, max_iter, bp_method, ms_scaling_factor, osd_method,
+ * osd_order)`, src/Decoders.py:29-36; BPOSD_Decoder.decode returns
+ * `osdw_decoding`, :39-41).  Host-side stage (GF(2) elimination per
+ * non-converged syndrome, std::thread pool); all pointers are HOST pointers.
+ *   osd_method : 0 = "osd_0", 1 = "osd_e" (exhaustive over 2^osd_order
+ *                inputs; the reference's choice), 2 = "osd_cs";
+ *   decode     : synd uint8 [B][m], post double [B][n] (BP posteriors), conv
+ *                uint8 [B] or NULL (converged shots copy bp_corr [B][n]),
+ *                out_osd0 (or NULL) / out_osdw uint8 [B][n];
+ *   threads    : <= 0 = all hardware threads.
+ */
+typedef struct qldpc_osd qldpc_osd;
+int qldpc_osd_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
+                     const double *channel_probs, int32_t osd_method, int32_t osd_order, qldpc_osd **out);
+int qldpc_osd_destroy(qldpc_osd *osd);
+int qldpc_osd_rank(const qldpc_osd *osd, int32_t *rank);
+int qldpc_osd_decode_batch(const qldpc_osd *osd, const uint8_t *synd, const double *post, const uint8_t *conv,
+                           const uint8_t *bp_corr, uint8_t *out_osd0, uint8_t *out_osdw, int64_t B,
+                           int32_t threads);
+
+/*
  * Fused Monte Carlo shot loop = CodeSimulator_DataError._single_run
  * (src/Simulators.py:117-168) for many shots in one launch: per shot sample
  * the Pauli error (3-way split of u, :99-113), syndrome H e, BP decode,

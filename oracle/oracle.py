@@ -48,6 +48,10 @@ def lib():
         L.oracle_bp_decode_batch.argtypes = [
             ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
             ctypes.c_int, _u8p, _u8p, _i32p, _u8p, ctypes.c_int64, ctypes.c_int]
+        L.oracle_bp_decode_batch_soft.restype = ctypes.c_int
+        L.oracle_bp_decode_batch_soft.argtypes = [
+            ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, ctypes.c_double,
+            ctypes.c_int, _u8p, _u8p, _i32p, _u8p, _f64p, ctypes.c_int64, ctypes.c_int]
         L.oracle_philox4x32_10.restype = None
         L.oracle_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.oracle_uniform.restype = ctypes.c_double
@@ -84,6 +88,143 @@ def bp_decode_batch(H, channel_probs, max_iter, bp_method="minimum_sum", ms_scal
     if rc:
         raise RuntimeError("oracle_bp_decode_batch failed")
     return corr, iters, conv.astype(bool)
+
+
+def bp_decode_batch_soft(H, channel_probs, max_iter, ms_scaling_factor=0.625, synd=None, precision=64,
+                         nthreads=0):
+    """Min-sum BP that also returns the final ``log_prob_ratios`` [B, n] (OSD's sort key)."""
+    m, n, rp, ci = _csr(H)
+    synd = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.uint8) & 1)
+    B = synd.shape[0]
+    assert synd.shape[1] == m
+    corr = np.zeros((B, n), np.uint8)
+    iters = np.zeros(B, np.int32)
+    conv = np.zeros(B, np.uint8)
+    post = np.zeros((B, n), np.float64)
+    probs = np.ascontiguousarray(np.broadcast_to(np.asarray(channel_probs, np.float64), (n,)))
+    rc = lib().oracle_bp_decode_batch_soft(m, n, rp, ci, probs, int(max_iter), float(ms_scaling_factor),
+                                           int(precision), synd, corr, iters, conv, post, B, int(nthreads))
+    if rc:
+        raise RuntimeError("oracle_bp_decode_batch_soft failed")
+    return corr, iters, conv.astype(bool), post
+
+
+OSD_METHODS = {"osd_0": 0, "osd0": 0, "osd_e": 1, "osde": 1, "exhaustive": 1, "osd_cs": 2, "osdcs": 2,
+               "combination_sweep": 2}
+
+
+def _gf2_rank(H):
+    A = (np.asarray(H) % 2).astype(np.uint8).copy()
+    m, n = A.shape
+    r = 0
+    for c in range(n):
+        piv = np.flatnonzero(A[r:, c])
+        if piv.size == 0:
+            continue
+        p = r + piv[0]
+        A[[r, p]] = A[[p, r]]
+        below = np.flatnonzero(A[:, c])
+        below = below[below != r]
+        A[below] ^= A[r]
+        r += 1
+        if r == m:
+            break
+    return r
+
+
+def osd_decode(H, channel_probs, synd, post, osd_method="osd_e", osd_order=10):
+    """ldpc 0.1 ``bposd_decoder.osd`` restated literally (pure numpy, small codes only).
+
+    Follows the structure of the reference's OSD dependency (src/Decoders.py:29-36
+    builds ``bposd_decoder``; ``decode`` returns ``osdw_decoding``, :39-41):
+    stable ascending sort of the columns by ``post`` (log_prob_ratios), Neal's
+    ``mod2sparse_decomp`` with the "first" strategy on that order (pivot column
+    swapped into position i, pivot row = first remaining row of the partially
+    eliminated column), OSD-0 by forward/back substitution on the LU factors,
+    then the candidates of ``osd_method`` (osd_e: all 2^w inputs on the first
+    w = min(order, n-rank) non-pivot columns in natural binary order; osd_cs:
+    weight-1 on every non-pivot column, then weight-2 inside the first w), each
+    solved the same way; the first candidate of strictly smaller
+    sum_{j: x_j=1} log(1/p_j) wins.  Returns (osd0, osdw) uint8 [n].
+    Parity unpinned: ldpc/bposd are absent, so this is the published algorithm,
+    not a replay of the package.
+    """
+    H = (np.asarray(H) % 2).astype(np.uint8)
+    m, n = H.shape
+    p = np.broadcast_to(np.asarray(channel_probs, np.float64), (n,))
+    wts = np.log(1.0 / p)
+    s = (np.asarray(synd).astype(np.int64) % 2).astype(np.uint8)
+    rank = _gf2_rank(H)
+    cols = list(np.argsort(np.asarray(post, np.float64), kind="stable"))
+    rows = list(range(m))
+    rinv = list(range(m))
+    Bm = H.copy()
+    ops = []  # (pivot row, rows it was added to)
+    for i in range(rank):
+        found = None
+        for k in range(i, n):
+            for r in range(m):
+                if Bm[r, cols[k]] and rinv[r] >= i:
+                    found = (k, r)
+                    break
+            if found:
+                break
+        k, r = found
+        cols[k], cols[i] = cols[i], cols[k]
+        kr = rinv[r]
+        rows[kr], rows[i] = rows[i], rows[kr]
+        rinv[rows[kr]] = kr
+        rinv[rows[i]] = i
+        c = cols[i]
+        tgt = [r2 for r2 in range(m) if Bm[r2, c] and rinv[r2] > i]
+        for r2 in tgt:
+            Bm[r2] ^= Bm[r]
+        ops.append((r, tgt))
+    piv, ht = cols[:rank], cols[rank:]
+
+    def solve(g):
+        g = g.copy()
+        for r, tgt in ops:
+            if g[r]:
+                for r2 in tgt:
+                    g[r2] ^= 1
+        x = np.zeros(n, np.uint8)
+        for i in range(rank - 1, -1, -1):
+            acc = g[rows[i]]
+            for j in range(i + 1, rank):
+                acc ^= Bm[rows[i], piv[j]] & x[piv[j]]
+            x[piv[i]] = acc
+        return x
+
+    def weight(x):
+        t = 0.0
+        for j in range(n):
+            if x[j]:
+                t += wts[j]
+        return t
+
+    osd0 = solve(s)
+    meth = OSD_METHODS[osd_method] if isinstance(osd_method, str) else int(osd_method)
+    k = n - rank
+    if meth == 0 or osd_order == 0 or k == 0:
+        return osd0, osd0.copy()
+    w = min(int(osd_order), k)
+    if meth == 1:
+        inputs = [[j for j in range(w) if (l >> j) & 1] for l in range(1 << w)]
+    else:
+        inputs = [[j] for j in range(k)] + [[i, j] for i in range(w) for j in range(w) if j > i]
+    best, best_w = osd0.copy(), weight(osd0)
+    for t in inputs:
+        g = s.copy()
+        for j in t:
+            g ^= H[:, ht[j]]
+        x = solve(g)
+        for j in t:
+            x[ht[j]] = 1
+        wx = weight(x)
+        if wx < best_w:
+            best, best_w = x, wx
+    return osd0, best
 
 
 def philox4x32_10(ctr, key):

@@ -83,7 +83,7 @@ typedef struct {
 
 #define DEFINE_BP(T, SUFFIX, SENTINEL)                                                          \
 typedef struct {                                                                                \
-    T *b2c, *c2b; int *sgn; T *prior; T *ratio; uint8_t *dec, *dsyn;                          \
+    T *b2c, *c2b; int *sgn; T *prior; T *ratio; T *lpr; uint8_t *dec, *dsyn;                  \
 } ws_##SUFFIX;                                                                                  \
                                                                                                 \
 static int ws_alloc_##SUFFIX(ws_##SUFFIX *w, const graph_t *g) {                                \
@@ -92,11 +92,12 @@ static int ws_alloc_##SUFFIX(ws_##SUFFIX *w, const graph_t *g) {                
     w->sgn = (int *)malloc(sizeof(int) * E);                                                    \
     w->prior = (T *)malloc(sizeof(T) * (size_t)(g->n + 1));                                     \
     w->ratio = (T *)malloc(sizeof(T) * (size_t)(g->n + 1));                                     \
+    w->lpr = (T *)malloc(sizeof(T) * (size_t)(g->n + 1));                                       \
     w->dec = (uint8_t *)malloc((size_t)g->n + 1); w->dsyn = (uint8_t *)malloc((size_t)g->m + 1);\
-    return (w->b2c && w->c2b && w->sgn && w->prior && w->ratio && w->dec && w->dsyn) ? 0 : -1;\
+    return (w->b2c && w->c2b && w->sgn && w->prior && w->ratio && w->lpr && w->dec && w->dsyn) ? 0 : -1;\
 }                                                                                               \
 static void ws_free_##SUFFIX(ws_##SUFFIX *w) {                                                  \
-    free(w->b2c); free(w->c2b); free(w->sgn); free(w->prior); free(w->ratio);                  \
+    free(w->b2c); free(w->c2b); free(w->sgn); free(w->prior); free(w->ratio); free(w->lpr);    \
     free(w->dec); free(w->dsyn);                                                                \
 }                                                                                               \
 /* channel priors, computed in double with libm like the Cython code */                         \
@@ -152,6 +153,7 @@ static int bp_ms_##SUFFIX(const graph_t *g, const bp_params_t *P, ws_##SUFFIX *w
                 int e = g->col_edge[k];                                                         \
                 w->b2c[e] = temp; temp += w->c2b[e];                                            \
             }                                                                                   \
+            w->lpr[j] = temp; /* log_prob_ratios[j], the OSD sort key */                        \
             w->dec[j] = (temp <= 0) ? 1 : 0;                                                    \
             temp = (T)0;                                                                        \
             for (int k = k1 - 1; k >= k0; k--) {                                                \
@@ -222,10 +224,33 @@ static int norm_max_iter(int max_iter, int n) { return max_iter > 0 ? max_iter :
  * src/Decoders.py:88-90).  synd: [B][m] 0/1 bytes; corr: [B][n] 0/1 bytes.
  * precision: 64 or 32.  Returns 0 on success.
  */
+static int bp_decode_batch_impl(int m, int n, const int32_t *row_ptr, const int32_t *col_idx,
+                                const double *channel_probs, int max_iter, int method, double alpha,
+                                int precision, const uint8_t *synd, uint8_t *corr, int32_t *iters,
+                                uint8_t *conv, double *post, int64_t B, int nthreads);
+
 ORACLE_API int oracle_bp_decode_batch(int m, int n, const int32_t *row_ptr, const int32_t *col_idx,
                                       const double *channel_probs, int max_iter, int method, double alpha,
                                       int precision, const uint8_t *synd, uint8_t *corr, int32_t *iters,
                                       uint8_t *conv, int64_t B, int nthreads) {
+    return bp_decode_batch_impl(m, n, row_ptr, col_idx, channel_probs, max_iter, method, alpha, precision,
+                                synd, corr, iters, conv, NULL, B, nthreads);
+}
+
+/* The same plus post [B][n]: the final log_prob_ratios (min-sum only), the
+ * input of ldpc's OSD (bposd_decoder.osd). */
+ORACLE_API int oracle_bp_decode_batch_soft(int m, int n, const int32_t *row_ptr, const int32_t *col_idx,
+                                           const double *channel_probs, int max_iter, double alpha,
+                                           int precision, const uint8_t *synd, uint8_t *corr, int32_t *iters,
+                                           uint8_t *conv, double *post, int64_t B, int nthreads) {
+    return bp_decode_batch_impl(m, n, row_ptr, col_idx, channel_probs, max_iter, 1, alpha, precision,
+                                synd, corr, iters, conv, post, B, nthreads);
+}
+
+static int bp_decode_batch_impl(int m, int n, const int32_t *row_ptr, const int32_t *col_idx,
+                                const double *channel_probs, int max_iter, int method, double alpha,
+                                int precision, const uint8_t *synd, uint8_t *corr, int32_t *iters,
+                                uint8_t *conv, double *post, int64_t B, int nthreads) {
     graph_t g;
     if (graph_init(&g, m, n, row_ptr, col_idx)) return -1;
     bp_params_t P = {norm_max_iter(max_iter, n), method, alpha};
@@ -245,6 +270,7 @@ ORACLE_API int oracle_bp_decode_batch(int m, int n, const int32_t *row_ptr, cons
                 for (int64_t b = tid; b < B; b += nth) {
                     int it; int c = bp_run_f32(&g, &P, &w, synd + b * m, &it);
                     memcpy(corr + b * n, w.dec, (size_t)n);
+                    if (post) for (int j = 0; j < n; j++) post[b * n + j] = (double)w.lpr[j];
                     if (iters) iters[b] = it;
                     if (conv) conv[b] = (uint8_t)c;
                 }
@@ -256,6 +282,7 @@ ORACLE_API int oracle_bp_decode_batch(int m, int n, const int32_t *row_ptr, cons
                 for (int64_t b = tid; b < B; b += nth) {
                     int it; int c = bp_run_f64(&g, &P, &w, synd + b * m, &it);
                     memcpy(corr + b * n, w.dec, (size_t)n);
+                    if (post) for (int j = 0; j < n; j++) post[b * n + j] = (double)w.lpr[j];
                     if (iters) iters[b] = it;
                     if (conv) conv[b] = (uint8_t)c;
                 }

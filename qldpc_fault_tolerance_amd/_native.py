@@ -20,7 +20,9 @@ EXPORTED = [
     "qldpc_graph_info", "qldpc_bp_create", "qldpc_bp_destroy", "qldpc_bp_set_channel_probs",
     "qldpc_bp_decode_batch", "qldpc_mc_create", "qldpc_mc_destroy", "qldpc_mc_launch", "qldpc_mc_run",
     "qldpc_bp_geometry", "qldpc_bp_engine", "qldpc_phenl_create", "qldpc_phenl_destroy",
-    "qldpc_phenl_trace_len", "qldpc_phenl_launch", "qldpc_bp_degree3_slots",
+    "qldpc_phenl_trace_len", "qldpc_phenl_launch", "qldpc_bp_degree3_slots", "qldpc_bp_create_soft",
+    "qldpc_bp_decode_batch_soft", "qldpc_osd_create", "qldpc_osd_destroy", "qldpc_osd_rank",
+    "qldpc_osd_decode_batch",
 ]
 
 
@@ -79,6 +81,18 @@ def _declare(L):
     L.qldpc_bp_set_channel_probs.argtypes = [_vp, _vp]
     L.qldpc_bp_decode_batch.restype = ctypes.c_int
     L.qldpc_bp_decode_batch.argtypes = [_vp, _vp, _vp, _vp, _vp, _i64, _vp]
+    L.qldpc_bp_create_soft.restype = ctypes.c_int
+    L.qldpc_bp_create_soft.argtypes = [_vp, _vp, _i32, _dbl, _i32, _pp]
+    L.qldpc_bp_decode_batch_soft.restype = ctypes.c_int
+    L.qldpc_bp_decode_batch_soft.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]
+    L.qldpc_osd_create.restype = ctypes.c_int
+    L.qldpc_osd_create.argtypes = [_i32, _i32, _vp, _vp, _vp, _i32, _i32, _pp]
+    L.qldpc_osd_destroy.restype = ctypes.c_int
+    L.qldpc_osd_destroy.argtypes = [_vp]
+    L.qldpc_osd_rank.restype = ctypes.c_int
+    L.qldpc_osd_rank.argtypes = [_vp, ctypes.POINTER(_i32)]
+    L.qldpc_osd_decode_batch.restype = ctypes.c_int
+    L.qldpc_osd_decode_batch.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32]
     L.qldpc_mc_create.restype = ctypes.c_int
     L.qldpc_mc_create.argtypes = [_vp, _vp, _vp, _vp, _pp]
     L.qldpc_mc_destroy.restype = ctypes.c_int

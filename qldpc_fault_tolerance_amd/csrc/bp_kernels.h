@@ -104,6 +104,7 @@ struct DecArgs {
   uint8_t* corr;
   int* iters;
   uint8_t* conv;
+  double* post;  // [B][n] final posterior log-probability ratios (BP+OSD input) or null
   long long B;
 };
 
@@ -180,7 +181,7 @@ __device__ inline void insert_priors(VarRegs<T, VPL, DMAX>& R, Pair<T>* P0, uint
 // v2c / posterior / decision, and insert into the next check state `Pn`/`Fn`.
 template <typename T, int VPL, int DMAX>
 __device__ inline uint32_t variable_phase(VarRegs<T, VPL, DMAX>& R, const Pair<T>* Pc, Pair<T>* Pn,
-                                          uint32_t* Fn, T alpha, int tid, int TB, int n) {
+                                          uint32_t* Fn, T alpha, int tid, int TB, int n, T (&lam)[VPL]) {
   using U = typename FT<T>::U;
   uint32_t xbits = 0;
   unsigned long long nsgn = 0;
@@ -208,6 +209,7 @@ __device__ inline uint32_t variable_phase(VarRegs<T, VPL, DMAX>& R, const Pair<T
       f[t] = acc;
       if (R.chk(k, t) != kNoEdge) acc = acc + c[t];
     }
+    lam[k] = acc;
     const uint32_t x = (acc <= (T)0) ? 1u : 0u;
     if (k * TB + tid < n) xbits |= x << k;
     // backward sums and insertion into the next check state
@@ -232,10 +234,12 @@ __device__ inline uint32_t variable_phase(VarRegs<T, VPL, DMAX>& R, const Pair<T
 
 // Full BP decode of one sector for the block.  Entry: F0 set as for
 // insert_priors, P0/P1 = SENT, F1 arbitrary.  Returns decision bits of the
-// thread's variables; iters/conv set for all threads.
+// thread's variables (and their last-iteration posteriors in `lam`);
+// iters/conv set for all threads.
 template <typename T, int VPL, int DMAX>
 __device__ inline uint32_t bp_decode_block(VarRegs<T, VPL, DMAX>& R, const SectorDev& S, Pair<T>* P, uint32_t* F,
-                                           int mmax, uint32_t ebits, int tid, int TB, int& iters, bool& conv) {
+                                           int mmax, uint32_t ebits, int tid, int TB, int& iters, bool& conv,
+                                           T (&lam)[VPL]) {
   using U = typename FT<T>::U;
   const int m = S.m, n = S.n;
   Pair<T>* P0 = P;
@@ -268,7 +272,7 @@ __device__ inline uint32_t bp_decode_block(VarRegs<T, VPL, DMAX>& R, const Secto
     Pair<T>* Pn = cur ? P0 : P1;
     uint32_t* Fc = cur ? F1 : F0;
     uint32_t* Fn = cur ? F0 : F1;
-    xbits = variable_phase<T, VPL, DMAX>(R, Pc, Pn, Fn, alpha, tid, TB, n);
+    xbits = variable_phase<T, VPL, DMAX>(R, Pc, Pn, Fn, alpha, tid, TB, n, lam);
     __syncthreads();
     int mism = 0;
     int q = 0;
@@ -319,11 +323,15 @@ __global__ __launch_bounds__(kMaxThreads) void bp_decode_kernel(DecArgs A) {
     __syncthreads();
     int iters;
     bool conv;
-    const uint32_t x = bp_decode_block<T, VPL, DMAX>(R, A.sec, P, F, m, 0u, tid, TB, iters, conv);
+    T lam[VPL];
+    const uint32_t x = bp_decode_block<T, VPL, DMAX>(R, A.sec, P, F, m, 0u, tid, TB, iters, conv, lam);
 #pragma unroll
     for (int k = 0; k < VPL; ++k) {
       const int j = k * TB + tid;
-      if (j < n) A.corr[b * (long long)n + j] = (uint8_t)((x >> k) & 1u);
+      if (j < n) {
+        A.corr[b * (long long)n + j] = (uint8_t)((x >> k) & 1u);
+        if (A.post) A.post[b * (long long)n + j] = (double)lam[k];
+      }
     }
     if (tid == 0) {
       if (A.iters) A.iters[b] = iters;
@@ -378,7 +386,8 @@ __global__ __launch_bounds__(kMaxThreads) void mc_kernel(McArgs A) {
       __syncthreads();
       int iters;
       bool conv;
-      const uint32_t x = bp_decode_block<T, VPL, DMAX>(R, S, P, F, mmax, ebits, tid, TB, iters, conv);
+      T lam[VPL];
+      const uint32_t x = bp_decode_block<T, VPL, DMAX>(R, S, P, F, mmax, ebits, tid, TB, iters, conv, lam);
       // --- residual r = e ^ x and its logical syndrome L r (src/Simulators.py:135-160)
       const uint32_t r = ebits ^ x;
       if (r) {

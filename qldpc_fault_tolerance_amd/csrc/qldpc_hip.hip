@@ -417,9 +417,26 @@ static int create_ps(qldpc_graph* g, const double* channel_probs, int32_t max_it
   return 0;
 }
 
+static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t max_iter, int32_t bp_method,
+                          double ms_scaling_factor, int32_t precision, int32_t vars_per_thread,
+                          int32_t min_col_slots, int forced_engine, qldpc_bp** out);
+
 int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_iter, int32_t bp_method,
                     double ms_scaling_factor, int32_t precision, int32_t vars_per_thread, int32_t min_col_slots,
                     qldpc_bp** out) {
+  return create_min_sum(g, channel_probs, max_iter, bp_method, ms_scaling_factor, precision, vars_per_thread,
+                        min_col_slots, 0, out);
+}
+
+// Engine 1 is the one whose decode kernel can hand back the final posteriors.
+int qldpc_bp_create_soft(qldpc_graph* g, const double* channel_probs, int32_t max_iter, double ms_scaling_factor,
+                         int32_t precision, qldpc_bp** out) {
+  return create_min_sum(g, channel_probs, max_iter, QLDPC_MIN_SUM, ms_scaling_factor, precision, 0, 0, 1, out);
+}
+
+static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t max_iter, int32_t bp_method,
+                          double ms_scaling_factor, int32_t precision, int32_t vars_per_thread,
+                          int32_t min_col_slots, int forced_engine, qldpc_bp** out) {
   if (!g || !channel_probs || !out) return set_err(QLDPC_EINVAL, "NULL argument");
   if (precision != 32 && precision != 64) return set_err(QLDPC_EINVAL, "precision must be 32 or 64");
   if (bp_method != QLDPC_MIN_SUM && bp_method != QLDPC_PRODUCT_SUM)
@@ -429,7 +446,7 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
   if (g->max_col > 8 || min_col_slots > 8) return set_err(QLDPC_ENOTSUP, "column degree > 8");
   auto* bp = new qldpc_bp();
   bp->g = g;
-  const int want_engine = env_int("QLDPC_ENGINE", 3);
+  const int want_engine = forced_engine ? forced_engine : env_int("QLDPC_ENGINE", 3);
   bp->engine = (want_engine >= 1 && want_engine <= 4) ? want_engine : 3;
   bp->max_iter = max_iter > 0 ? max_iter : g->n;
   bp->method = bp_method;
@@ -644,8 +661,23 @@ static int chunk_for(long long count, long long grid, int ns) {
   return (int)c;
 }
 
+static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, int32_t* d_iters, uint8_t* d_conv,
+                        double* d_post, int64_t B, void* stream);
+
 int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, int32_t* d_iters, uint8_t* d_conv,
                           int64_t B, void* stream) {
+  return decode_batch(bp, d_synd, d_corr, d_iters, d_conv, nullptr, B, stream);
+}
+
+int qldpc_bp_decode_batch_soft(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, int32_t* d_iters,
+                               uint8_t* d_conv, double* d_post, int64_t B, void* stream) {
+  if (!bp || (B > 0 && !d_post)) return set_err(QLDPC_EINVAL, "NULL argument");
+  if (bp->engine != 1) return set_err(QLDPC_ENOTSUP, "soft output needs a decoder from qldpc_bp_create_soft");
+  return decode_batch(bp, d_synd, d_corr, d_iters, d_conv, d_post, B, stream);
+}
+
+static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, int32_t* d_iters, uint8_t* d_conv,
+                        double* d_post, int64_t B, void* stream) {
   if (!bp || (B > 0 && (!d_synd || !d_corr))) return set_err(QLDPC_EINVAL, "NULL argument");
   if (B == 0) return 0;
   QLDPC_HIP(hipSetDevice(bp->g->device));
@@ -658,6 +690,7 @@ int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, 
     a.corr = d_corr;
     a.iters = d_iters;
     a.conv = d_conv;
+    a.post = d_post;
     a.B = B;
     const int grid = (int)std::max<long long>(1, std::min<long long>(B, cap));
     Variant v = get_variant(bp->precision, bp->VPL, bp->DMAX);

@@ -8,9 +8,8 @@ BP engine (:class:`engine.DeviceBP`): same constructor arguments, same
 syndromes per launch.  ``DecoderClass.GetDecoder(params)`` keeps the reference's
 dict keys and assertions (``:94-172``; ``src/Decoders_SpaceTime.py:227-257``).
 
-BP+OSD (``BPOSD_Decoder``) is outside this engine's scope:
-the class exists so code written against the reference imports cleanly, and
-raises ``NotImplementedError`` when constructed.
+BP+OSD (``BPOSD_Decoder``): GPU BP with soft output, then
+the native OSD stage (csrc/osd.hip) on the syndromes BP did not converge on.
 """
 from __future__ import annotations
 
@@ -96,11 +95,48 @@ class FirstMinBPDecoder:
 
 
 class BPOSD_Decoder:
-    """Placeholder for ``src/Decoders.py:26-41`` (OSD post-processing is out of scope)."""
+    """``BPOSD_Decoder(h, channel_probs, max_iter, bp_method, ms_scaling_factor, osd_method, osd_order)``
+    (``src/Decoders.py:26-41``): ``bposd_decoder`` = BP, then OSD when BP does not converge.
 
-    def __init__(self, *a, **k):
-        raise NotImplementedError("BP+OSD is not part of the MI355X engine's hot path (SURVEY.md §8f rank 2); "
-                                  "use BPDecoder / BP_Decoder_Class")
+    BP runs on the GPU (engine 1 with soft output: ``qldpc_bp_decode_batch_soft``)
+    and hands its final posteriors to the native OSD stage (``qldpc_osd_decode_batch``).
+    ``decode`` returns ``osdw_decoding`` like the reference; ``osd0_decoding``,
+    ``bp_decoding``, ``converge``, ``iter`` and ``log_prob_ratios`` are kept.
+    """
+
+    def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, osd_method, osd_order,
+                 precision: int = 64, device: int = 0, osd_threads: int = 0):
+        from .engine import DeviceBP, HostOSD
+
+        self.h = h
+        H = h if isinstance(h, CSR) else CSR.from_dense(h)
+        self.num_checks, self.num_qubits = H.m, H.n
+        self.channel_probs = np.asarray(channel_probs, dtype=np.float64)
+        self.osd_method, self.osd_order = osd_method, osd_order
+        self.decoder = DeviceBP(H, self.channel_probs, max_iter=_int_max_iter(max_iter, H.n), bp_method=bp_method,
+                                ms_scaling_factor=ms_scaling_factor, precision=precision, device=device, soft=True)
+        self.osd = HostOSD(H, self.channel_probs, osd_method=osd_method, osd_order=osd_order)
+        self.osd_threads = osd_threads
+        self.iter, self.converge = 0, 0
+
+    def decode_batch(self, synd):
+        """[B, m] syndromes -> osdw corrections [B, n] (int); also sets the batch's
+        ``osd0_batch``, ``bp_batch``, ``conv_batch``, ``iters_batch``, ``post_batch``."""
+        s = np.atleast_2d(np.asarray(synd))
+        corr, iters, conv, post = self.decoder.decode_batch_soft(s)
+        o0, ow = self.osd.decode_batch(s, post, conv, corr, threads=self.osd_threads)
+        self.bp_batch, self.iters_batch, self.conv_batch, self.post_batch = corr, iters, conv, post
+        self.osd0_batch = o0.astype(np.int64)
+        return ow.astype(np.int64)
+
+    def decode(self, synd):
+        ow = self.decode_batch(np.asarray(synd).reshape(1, -1))
+        self.bp_decoding = self.bp_batch[0]
+        self.osd0_decoding = self.osd0_batch[0]
+        self.osdw_decoding = ow[0]
+        self.log_prob_ratios = self.post_batch[0]
+        self.iter, self.converge = int(self.iters_batch[0]), int(self.conv_batch[0])
+        return self.osdw_decoding
 
 
 class DecoderClass(ABC):
@@ -145,16 +181,26 @@ class BP_Decoder_Class(DecoderClass):
 
 
 class BPOSD_Decoder_Class(DecoderClass):
-    """``src/Decoders.py:100-138`` (OSD out of scope; constructing a decoder raises)."""
+    """``src/Decoders.py:100-138``: BP+OSD factory keyed like :class:`BP_Decoder_Class`."""
 
     def __init__(self, max_iter_ratio: int, bp_method: str, ms_scaling_factor: float, osd_method: str,
-                 osd_order: int):
+                 osd_order: int, precision: int = 64, device: int = 0):
         self.decoder_default_params = {"max_iter_ratio": max_iter_ratio, "bp_method": bp_method,
                                        "ms_scaling_factor": ms_scaling_factor, "osd_method": osd_method,
                                        "osd_order": osd_order}
+        self.precision = precision
+        self.device = device
 
     def GetDecoder(self, code_and_noise_channel_params):
-        raise NotImplementedError("BP+OSD is not part of the MI355X engine's hot path (SURVEY.md §8f rank 2)")
+        p = code_and_noise_channel_params
+        assert "h" in p.keys(), "missing the check matrix h"
+        assert "p_data" in p.keys(), "missing the data error prob: p_data"
+        num_qubits, probs = BP_Decoder_Class._probs(p)
+        d = self.decoder_default_params
+        max_iter = num_qubits / d["max_iter_ratio"]
+        return BPOSD_Decoder(h=p["h"], channel_probs=probs, max_iter=max_iter, bp_method=d["bp_method"],
+                             ms_scaling_factor=d["ms_scaling_factor"], osd_method=d["osd_method"],
+                             osd_order=d["osd_order"], precision=self.precision, device=self.device)
 
 
 # ------------------------------------------------------------------ space-time

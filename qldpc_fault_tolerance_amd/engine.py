@@ -73,7 +73,7 @@ class DeviceBP:
 
     def __init__(self, H, channel_probs, max_iter: int = 0, bp_method="minimum_sum", ms_scaling_factor=0.625,
                  precision: int = 64, vars_per_thread: int = 0, device: int = 0, graph: DeviceGraph | None = None,
-                 min_col_slots: int = 0):
+                 min_col_slots: int = 0, soft: bool = False):
         self.graph = graph if graph is not None else DeviceGraph(H, device=device)
         n = self.graph.n
         probs = np.asarray(channel_probs, dtype=np.float64)
@@ -86,11 +86,20 @@ class DeviceBP:
         self.bp_method = bp_method_code(bp_method)
         self.ms_scaling_factor = float(ms_scaling_factor)
         self.precision = int(precision)
+        self.soft = bool(soft)
         h = ctypes.c_void_p()
-        _native.check(_native.lib().qldpc_bp_create(
-            self.graph.handle, self.channel_probs.ctypes.data_as(ctypes.c_void_p), self.max_iter, self.bp_method,
-            self.ms_scaling_factor, self.precision, int(vars_per_thread), int(min_col_slots), ctypes.byref(h)),
-            "qldpc_bp_create")
+        if self.soft:
+            # BP+OSD: engine 1 hands back the final posteriors (qldpc_bp_create_soft)
+            if self.bp_method != 1:
+                raise NotImplementedError("soft-output BP (BP+OSD) is implemented for minimum_sum")
+            _native.check(_native.lib().qldpc_bp_create_soft(
+                self.graph.handle, self.channel_probs.ctypes.data_as(ctypes.c_void_p), self.max_iter,
+                self.ms_scaling_factor, self.precision, ctypes.byref(h)), "qldpc_bp_create_soft")
+        else:
+            _native.check(_native.lib().qldpc_bp_create(
+                self.graph.handle, self.channel_probs.ctypes.data_as(ctypes.c_void_p), self.max_iter,
+                self.bp_method, self.ms_scaling_factor, self.precision, int(vars_per_thread), int(min_col_slots),
+                ctypes.byref(h)), "qldpc_bp_create")
         self.handle = h
 
     @property
@@ -140,10 +149,92 @@ class DeviceBP:
         torch.cuda.synchronize(dev)
         return corr.cpu().numpy().astype(np.int64), iters.cpu().numpy(), conv.cpu().numpy().astype(bool)
 
+    def decode_batch_soft(self, synd):
+        """Like :meth:`decode_batch` plus the final posteriors ``post`` [B, n] float64
+        (ldpc's ``log_prob_ratios``); needs ``soft=True``."""
+        torch = _torch()
+        s = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.int64) % 2, dtype=np.uint8)
+        if s.shape[1] != self.m:
+            raise ValueError(f"syndrome length {s.shape[1]} != number of checks {self.m}")
+        B = s.shape[0]
+        dev = torch.device("cuda", self.graph.device)
+        sd = torch.from_numpy(s).to(dev)
+        corr = torch.empty((B, self.n), dtype=torch.uint8, device=dev)
+        iters = torch.empty(B, dtype=torch.int32, device=dev)
+        conv = torch.empty(B, dtype=torch.uint8, device=dev)
+        post = torch.empty((B, self.n), dtype=torch.float64, device=dev)
+        _native.check(_native.lib().qldpc_bp_decode_batch_soft(
+            self.handle, ctypes.c_void_p(sd.data_ptr()), ctypes.c_void_p(corr.data_ptr()),
+            ctypes.c_void_p(iters.data_ptr()), ctypes.c_void_p(conv.data_ptr()), ctypes.c_void_p(post.data_ptr()),
+            B, _stream_handle(torch, dev)), "qldpc_bp_decode_batch_soft")
+        torch.cuda.synchronize(dev)
+        return (corr.cpu().numpy().astype(np.int64), iters.cpu().numpy(), conv.cpu().numpy().astype(bool),
+                post.cpu().numpy())
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h and _native._lib is not None:
             _native.lib().qldpc_bp_destroy(h)
+            self.handle = None
+
+
+OSD_METHODS = {"osd_0": 0, "osd0": 0, "osd_e": 1, "osde": 1, "exhaustive": 1, "osd_cs": 2, "osdcs": 2,
+               "combination_sweep": 2}
+
+
+class HostOSD:
+    """Ordered-statistics post-processing stage (``qldpc_osd_*``, csrc/osd.hip).
+
+    Native host code (GF(2) elimination on bit-packed columns, a std::thread
+    pool over syndromes); it consumes the GPU BP's posteriors.  Needs only the
+    library, not a GPU.
+    """
+
+    def __init__(self, H, channel_probs, osd_method="osd_e", osd_order=10):
+        c = H if isinstance(H, CSR) else CSR.from_dense(H)
+        self.m, self.n = c.m, c.n
+        key = str(osd_method).lower() if not isinstance(osd_method, (int, np.integer)) else None
+        if key is not None and key not in OSD_METHODS:
+            raise ValueError(f"unknown osd_method {osd_method!r}")
+        self.osd_method = OSD_METHODS[key] if key is not None else int(osd_method)
+        self.osd_order = int(osd_order)
+        probs = np.asarray(channel_probs, dtype=np.float64)
+        if probs.ndim == 0:
+            probs = np.full(self.n, float(probs))
+        self._probs = np.ascontiguousarray(probs)
+        rp = np.ascontiguousarray(c.row_ptr, dtype=np.int32)
+        ci = np.ascontiguousarray(c.col_idx, dtype=np.int32)
+        h = ctypes.c_void_p()
+        _native.check(_native.lib().qldpc_osd_create(
+            self.m, self.n, rp.ctypes.data_as(ctypes.c_void_p), ci.ctypes.data_as(ctypes.c_void_p),
+            self._probs.ctypes.data_as(ctypes.c_void_p), self.osd_method, self.osd_order, ctypes.byref(h)),
+            "qldpc_osd_create")
+        self.handle = h
+        r = ctypes.c_int32()
+        _native.check(_native.lib().qldpc_osd_rank(h, ctypes.byref(r)), "qldpc_osd_rank")
+        self.rank = r.value
+
+    def decode_batch(self, synd, post, conv=None, bp_corr=None, threads: int = 0):
+        """(osd0 [B, n], osdw [B, n]) uint8; converged rows (``conv``) copy ``bp_corr``."""
+        s = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.int64) % 2, dtype=np.uint8)
+        B = s.shape[0]
+        pst = np.ascontiguousarray(np.asarray(post, dtype=np.float64).reshape(B, self.n))
+        if s.shape[1] != self.m:
+            raise ValueError(f"syndrome length {s.shape[1]} != number of checks {self.m}")
+        cv = None if conv is None else np.ascontiguousarray(np.asarray(conv).reshape(B), dtype=np.uint8)
+        bc = None if bp_corr is None else np.ascontiguousarray(np.asarray(bp_corr).reshape(B, self.n),
+                                                                 dtype=np.uint8)
+        o0 = np.zeros((B, self.n), np.uint8)
+        ow = np.zeros((B, self.n), np.uint8)
+        vp = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        _native.check(_native.lib().qldpc_osd_decode_batch(self.handle, vp(s), vp(pst), vp(cv), vp(bc), vp(o0),
+                                                           vp(ow), B, int(threads)), "qldpc_osd_decode_batch")
+        return o0, ow
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _native._lib is not None:
+            _native.lib().qldpc_osd_destroy(h)
             self.handle = None
 
 

@@ -80,6 +80,8 @@ def _engine_bp(decoder):
     """The engine's DeviceBP behind a drop-in decoder, or None for a foreign decoder."""
     from .engine import DeviceBP
 
+    if getattr(decoder, "osd", None) is not None:  # BPOSD_Decoder: OSD runs after BP, per-shot path
+        return None
     bp = getattr(decoder, "decoder", None)
     return bp if isinstance(bp, DeviceBP) else None
 
