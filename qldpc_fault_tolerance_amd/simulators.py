@@ -86,6 +86,20 @@ def _engine_bp(decoder):
     return bp if isinstance(bp, DeviceBP) else None
 
 
+def _is_bposd(decoder) -> bool:
+    return getattr(decoder, "osd", None) is not None
+
+
+def gf2_rows(csr, X):
+    """Rows of ``X`` [S, n] (0/1) times ``H^T`` mod 2 -> [S, m] uint8, for a :class:`~.codes.CSR` ``H``."""
+    import scipy.sparse as sp
+
+    A = sp.csr_matrix((np.ones(len(csr.col_idx), np.int32), np.asarray(csr.col_idx), np.asarray(csr.row_ptr)),
+                      shape=(csr.m, csr.n))
+    X = np.asarray(X, dtype=np.int32)
+    return (np.asarray(A @ X.T).T % 2).astype(np.uint8)
+
+
 class CodeSimulator_DataError:
     """Data-error simulator (``src/Simulators.py:75-188``).
 
@@ -174,10 +188,87 @@ class CodeSimulator_DataError:
         self.last_result = res
         return res
 
+    # -- BP+OSD shot loop ---------------------------------------------------------
+    def _bposd_ready(self):
+        need_x = self.eval_logical_type != "Z"
+        need_z = self.eval_logical_type != "X"
+        return (not need_x or _is_bposd(self.decoder_x)) and (not need_z or _is_bposd(self.decoder_z))
+
+    def bposd_counts(self, num_run: int, batch: int = 16384, keep_shots: bool = False):
+        """``num_run`` shots with BPOSD_Decoder sectors (the notebooks' decoder,
+        src/Decoders.py:26-41) -> (failures, shots, osd_decodes), all-reduced.
+
+        Per batch, the fused GPU shot loop samples the Philox errors, forms the
+        syndromes and runs BP with the BPOSD decoders' own (soft-capable) BP,
+        handing back per-shot errors and BP corrections.  Shots whose BP
+        correction leaves a syndrome mismatch (BP did not converge) are
+        re-decoded with BP+OSD (GPU soft BP, bit-identical to the first BP, then
+        the native OSD stage) and their failure re-checked; converged shots keep
+        the fused verdict, exactly as ``bposd_decoder`` returns the BP decoding
+        when BP converges.  ``keep_shots`` stores ``last_shots`` =
+        (errors [S, n] bit0 x / bit1 z, sector failures [S, 2]) of the run.
+        """
+        if not self._bposd_ready():
+            raise TypeError("bposd_counts needs BPOSD_Decoder instances for the sectors eval_logical_type uses")
+        from .engine import DeviceMC, _torch
+
+        torch = _torch()
+        if self.seed is None:
+            self.seed = random.getrandbits(64)
+        need_x = self.eval_logical_type != "Z"
+        need_z = self.eval_logical_type != "X"
+        if getattr(self, "_bposd_mc", None) is None:
+            self._bposd_mc = DeviceMC(self.code, self.decoder_x.decoder if need_x else None,
+                                      self.decoder_z.decoder if need_z else None)
+        mc = self._bposd_mc
+        rank, ws = parallel.world()
+        b, c = parallel.shard_range(num_run, rank, ws, begin=self._shot_offset)
+        self._shot_offset += int(num_run)
+        px, py, pz = self.channel_probs
+        code = self.code
+        sectors = [(0, need_x, self.decoder_x, code.csr("hz"), code.csr("lz")),
+                   (1, need_z, self.decoder_z, code.csr("hx"), code.csr("lx"))]
+        fails = osd_n = 0
+        kept_e, kept_f = [], []
+        for s0 in range(b, b + c, int(batch)):
+            S = min(int(batch), b + c - s0)
+            res = mc.run(px, py, pz, self.seed, s0, S, self.eval_logical_type, per_shot=True)
+            sf = np.zeros((S, 2), dtype=bool)
+            for q, need, dec, H, L in sectors:
+                if not need:
+                    continue
+                e = ((res.err >> q) & 1).astype(np.uint8)
+                synd = gf2_rows(H, e)
+                f = ((res.fail >> q) & 1).astype(bool)
+                idx = np.flatnonzero((gf2_rows(H, res.corr[:, q, :]) != synd).any(1))
+                if idx.size:
+                    r = e[idx] ^ dec.decode_batch(synd[idx]).astype(np.uint8)
+                    f[idx] = gf2_rows(H, r).any(1) | gf2_rows(L, r).any(1)
+                    osd_n += int(idx.size)
+                sf[:, q] = f
+            if self.eval_logical_type == "X":
+                fails += int(sf[:, 0].sum())
+            elif self.eval_logical_type == "Z":
+                fails += int(sf[:, 1].sum())
+            else:
+                fails += int((sf[:, 0] | sf[:, 1]).sum())
+            if keep_shots:
+                kept_e.append(res.err)
+                kept_f.append(sf)
+        if keep_shots:
+            self.last_shots = (np.concatenate(kept_e) if kept_e else None, np.concatenate(kept_f) if kept_f else None)
+        cnt = torch.tensor([fails, c, osd_n], dtype=torch.int64,
+                           device=torch.device("cuda", mc.device))
+        parallel.allreduce_counters(cnt)
+        out = cnt.cpu().numpy()
+        return int(out[0]), int(out[1]), int(out[2])
+
     def _batch_failures(self, n: int) -> int:
         ok, _, _ = self._engine_ready()
         if ok:
             return self.fused_counts(n).failures
+        if self._bposd_ready():
+            return self.bposd_counts(n)[0]
         return int(np.sum([self._single_run() for _ in range(n)]))
 
     def WordErrorRate(self, num_run: int):

@@ -91,3 +91,42 @@ def test_bposd_factory_and_simulator(gpu):
                                      bcls.GetDecoder({"h": code.hx, "p_data": p}), [p / 2] * 3, "Total")
     fails_bp = sum(sim_bp._single_run() for _ in range(150))
     assert fails_osd <= fails_bp
+
+
+def test_bposd_shot_loop_matches_oracle_per_shot(gpu, oracle):
+    """CodeSimulator_DataError with BPOSD decoders: fused GPU MC + OSD on the
+    non-converged shots.  Per shot and sector, the failure equals the oracle's
+    BP (+ literal OSD when BP did not converge) on the same Philox errors; the
+    same seed with plain BP decoders fails at least as often."""
+    from qldpc_fault_tolerance_amd.decoders import BP_Decoder_Class, BPOSD_Decoder_Class
+    from qldpc_fault_tolerance_amd.simulators import CodeSimulator_DataError, gf2_rows
+
+    code = codes.get_code("hgp_34_n225")
+    p, order, S = 0.08, 4, 160
+    cls = BPOSD_Decoder_Class(10, "minimum_sum", 0.625, "osd_e", order)
+    dx, dz = cls.GetDecoder({"h": code.hz, "p_data": p}), cls.GetDecoder({"h": code.hx, "p_data": p})
+    sim = CodeSimulator_DataError(code, dx, dz, [p / 2] * 3, "Total", seed=77)
+    fails, shots, osd_n = sim.bposd_counts(S, batch=64, keep_shots=True)
+    assert shots == S and osd_n > 0
+    err, sf = sim.last_shots
+    assert err.shape == (S, code.N) and sf.shape == (S, 2)
+    assert fails == int((sf[:, 0] | sf[:, 1]).sum())
+    mi = int(code.N / 10)
+    for q, H, L in ((0, code.hz, code.lz), (1, code.hx, code.lx)):
+        e = ((err >> q) & 1).astype(np.uint8)
+        synd = gf2_rows(code.csr("hz" if q == 0 else "hx"), e)
+        oc, _, ov, op = oracle.bp_decode_batch_soft(H, p, mi, 0.625, synd, 64)
+        for s in range(S):
+            x = oc[s] if ov[s] else oracle.osd_decode(H, p * np.ones(code.N), synd[s], op[s], "osd_e", order)[1]
+            r = (e[s] ^ x).astype(np.int64)
+            f = bool((H.astype(np.int64) @ r % 2).any() or (L.astype(np.int64) @ r % 2).any())
+            assert f == bool(sf[s, q]), (q, s)
+    bcls = BP_Decoder_Class(10, "minimum_sum", 0.625)
+    sim_bp = CodeSimulator_DataError(code, bcls.GetDecoder({"h": code.hz, "p_data": p}),
+                                     bcls.GetDecoder({"h": code.hx, "p_data": p}), [p / 2] * 3, "Total", seed=77)
+    assert sim_bp.fused_counts(S).failures >= fails
+    # WordErrorRate routes BPOSD decoders through the same loop
+    wer, _ = CodeSimulator_DataError(code, dx, dz, [p / 2] * 3, "Total", seed=77).WordErrorRate(S)
+    from qldpc_fault_tolerance_amd.simulators import word_error_rate
+
+    assert wer == word_error_rate(fails, S, code.K)[0]
