@@ -127,7 +127,7 @@ int qldpc_bp_decode_batch_soft(qldpc_bp *bp, const uint8_t *d_synd, uint8_t *d_c
  *   decode     : synd uint8 [B][m], post double [B][n] (BP posteriors), conv
  *                uint8 [B] or NULL (converged shots copy bp_corr [B][n]),
  *                out_osd0 (or NULL) / out_osdw uint8 [B][n];
- *   threads    : <= 0 = all hardware threads.
+ *   threads    : <= 0 = OMP_NUM_THREADS if set, else all hardware threads.
  */
 typedef struct qldpc_osd qldpc_osd;
 int qldpc_osd_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_t *col_idx,

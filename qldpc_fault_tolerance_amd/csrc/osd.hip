@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <numeric>
 #include <thread>
 #include <vector>
@@ -297,7 +298,12 @@ int qldpc_osd_decode_batch(const qldpc_osd* osd, const uint8_t* synd, const doub
       todo.push_back(b);
     }
   }
-  int T = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  int T = threads;
+  if (T <= 0) {  // the process's CPU share when the launcher states it (OMP_NUM_THREADS), else all cores
+    const char* e = std::getenv("OMP_NUM_THREADS");
+    T = e ? std::atoi(e) : 0;
+    if (T <= 0) T = (int)std::max(1u, std::thread::hardware_concurrency());
+  }
   T = (int)std::min<int64_t>(T, (int64_t)todo.size());
   if (T <= 0) return 0;
   auto run = [&](int t) {
