@@ -139,6 +139,19 @@ int qldpc_osd_decode_batch(const qldpc_osd *osd, const uint8_t *synd, const doub
                            int32_t threads);
 
 /*
+ * GPU OSD (uniform channel_probs, n <= 8192): the same outputs as
+ * qldpc_osd_decode_batch, one workgroup per syndrome; all pointers are DEVICE
+ * pointers (d_post from qldpc_bp_decode_batch_soft).  Non-uniform priors
+ * return QLDPC_ENOTSUP (use the host stage).
+ */
+typedef struct qldpc_osd_gpu qldpc_osd_gpu;
+int qldpc_osd_gpu_create(const qldpc_graph *g, const double *channel_probs, int32_t osd_method, int32_t osd_order,
+                         qldpc_osd_gpu **out);
+int qldpc_osd_gpu_destroy(qldpc_osd_gpu *osd);
+int qldpc_osd_gpu_decode(qldpc_osd_gpu *osd, const uint8_t *d_synd, const double *d_post, const uint8_t *d_conv,
+                         const uint8_t *d_bp_corr, uint8_t *d_out0, uint8_t *d_outw, int64_t B, void *stream);
+
+/*
  * Fused Monte Carlo shot loop = CodeSimulator_DataError._single_run
  * (src/Simulators.py:117-168) for many shots in one launch: per shot sample
  * the Pauli error (3-way split of u, :99-113), syndrome H e, BP decode,

@@ -325,3 +325,366 @@ int qldpc_osd_decode_batch(const qldpc_osd* osd, const uint8_t* synd, const doub
 }
 
 }  // extern "C"
+
+// ===========================================================================
+// GPU OSD (uniform priors): one workgroup per syndrome, persistent over the
+// batch.  Same algorithm and outputs as the host stage above, laid out for the
+// GPU: the columns are bitonic-sorted in LDS by (posterior, index) — a stable
+// ascending order — and H is loaded with its columns permuted into that order,
+// word-major (word q of row i at q*m + i) in a per-workgroup HBM slice, so a
+// pivot search tests one coalesced word per row and a row update xors
+// coalesced words.  Full Gauss-Jordan over the positions in order finds the
+// same greedy pivots (the x of an independent pivot set is unique, whatever
+// pivot rows are chosen); the OSD inputs are then bit-vectors over the pivot
+// index, and every candidate's weight (popcount, the order relation of the
+// uniform soft weight) is reduced to the lexicographic minimum of
+// (weight, candidate index) = the first strictly lightest in ldpc's order.
+namespace {
+
+constexpr int kOsdThreads = 256;
+constexpr int kOsdMaxN = 8192;
+
+struct OsdGpuArgs {
+  const int32_t* rp;
+  const int32_t* ci;
+  const uint8_t* synd;     // [B][m]
+  const double* post;      // [B][n]
+  const uint8_t* conv;     // [B] or null
+  const uint8_t* bp_corr;  // [B][n] or null
+  uint8_t* out0;           // [B][n] or null
+  uint8_t* outw;           // [B][n]
+  u64* ws;                 // per workgroup: M [W][m] | X [(1 + nh)][RW]
+  int32_t* iws;            // per workgroup: pivrow [rank] | pivpos [rank] | swp [n]
+  long long B;
+  int m, n, W, RW, rank, method, order, NP;
+  long long ws_words, iws_ints;
+};
+
+__device__ inline u64 ord_key(double x) {
+  if (x == 0.0) x = 0.0;  // -0 ties +0, as std::stable_sort's `<` has it
+  const u64 u = (u64)__double_as_longlong(x);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, TB = blockDim.x;
+  const int m = A.m, n = A.n, W = A.W, RW = A.RW, NP = A.NP, rank = A.rank;
+  u64* skey = reinterpret_cast<u64*>(smem);                    // [NP]
+  int32_t* sidx = reinterpret_cast<int32_t*>(skey + NP);       // [NP] -> cols (sorted position -> column)
+  int32_t* pos = sidx + NP;                                    // [n]  column -> sorted position
+  uint32_t* used = reinterpret_cast<uint32_t*>(pos + n);       // [ceil(m/32)]
+  uint32_t* sb = used + (m + 31) / 32;                         // [ceil(m/32)] syndrome, reduced
+  __shared__ int s_piv[2], s_npiv;  // s_piv double-buffered by position parity
+  __shared__ u64 s_best;
+  u64* M = A.ws + (size_t)blockIdx.x * A.ws_words;
+  u64* X = M + (size_t)W * m;  // X[0] = S0, X[1 + j] = x(h_j)
+  int32_t* pivrow = A.iws + (size_t)blockIdx.x * A.iws_ints;
+  int32_t* pivpos = pivrow + rank;
+  int32_t* swp = pivpos + rank;
+  const int k = n - rank;
+  const int w = A.order < k ? A.order : k;
+  const int nh = A.method == 2 ? k : w;
+
+  for (long long b = blockIdx.x; b < A.B; b += gridDim.x) {
+    uint8_t* ow = A.outw + b * (long long)n;
+    uint8_t* o0 = A.out0 ? A.out0 + b * (long long)n : nullptr;
+    if (A.conv && A.conv[b]) {  // BP converged: bposd_decoder returns the BP decoding
+      for (int j = tid; j < n; j += TB) {
+        const uint8_t v = A.bp_corr[b * (long long)n + j];
+        ow[j] = v;
+        if (o0) o0[j] = v;
+      }
+      continue;  // uniform over the workgroup
+    }
+    const double* post = A.post + b * (long long)n;
+    const uint8_t* synd = A.synd + b * (long long)m;
+    // 1. stable ascending sort of the columns by posterior (bitonic on (key, index))
+    for (int q = tid; q < NP; q += TB) {
+      skey[q] = q < n ? ord_key(post[q]) : ~0ull;
+      sidx[q] = q < n ? q : 0x7FFFFFFF;
+    }
+    __syncthreads();
+    for (int size = 2; size <= NP; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int q = tid; q < NP / 2; q += TB) {
+          const int lo = 2 * q - (q & (stride - 1));
+          const int hi = lo + stride;
+          const bool up = (lo & size) == 0;
+          const u64 ka = skey[lo], kb = skey[hi];
+          const int ia = sidx[lo], ib = sidx[hi];
+          const bool gt = ka > kb || (ka == kb && ia > ib);
+          if (gt == up) {
+            skey[lo] = kb; skey[hi] = ka;
+            sidx[lo] = ib; sidx[hi] = ia;
+          }
+        }
+        __syncthreads();
+      }
+    for (int q = tid; q < n; q += TB) pos[sidx[q]] = q;
+    for (int q = tid; q < (m + 31) / 32; q += TB) {
+      used[q] = 0;
+      uint32_t v = 0;
+      for (int t = 0; t < 32 && q * 32 + t < m; ++t) v |= (uint32_t)(synd[q * 32 + t] & 1u) << t;
+      sb[q] = v;
+    }
+    if (tid == 0) s_npiv = 0;
+    __syncthreads();
+    // 2. H with permuted columns, word-major; each thread owns whole rows
+    for (int i = tid; i < m; i += TB) {
+      for (int q = 0; q < W; ++q) M[(size_t)q * m + i] = 0;
+      for (int e = A.rp[i]; e < A.rp[i + 1]; ++e) {
+        const int p = pos[A.ci[e]];
+        M[(size_t)(p >> 6) * m + i] ^= 1ull << (p & 63);
+      }
+    }
+    __syncthreads();
+    // 3. Gauss-Jordan over positions in order (greedy pivots = ldpc's pivot set)
+    for (int p = 0; p < n; ++p) {
+      if (s_npiv >= rank) break;
+      if (tid == 0) s_piv[p & 1] = 0x7FFFFFFF;  // the other slot may still be read
+      __syncthreads();
+      const u64* Mp = M + (size_t)(p >> 6) * m;
+      const u64 bit = 1ull << (p & 63);
+      for (int i = tid; i < m; i += TB)
+        if (!((used[i >> 5] >> (i & 31)) & 1u) && (Mp[i] & bit)) {
+          atomicMin(&s_piv[p & 1], i);
+          break;
+        }
+      __syncthreads();
+      const int r = s_piv[p & 1];
+      if (r == 0x7FFFFFFF) continue;  // dependent position (uniform)
+      const uint32_t sr = (sb[r >> 5] >> (r & 31)) & 1u;
+      for (int i = tid; i < m; i += TB)
+        if (i != r && (Mp[i] & bit)) {
+          for (int q = 0; q < W; ++q) M[(size_t)q * m + i] ^= M[(size_t)q * m + r];
+          if (sr) atomicXor(&sb[i >> 5], 1u << (i & 31));
+        }
+      __syncthreads();
+      if (tid == 0) {
+        used[r >> 5] |= 1u << (r & 31);
+        pivrow[s_npiv] = r;
+        pivpos[s_npiv] = p;
+        s_npiv = s_npiv + 1;
+      }
+      __syncthreads();
+    }
+    const int r = s_npiv;
+    // 4. Neal's column swaps -> non-pivot order Ht (positions swp[r + j])
+    for (int q = tid; q < n; q += TB) swp[q] = q;
+    __syncthreads();
+    if (tid == 0)
+      for (int i = 0; i < r; ++i) {
+        const int a = swp[i];
+        swp[i] = swp[pivpos[i]];
+        swp[pivpos[i]] = a;
+      }
+    __syncthreads();
+    // 5. S0 and x(h_j) as bit-vectors over the pivot index
+    const int RWr = (r + 63) / 64;
+    for (int t = tid; t < (1 + nh) * RWr; t += TB) {
+      const int j = t / RWr, q = t % RWr;
+      u64 v = 0;
+      for (int c = 0; c < 64 && q * 64 + c < r; ++c) {
+        const int row = pivrow[q * 64 + c];
+        u64 bitv;
+        if (j == 0) {
+          bitv = (sb[row >> 5] >> (row & 31)) & 1u;
+        } else {
+          const int hp = swp[r + j - 1];
+          bitv = (M[(size_t)(hp >> 6) * m + row] >> (hp & 63)) & 1ull;
+        }
+        v |= bitv << c;
+      }
+      X[(size_t)j * RW + q] = v;
+    }
+    if (tid == 0) s_best = ~0ull;
+    __syncthreads();
+    // 6. candidates: lexicographic min of (weight, index)
+    long long L = 1;
+    if (A.method == 1 && w > 0) L = 1ll << w;
+    if (A.method == 2 && w >= 0) L = 1 + (long long)k + (long long)w * (w - 1) / 2;
+    if (A.method == 0 || A.order == 0 || k == 0) L = 1;
+    u64 best = ~0ull;
+    for (long long c = tid; c < L; c += TB) {
+      int tj[2];
+      int nt = 0;
+      unsigned long long ebits = 0;
+      if (A.method == 1) {
+        ebits = (unsigned long long)c;
+        nt = __popcll(ebits);
+      } else if (c >= 1 && c <= k) {
+        tj[0] = (int)(c - 1);
+        nt = 1;
+      } else if (c > k) {
+        long long rem = c - 1 - k;
+        int i = 0;
+        while (rem >= w - 1 - i) {
+          rem -= w - 1 - i;
+          ++i;
+        }
+        tj[0] = i;
+        tj[1] = i + 1 + (int)rem;
+        nt = 2;
+      }
+      long long cnt = nt;
+      for (int q = 0; q < RWr; ++q) {
+        u64 v = X[q];
+        if (A.method == 1) {
+          for (unsigned long long e = ebits; e; e &= e - 1) v ^= X[(size_t)(1 + __ffsll((long long)e) - 1) * RW + q];
+        } else {
+          for (int a = 0; a < nt; ++a) v ^= X[(size_t)(1 + tj[a]) * RW + q];
+        }
+        cnt += __popcll(v);
+      }
+      const u64 key = ((u64)cnt << 40) | (u64)c;
+      if (key < best) best = key;
+    }
+    if (best != ~0ull) atomicMin(&s_best, best);
+    __syncthreads();
+    // 7. outputs
+    const long long cw = (long long)(s_best & ((1ull << 40) - 1));
+    int tw[2];
+    int ntw = 0;
+    unsigned long long ewb = 0;
+    if (A.method == 1) {
+      ewb = (unsigned long long)cw;
+    } else if (cw >= 1 && cw <= k) {
+      tw[0] = (int)(cw - 1);
+      ntw = 1;
+    } else if (cw > k) {
+      long long rem = cw - 1 - k;
+      int i = 0;
+      while (rem >= w - 1 - i) {
+        rem -= w - 1 - i;
+        ++i;
+      }
+      tw[0] = i;
+      tw[1] = i + 1 + (int)rem;
+      ntw = 2;
+    }
+    for (int j = tid; j < n; j += TB) {
+      ow[j] = 0;
+      if (o0) o0[j] = 0;
+    }
+    __syncthreads();
+    for (int i = tid; i < r; i += TB) {
+      const int q = i >> 6, c = i & 63;
+      const u64 s0 = (X[q] >> c) & 1ull;
+      u64 v = X[q];
+      if (A.method == 1) {
+        for (unsigned long long e = ewb; e; e &= e - 1) v ^= X[(size_t)(1 + __ffsll((long long)e) - 1) * RW + q];
+      } else {
+        for (int a = 0; a < ntw; ++a) v ^= X[(size_t)(1 + tw[a]) * RW + q];
+      }
+      const int col = sidx[pivpos[i]];
+      ow[col] = (uint8_t)((v >> c) & 1ull);
+      if (o0) o0[col] = (uint8_t)s0;
+    }
+    if (tid == 0) {
+      if (A.method == 1) {
+        for (unsigned long long e = ewb; e; e &= e - 1) ow[sidx[swp[r + __ffsll((long long)e) - 1]]] = 1;
+      } else {
+        for (int a = 0; a < ntw; ++a) ow[sidx[swp[r + tw[a]]]] = 1;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+struct qldpc_osd_gpu {
+  qldpc_osd host;  // shape, method, order, rank
+  int device = 0, grid = 0, W = 0, RW = 0, NP = 0, nh = 0;
+  size_t lds = 0;
+  long long ws_words = 0, iws_ints = 0;
+  qldpc_rt::DevBuf rp, ci, ws, iws;
+};
+
+extern "C" {
+
+int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int32_t osd_method, int32_t osd_order,
+                         qldpc_osd_gpu** out) {
+  if (!g || !channel_probs || !out) return set_err(QLDPC_EINVAL, "NULL argument");
+  qldpc_osd* O = nullptr;
+  int rc = qldpc_osd_create(g->m, g->n, g->row_ptr.data(), g->col_idx.data(), channel_probs, osd_method, osd_order,
+                            &O);
+  if (rc) return rc;
+  if (!O->uniform) {
+    qldpc_osd_destroy(O);
+    return set_err(QLDPC_ENOTSUP, "GPU OSD needs uniform channel_probs (use the host stage, qldpc_osd_*)");
+  }
+  if (g->n > kOsdMaxN || (osd_method == 1 && osd_order > 24)) {
+    qldpc_osd_destroy(O);
+    return set_err(QLDPC_ENOTSUP, "GPU OSD: n > 8192 or osd_e order > 24");
+  }
+  auto* G = new qldpc_osd_gpu();
+  G->host = *O;
+  qldpc_osd_destroy(O);
+  G->device = g->device;
+  const int m = g->m, n = g->n, rank = G->host.rank, k = n - rank;
+  const int w = std::min(G->host.order, k);
+  G->W = (n + 63) / 64;
+  G->RW = std::max(1, (rank + 63) / 64);
+  G->NP = 1;
+  while (G->NP < n) G->NP <<= 1;
+  G->nh = G->host.method == 2 ? k : w;
+  G->lds = (size_t)G->NP * 12 + (size_t)n * 4 + (size_t)((m + 31) / 32) * 8 + 64;
+  G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW;
+  G->iws_ints = 2ll * rank + n;
+  auto fail = [&](int code) {
+    G->rp.release(); G->ci.release(); G->ws.release(); G->iws.release();
+    delete G;
+    return code;
+  };
+  if (hipSetDevice(g->device) != hipSuccess) return fail(set_err(QLDPC_EHIP, "hipSetDevice"));
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)
+    return fail(set_err(QLDPC_EHIP, "device CU count"));
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&osd_gpu_kernel), kOsdThreads,
+                                                   G->lds) != hipSuccess || nb <= 0)
+    nb = 1;
+  G->grid = cus * nb;
+  const size_t E = g->col_idx.size();
+  if ((rc = G->rp.alloc((size_t)(m + 1) * 4)) || (rc = G->ci.alloc(std::max<size_t>(E, 1) * 4)) ||
+      (rc = G->ws.alloc((size_t)G->grid * G->ws_words * 8)) || (rc = G->iws.alloc((size_t)G->grid * G->iws_ints * 4)))
+    return fail(rc);
+  if (hipMemcpy(G->rp.p, g->row_ptr.data(), (size_t)(m + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      (E && hipMemcpy(G->ci.p, g->col_idx.data(), E * 4, hipMemcpyHostToDevice) != hipSuccess))
+    return fail(set_err(QLDPC_EHIP, "upload OSD graph"));
+  *out = G;
+  return 0;
+}
+
+int qldpc_osd_gpu_destroy(qldpc_osd_gpu* osd) {
+  if (!osd) return 0;
+  osd->rp.release(); osd->ci.release(); osd->ws.release(); osd->iws.release();
+  delete osd;
+  return 0;
+}
+
+int qldpc_osd_gpu_decode(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double* d_post, const uint8_t* d_conv,
+                         const uint8_t* d_bp_corr, uint8_t* d_out0, uint8_t* d_outw, int64_t B, void* stream) {
+  if (!osd || (B > 0 && (!d_synd || !d_post || !d_outw))) return set_err(QLDPC_EINVAL, "NULL argument");
+  if (d_conv && !d_bp_corr) return set_err(QLDPC_EINVAL, "conv needs bp_corr");
+  if (B <= 0) return 0;
+  QLDPC_HIP(hipSetDevice(osd->device));
+  OsdGpuArgs a;
+  a.rp = static_cast<const int32_t*>(osd->rp.p);
+  a.ci = static_cast<const int32_t*>(osd->ci.p);
+  a.synd = d_synd; a.post = d_post; a.conv = d_conv; a.bp_corr = d_bp_corr; a.out0 = d_out0; a.outw = d_outw;
+  a.ws = static_cast<u64*>(osd->ws.p);
+  a.iws = static_cast<int32_t*>(osd->iws.p);
+  a.B = B;
+  a.m = osd->host.m; a.n = osd->host.n; a.W = osd->W; a.RW = osd->RW; a.rank = osd->host.rank;
+  a.method = osd->host.method; a.order = osd->host.order; a.NP = osd->NP;
+  a.ws_words = osd->ws_words; a.iws_ints = osd->iws_ints;
+  const int grid = (int)std::min<long long>(B, osd->grid);
+  hipLaunchKernelGGL(osd_gpu_kernel, dim3(grid), dim3(kOsdThreads), osd->lds, (hipStream_t)stream, a);
+  QLDPC_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

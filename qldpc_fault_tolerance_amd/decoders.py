@@ -105,8 +105,8 @@ class BPOSD_Decoder:
     """
 
     def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, osd_method, osd_order,
-                 precision: int = 64, device: int = 0, osd_threads: int = 0):
-        from .engine import DeviceBP, HostOSD
+                 precision: int = 64, device: int = 0, osd_threads: int = 0, use_gpu_osd: bool = True):
+        from .engine import DeviceBP, DeviceOSD, HostOSD
 
         self.h = h
         H = h if isinstance(h, CSR) else CSR.from_dense(h)
@@ -116,6 +116,10 @@ class BPOSD_Decoder:
         self.decoder = DeviceBP(H, self.channel_probs, max_iter=_int_max_iter(max_iter, H.n), bp_method=bp_method,
                                 ms_scaling_factor=ms_scaling_factor, precision=precision, device=device, soft=True)
         self.osd = HostOSD(H, self.channel_probs, osd_method=osd_method, osd_order=osd_order)
+        # OSD on the GPU for uniform priors (every reference call site); the host stage otherwise
+        self.gpu_osd = (DeviceOSD(self.decoder.graph, self.channel_probs, osd_method, osd_order)
+                        if use_gpu_osd and DeviceOSD.supported(H.n, self.channel_probs, osd_method, osd_order)
+                        else None)
         self.osd_threads = osd_threads
         self.iter, self.converge = 0, 0
 
@@ -123,8 +127,11 @@ class BPOSD_Decoder:
         """[B, m] syndromes -> osdw corrections [B, n] (int); also sets the batch's
         ``osd0_batch``, ``bp_batch``, ``conv_batch``, ``iters_batch``, ``post_batch``."""
         s = np.atleast_2d(np.asarray(synd))
-        corr, iters, conv, post = self.decoder.decode_batch_soft(s)
-        o0, ow = self.osd.decode_batch(s, post, conv, corr, threads=self.osd_threads)
+        if self.gpu_osd is not None:
+            ow, o0, corr, iters, conv, post = self.gpu_osd.bposd_batch(self.decoder, s)
+        else:
+            corr, iters, conv, post = self.decoder.decode_batch_soft(s)
+            o0, ow = self.osd.decode_batch(s, post, conv, corr, threads=self.osd_threads)
         self.bp_batch, self.iters_batch, self.conv_batch, self.post_batch = corr, iters, conv, post
         self.osd0_batch = o0.astype(np.int64)
         return ow.astype(np.int64)

@@ -238,6 +238,79 @@ class HostOSD:
             self.handle = None
 
 
+class DeviceOSD:
+    """OSD on the GPU (``qldpc_osd_gpu_*``): one workgroup per non-converged syndrome, fed
+    straight from the soft-output BP's device buffers.  Uniform priors only (every
+    reference call site); ``supported`` says whether a graph / prior vector qualifies."""
+
+    MAX_N = 8192
+
+    @staticmethod
+    def supported(n, channel_probs, osd_method, osd_order) -> bool:
+        p = np.broadcast_to(np.asarray(channel_probs, dtype=np.float64), (n,))
+        key = str(osd_method).lower() if not isinstance(osd_method, (int, np.integer)) else None
+        meth = OSD_METHODS.get(key, -1) if key is not None else int(osd_method)
+        return n <= DeviceOSD.MAX_N and bool(np.all(p == p[0])) and not (meth == 1 and int(osd_order) > 24)
+
+    def __init__(self, graph: DeviceGraph, channel_probs, osd_method="osd_e", osd_order=10):
+        self.graph = graph
+        n = graph.n
+        key = str(osd_method).lower() if not isinstance(osd_method, (int, np.integer)) else None
+        if key is not None and key not in OSD_METHODS:
+            raise ValueError(f"unknown osd_method {osd_method!r}")
+        self.osd_method = OSD_METHODS[key] if key is not None else int(osd_method)
+        self.osd_order = int(osd_order)
+        probs = np.asarray(channel_probs, dtype=np.float64)
+        self._probs = np.ascontiguousarray(np.full(n, float(probs)) if probs.ndim == 0 else probs)
+        h = ctypes.c_void_p()
+        _native.check(_native.lib().qldpc_osd_gpu_create(graph.handle, self._probs.ctypes.data_as(ctypes.c_void_p),
+                                                         self.osd_method, self.osd_order, ctypes.byref(h)),
+                      "qldpc_osd_gpu_create")
+        self.handle = h
+
+    def decode_device(self, synd_dev, post_dev, conv_dev, corr_dev, out0_dev, outw_dev, stream=None):
+        torch = _torch()
+        B = int(synd_dev.shape[0])
+        s = stream if stream is not None else _stream_handle(torch, synd_dev.device)
+
+        def ptr(t):
+            return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+        _native.check(_native.lib().qldpc_osd_gpu_decode(self.handle, ptr(synd_dev), ptr(post_dev), ptr(conv_dev),
+                                                         ptr(corr_dev), ptr(out0_dev), ptr(outw_dev), B, s),
+                      "qldpc_osd_gpu_decode")
+
+    def bposd_batch(self, bp: "DeviceBP", synd):
+        """Soft BP (``bp``, soft=True) then GPU OSD, all on the device: ``synd`` [B, m] ->
+        (osdw, osd0, bp_corr, iters, conv, post) as host arrays."""
+        torch = _torch()
+        s = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.int64) % 2, dtype=np.uint8)
+        B, n = s.shape[0], self.graph.n
+        dev = torch.device("cuda", self.graph.device)
+        sd = torch.from_numpy(s).to(dev)
+        corr = torch.empty((B, n), dtype=torch.uint8, device=dev)
+        iters = torch.empty(B, dtype=torch.int32, device=dev)
+        conv = torch.empty(B, dtype=torch.uint8, device=dev)
+        post = torch.empty((B, n), dtype=torch.float64, device=dev)
+        o0 = torch.empty((B, n), dtype=torch.uint8, device=dev)
+        ow = torch.empty((B, n), dtype=torch.uint8, device=dev)
+        st = _stream_handle(torch, dev)
+        _native.check(_native.lib().qldpc_bp_decode_batch_soft(
+            bp.handle, ctypes.c_void_p(sd.data_ptr()), ctypes.c_void_p(corr.data_ptr()),
+            ctypes.c_void_p(iters.data_ptr()), ctypes.c_void_p(conv.data_ptr()), ctypes.c_void_p(post.data_ptr()),
+            B, st), "qldpc_bp_decode_batch_soft")
+        self.decode_device(sd, post, conv, corr, o0, ow, st)
+        torch.cuda.synchronize(dev)
+        return (ow.cpu().numpy(), o0.cpu().numpy(), corr.cpu().numpy().astype(np.int64), iters.cpu().numpy(),
+                conv.cpu().numpy().astype(bool), post.cpu().numpy())
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _native._lib is not None:
+            _native.lib().qldpc_osd_gpu_destroy(h)
+            self.handle = None
+
+
 @dataclass
 class MCResult:
     shots: int

@@ -130,3 +130,39 @@ def test_bposd_shot_loop_matches_oracle_per_shot(gpu, oracle):
     from qldpc_fault_tolerance_amd.simulators import word_error_rate
 
     assert wer == word_error_rate(fails, S, code.K)[0]
+
+
+@pytest.mark.parametrize("name,t0,method,order", [
+    ("hgp_34_n225", 0, "osd_e", 10), ("hgp_34_n225", 0, "osd_cs", 8), ("hgp_34_n225", 0, "osd_0", 0),
+    ("hgp_34_n1600", 0, "osd_e", 10), ("hgp_34_n1600", 0, "osd_cs", 6), ("hgp_34_n225", 3, "osd_e", 8)])
+def test_gpu_osd_matches_host_osd(gpu, name, t0, method, order):
+    """GPU OSD kernel == native host OSD stage (itself pinned to the oracle in
+    tests/test_osd_cpu.py) on GPU soft-BP posteriors, incl. a rank-deficient
+    space-time graph (t0 = 3 repetitions)."""
+    from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceOSD, HostOSD
+
+    code = codes.get_code(name)
+    H = code.hz if t0 == 0 else codes.space_time_csr(code.hz, t0).to_dense().astype(np.uint8)
+    n = H.shape[1]
+    p = 0.05 if t0 else (0.09 if n < 1000 else 0.06)
+    synd, _ = _sample(H, p, 192, seed=len(method) + order)
+    bp = DeviceBP(H, p, max_iter=max(1, int(code.N / 10)), ms_scaling_factor=0.625, precision=64, soft=True)
+    osd = DeviceOSD(bp.graph, np.full(n, p), method, order)
+    ow, o0, corr, iters, conv, post = osd.bposd_batch(bp, synd)
+    assert (~conv).sum() > 0
+    h0, hw = HostOSD(H, np.full(n, p), method, order).decode_batch(synd, post, conv, corr)
+    assert np.array_equal(o0, h0)
+    assert np.array_equal(ow, hw)
+    assert np.array_equal((H.astype(np.int64) @ ow.T.astype(np.int64) % 2).T, synd)
+    assert DeviceOSD.supported(n, p, method, order) and not DeviceOSD.supported(n, np.linspace(.01, .1, n), method, 1)
+
+
+def test_bposd_decoder_host_and_gpu_osd_agree(gpu):
+    from qldpc_fault_tolerance_amd.decoders import BPOSD_Decoder
+
+    code = codes.get_code("hgp_34_n225")
+    synd, _ = _sample(code.hx, 0.1, 128, seed=3)
+    a = BPOSD_Decoder(code.hx, 0.1 * np.ones(code.N), 22, "minimum_sum", 0.625, "osd_e", 10)
+    b = BPOSD_Decoder(code.hx, 0.1 * np.ones(code.N), 22, "minimum_sum", 0.625, "osd_e", 10, use_gpu_osd=False)
+    assert a.gpu_osd is not None and b.gpu_osd is None
+    assert np.array_equal(a.decode_batch(synd), b.decode_batch(synd))
