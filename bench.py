@@ -232,7 +232,7 @@ def bposd_main(a, torch, dist, world, rank, dev):
         "osd_decodes": osd_n, "osd_frac_of_decodes": osd_n / max(1, 2 * shots),
         "logical_error_rate": fails / max(shots, 1),
         "roofline": None,
-        "note": "wall clock of fused GPU MC + GPU soft BP + host OSD on the non-converged decodes",
+        "note": "wall clock of fused GPU MC + GPU soft BP + GPU OSD (osd_gpu_kernel) on the non-converged decodes + host bookkeeping",
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -230,21 +230,33 @@ class CodeSimulator_DataError:
                    (1, need_z, self.decoder_z, code.csr("hx"), code.csr("lx"))]
         fails = osd_n = 0
         kept_e, kept_f = [], []
+        dev = torch.device("cuda", mc.device)
+        n = code.N
         for s0 in range(b, b + c, int(batch)):
             S = min(int(batch), b + c - s0)
-            res = mc.run(px, py, pz, self.seed, s0, S, self.eval_logical_type, per_shot=True)
+            cnt = mc.new_counters()
+            f_d = torch.zeros(S, dtype=torch.uint8, device=dev)
+            e_d = torch.zeros((S, n), dtype=torch.uint8, device=dev)
+            c_d = torch.zeros((S, 2, n), dtype=torch.uint8, device=dev)
+            it_d = torch.zeros((S, 2), dtype=torch.int32, device=dev)
+            mc.launch(px, py, pz, self.seed, s0, S, self.eval_logical_type, cnt, None, f_d, e_d, c_d, it_d)
+            fail = f_d.cpu().numpy()
             sf = np.zeros((S, 2), dtype=bool)
             for q, need, dec, H, L in sectors:
                 if not need:
                     continue
-                e = ((res.err >> q) & 1).astype(np.uint8)
-                synd = gf2_rows(H, e)
-                f = ((res.fail >> q) & 1).astype(bool)
-                idx = np.flatnonzero((gf2_rows(H, res.corr[:, q, :]) != synd).any(1))
-                if idx.size:
-                    r = e[idx] ^ dec.decode_batch(synd[idx]).astype(np.uint8)
-                    f[idx] = gf2_rows(H, r).any(1) | gf2_rows(L, r).any(1)
-                    osd_n += int(idx.size)
+                f = ((fail >> q) & 1).astype(bool)
+                # BP stopped before max_iter <=> it converged; only shots at max_iter may need OSD
+                cand = torch.nonzero(it_d[:, q] >= dec.decoder.max_iter).flatten()
+                if cand.numel():
+                    ci = cand.cpu().numpy()
+                    e = ((e_d[cand] >> q) & 1).cpu().numpy()
+                    synd = gf2_rows(H, e)
+                    bad = np.flatnonzero((gf2_rows(H, c_d[cand, q, :].cpu().numpy()) != synd).any(1))
+                    if bad.size:
+                        r = e[bad] ^ dec.decode_batch(synd[bad]).astype(np.uint8)
+                        f[ci[bad]] = gf2_rows(H, r).any(1) | gf2_rows(L, r).any(1)
+                        osd_n += int(bad.size)
                 sf[:, q] = f
             if self.eval_logical_type == "X":
                 fails += int(sf[:, 0].sum())
@@ -253,7 +265,7 @@ class CodeSimulator_DataError:
             else:
                 fails += int((sf[:, 0] | sf[:, 1]).sum())
             if keep_shots:
-                kept_e.append(res.err)
+                kept_e.append(e_d.cpu().numpy())
                 kept_f.append(sf)
         if keep_shots:
             self.last_shots = (np.concatenate(kept_e) if kept_e else None, np.concatenate(kept_f) if kept_f else None)
