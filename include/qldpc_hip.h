@@ -219,6 +219,13 @@ int qldpc_phenl_launch(qldpc_phenl *ph, double px, double py, double pz, double 
                        uint64_t shot_begin, int64_t shot_count, int32_t num_rounds, int32_t logical_mode,
                        const double *d_uniforms, void *d_counters, uint8_t *d_fail, uint8_t *d_trace, void *stream);
 
+/* BP+OSD as the final-round decoder (decoder2 = BPOSD_Decoder in the
+ * notebooks, src/Decoders.py:100-138): the sectors given a GPU OSD handle
+ * decode the perfect round with soft BP (dec2 must come from
+ * qldpc_bp_create_soft) and then OSD where BP did not converge.  NULL = plain
+ * BP for that sector.  Declared after qldpc_osd_gpu above. */
+int qldpc_phenl_set_final_osd(qldpc_phenl *ph, qldpc_osd_gpu *osd_x, qldpc_osd_gpu *osd_z);
+
 /* Launch geometry chosen for a decoder (threads per shot, vars per thread,
  * LDS bytes, resident blocks per CU) — reported by bench.py / DESIGN.md. */
 int qldpc_bp_geometry(const qldpc_bp *bp, int32_t *threads, int32_t *vars_per_thread, int32_t *lds_bytes,

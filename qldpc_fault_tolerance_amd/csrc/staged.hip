@@ -270,6 +270,9 @@ struct qldpc_phenl {
   int Wmax = 0;
   DevBuf hl_rp[2], hl_ci[2];  // [H; L] stacked CSR per sector
   DevBuf cur[2], serr[2], sprev, D[2], det[2], corr[2], iters, conv, failw[2];
+  // BP+OSD final round (qldpc_phenl_set_final_osd): soft BP posteriors and BP decisions
+  qldpc_osd_gpu* osd2[2] = {nullptr, nullptr};
+  DevBuf post, bpcorr;
 };
 
 extern "C" {
@@ -351,6 +354,26 @@ int qldpc_phenl_create(qldpc_bp* st_x, qldpc_bp* st_z, qldpc_bp* dec2_x, qldpc_b
   return 0;
 }
 
+int qldpc_phenl_set_final_osd(qldpc_phenl* P, qldpc_osd_gpu* osd_x, qldpc_osd_gpu* osd_z) {
+  if (!P) return set_err(QLDPC_EINVAL, "NULL phenl");
+  qldpc_osd_gpu* o[2] = {osd_x, osd_z};
+  for (int q = 0; q < 2; ++q) {
+    if (!o[q]) continue;
+    int32_t eng = 0;
+    qldpc_bp_engine(P->d2[q], &eng);
+    if (eng != 1) return set_err(QLDPC_ENOTSUP, "BP+OSD final round needs dec2 from qldpc_bp_create_soft");
+  }
+  if ((osd_x || osd_z) && !P->post.p) {
+    QLDPC_HIP(hipSetDevice(P->device));
+    int rc;
+    if ((rc = P->post.alloc((size_t)P->max_batch * P->n * 8)) || (rc = P->bpcorr.alloc((size_t)P->max_batch * P->n)))
+      return rc;
+  }
+  P->osd2[0] = osd_x;
+  P->osd2[1] = osd_z;
+  return 0;
+}
+
 int qldpc_phenl_destroy(qldpc_phenl* P) {
   if (!P) return 0;
   for (int q = 0; q < 2; ++q) {
@@ -358,6 +381,7 @@ int qldpc_phenl_destroy(qldpc_phenl* P) {
     P->D[q].release(); P->det[q].release(); P->corr[q].release(); P->failw[q].release();
   }
   P->sprev.release(); P->iters.release(); P->conv.release();
+  P->post.release(); P->bpcorr.release();
   delete P;
   return 0;
 }
@@ -474,9 +498,21 @@ int qldpc_phenl_launch(qldpc_phenl* P, double px, double py, double pz, double q
                            static_cast<const unsigned long long*>(P->D[s].p), static_cast<uint8_t*>(P->det[s].p),
                            d_trace, tlen, toff, c0, R, W, B);
         QLDPC_HIP(hipGetLastError());
-        int rc = qldpc_bp_decode_batch(P->d2[s], static_cast<const uint8_t*>(P->det[s].p),
-                                       static_cast<uint8_t*>(P->corr[s].p), static_cast<int32_t*>(P->iters.p),
-                                       static_cast<uint8_t*>(P->conv.p), B, stream);
+        int rc;
+        if (P->osd2[s]) {  // bposd_decoder as decoder2: BP, then OSD where BP did not converge
+          rc = qldpc_bp_decode_batch_soft(P->d2[s], static_cast<const uint8_t*>(P->det[s].p),
+                                          static_cast<uint8_t*>(P->bpcorr.p), static_cast<int32_t*>(P->iters.p),
+                                          static_cast<uint8_t*>(P->conv.p), static_cast<double*>(P->post.p), B, stream);
+          if (!rc)
+            rc = qldpc_osd_gpu_decode(P->osd2[s], static_cast<const uint8_t*>(P->det[s].p),
+                                      static_cast<const double*>(P->post.p), static_cast<const uint8_t*>(P->conv.p),
+                                      static_cast<const uint8_t*>(P->bpcorr.p), nullptr,
+                                      static_cast<uint8_t*>(P->corr[s].p), B, stream);
+        } else {
+          rc = qldpc_bp_decode_batch(P->d2[s], static_cast<const uint8_t*>(P->det[s].p),
+                                     static_cast<uint8_t*>(P->corr[s].p), static_cast<int32_t*>(P->iters.p),
+                                     static_cast<uint8_t*>(P->conv.p), B, stream);
+        }
         if (rc) return rc;
         hipLaunchKernelGGL(ph_iters, dim3((unsigned)((B + kTile - 1) / kTile)), dim3(kTile), 0, st,
                            static_cast<const int32_t*>(P->iters.p), static_cast<const uint8_t*>(P->conv.p), cnt, s, B);

@@ -435,6 +435,16 @@ class DevicePhenl:
             int(max_batch), ctypes.byref(h)), "qldpc_phenl_create")
         self.handle = h
 
+    def set_final_osd(self, osd_x: "DeviceOSD | None", osd_z: "DeviceOSD | None"):
+        """BP+OSD final round (decoder2 = BPOSD_Decoder): ``qldpc_phenl_set_final_osd``."""
+        for o, d in ((osd_x, self.decoders[2]), (osd_z, self.decoders[3])):
+            if o is not None and o.graph.n != d.n:
+                raise ValueError("OSD graph does not match the final-round decoder")
+        self._osd2 = (osd_x, osd_z)  # keep the handles alive
+        _native.check(_native.lib().qldpc_phenl_set_final_osd(
+            self.handle, osd_x.handle if osd_x is not None else None, osd_z.handle if osd_z is not None else None),
+            "qldpc_phenl_set_final_osd")
+
     def trace_len(self, num_rounds: int) -> int:
         v = ctypes.c_int64()
         _native.check(_native.lib().qldpc_phenl_trace_len(self.handle, int(num_rounds), ctypes.byref(v)),

@@ -86,6 +86,14 @@ def _engine_bp(decoder):
     return bp if isinstance(bp, DeviceBP) else None
 
 
+def _final_round_bp(decoder):
+    """DeviceBP of a final-round decoder: an engine BPDecoder, or a BPOSD_Decoder whose OSD
+    runs on the GPU (its soft BP then feeds qldpc_phenl_set_final_osd)."""
+    if _is_bposd(decoder):
+        return decoder.decoder if getattr(decoder, "gpu_osd", None) is not None else None
+    return _engine_bp(decoder)
+
+
 def _is_bposd(decoder) -> bool:
     return getattr(decoder, "osd", None) is not None
 
@@ -521,10 +529,13 @@ class CodeSimulator_Phenon_SpaceTime:
         d1 = (self.decoder1_x, self.decoder1_z)
         if not all(isinstance(d, ST_BP_Decoder_syndrome) and d.num_rep == self.num_rep for d in d1):
             return None
-        b2 = (_engine_bp(self.decoder2_x), _engine_bp(self.decoder2_z))
+        b2 = tuple(_final_round_bp(d) for d in (self.decoder2_x, self.decoder2_z))
         if any(b is None for b in b2):
             return None
         return d1[0].space_decoder, d1[1].space_decoder, b2[0], b2[1]
+
+    def _final_osd(self):
+        return tuple(getattr(d, "gpu_osd", None) for d in (self.decoder2_x, self.decoder2_z))
 
     def fused_counts(self, num_rounds: int, num_samples: int):
         """Run ``num_samples`` samples on the GPU; returns the all-reduced :class:`~.engine.MCResult`."""
@@ -538,6 +549,9 @@ class CodeSimulator_Phenon_SpaceTime:
             self.seed = random.getrandbits(64)
         if self._ph is None:
             self._ph = DevicePhenl(self.code, *parts, num_rep=self.num_rep, max_batch=self.max_batch)
+            ox, oz = self._final_osd()
+            if ox is not None or oz is not None:
+                self._ph.set_final_osd(ox, oz)
         rank, ws = parallel.world()
         b, c = parallel.shard_range(num_samples, rank, ws, begin=self._shot_offset)
         self._shot_offset += int(num_samples)

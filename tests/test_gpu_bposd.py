@@ -166,3 +166,52 @@ def test_bposd_decoder_host_and_gpu_osd_agree(gpu):
     b = BPOSD_Decoder(code.hx, 0.1 * np.ones(code.N), 22, "minimum_sum", 0.625, "osd_e", 10, use_gpu_osd=False)
     assert a.gpu_osd is not None and b.gpu_osd is None
     assert np.array_equal(a.decode_batch(synd), b.decode_batch(synd))
+
+
+def test_phenl_space_time_with_bposd_final_round(gpu):
+    """CodeSimulator_Phenon_SpaceTime with decoder2 = BPOSD_Decoder (the notebooks'
+    final-round decoder): the staged GPU pipeline runs soft BP + GPU OSD on the
+    perfect round.  Same seed as with a BP final round: identical detector
+    traces (noise and ST decodes do not depend on decoder2), and per sample the
+    BP+OSD verdict fails only where the BP verdict fails (OSD leaves no
+    syndrome mismatch), with strictly fewer sector failures here."""
+    from qldpc_fault_tolerance_amd.decoders import BPOSD_Decoder_Class, ST_BP_Decoder_Class
+    from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceOSD, DevicePhenl
+
+    code = codes.get_code("hgp_34_n225")
+    p, rep, rounds, S = 0.01, 3, 3, 3000
+    n = code.N
+    mi = int(n / 10)
+
+    def st(H, m):
+        return DeviceBP(codes.space_time_csr(H, rep), np.hstack([p * np.ones(n), p * np.ones(m)] * rep),
+                        max_iter=mi, precision=64)
+
+    def run(osd):
+        d2x = DeviceBP(code.hz, p, max_iter=mi, precision=64, soft=osd)
+        d2z = DeviceBP(code.hx, p, max_iter=mi, precision=64, soft=osd)
+        ph = DevicePhenl(code, st(code.hz, code.hz.shape[0]), st(code.hx, code.hx.shape[0]), d2x, d2z,
+                         num_rep=rep)
+        if osd:
+            ph.set_final_osd(DeviceOSD(d2x.graph, p * np.ones(n), "osd_e", 10),
+                             DeviceOSD(d2z.graph, p * np.ones(n), "osd_e", 10))
+        return ph.run(p / 2, p / 2, p / 2, p, 4242, 0, S, rounds, "Total", per_shot=True)
+
+    bp, bo = run(False), run(True)
+    assert np.array_equal(bp.trace, bo.trace)
+    assert not np.any((bo.fail != 0) & (bp.fail == 0))
+    assert bo.failures <= bp.failures
+    assert sum(bo.sector_fail) < sum(bp.sector_fail)
+    # the simulator routes BPOSD decoder2 objects onto that pipeline
+    from qldpc_fault_tolerance_amd.simulators import CodeSimulator_Phenon_SpaceTime
+
+    d1 = ST_BP_Decoder_Class(10, "minimum_sum", 0.625)
+    d2 = BPOSD_Decoder_Class(10, "minimum_sum", 0.625, "osd_e", 10)
+    ps = {"p_data": p, "p_syndrome": p, "num_rep": rep}
+    sim = CodeSimulator_Phenon_SpaceTime(code, d1.GetDecoder({**ps, "h": code.hz}), d1.GetDecoder({**ps, "h": code.hx}),
+                                         d2.GetDecoder({"h": code.hz, "p_data": p}),
+                                         d2.GetDecoder({"h": code.hx, "p_data": p}), pauli_error_probs=[p / 2] * 3,
+                                         q=p, eval_logical_type="Total", num_rep=rep, seed=4242)
+    assert sim._engine_parts() is not None and all(o is not None for o in sim._final_osd())
+    res = sim.fused_counts(rounds, 512)
+    assert res.shots == 512
