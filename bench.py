@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--workload", default="data", choices=("data", "phenl", "bposd"),
                     help="data = headline (config 2); phenl = space-time phenomenological (config 5)")
     ap.add_argument("--num-rep", type=int, default=3)
+    ap.add_argument("--dec2", default="bp", choices=("bp", "bposd"),
+                    help="phenl final-round decoder: BP, or BP+OSD-E(10) as the notebooks use")
     ap.add_argument("--num-cycles", type=int, default=13)
     return ap.parse_args()
 
@@ -130,10 +132,15 @@ def phenl_main(a, torch, dist, world, rank, dev):
         return DeviceBP(codes.space_time_csr(H, rep), np.hstack([p * np.ones(n), p * np.ones(m)] * rep),
                         max_iter=mi, precision=a.precision, device=dev.index)
 
-    ph = DevicePhenl(code, st(code.hz, hz.m), st(code.hx, hx.m),
-                     DeviceBP(hz, p * np.ones(n), max_iter=mi, precision=a.precision, device=dev.index),
-                     DeviceBP(hx, p * np.ones(n), max_iter=mi, precision=a.precision, device=dev.index),
-                     num_rep=rep, max_batch=a.shots)
+    soft = a.dec2 == "bposd"
+    d2x = DeviceBP(hz, p * np.ones(n), max_iter=mi, precision=a.precision, device=dev.index, soft=soft)
+    d2z = DeviceBP(hx, p * np.ones(n), max_iter=mi, precision=a.precision, device=dev.index, soft=soft)
+    ph = DevicePhenl(code, st(code.hz, hz.m), st(code.hx, hx.m), d2x, d2z, num_rep=rep, max_batch=a.shots)
+    if soft:
+        from qldpc_fault_tolerance_amd.engine import DeviceOSD
+
+        ph.set_final_osd(DeviceOSD(d2x.graph, p * np.ones(n), "osd_e", 10),
+                         DeviceOSD(d2z.graph, p * np.ones(n), "osd_e", 10))
     S = int(a.shots)
     cnt = ph.new_counters()
     for i in range(a.warmup):
@@ -172,7 +179,8 @@ def phenl_main(a, torch, dist, world, rank, dev):
         "dtype": "f32" if a.precision == 32 else "f64",
         "data": f"synthetic: Philox phenomenological noise on the synthesized {name} stand-in",
         "config": {"workload": f"{name} CodeSimulator_Phenon_SpaceTime, num_rep={rep}, num_cycles={a.num_cycles} "
-                               f"(num_rounds={R}), eval_p={p}, min-sum alpha=0.625, max_iter={mi}",
+                               f"(num_rounds={R}), eval_p={p}, min-sum alpha=0.625, max_iter={mi}"
+                               + (", decoder2 = BP+OSD-E(10)" if soft else ""),
                    "shots_per_gpu_step": S, "parallelism": f"sample-sharded x{world}"},
         "decodes_per_s": decodes / elapsed, "mean_iters_per_decode": iters / max(decodes, 1),
         "nonconverged_frac": int(w[6] + w[7]) / max(decodes, 1), "logical_error_rate": int(w[1]) / max(shots, 1),
