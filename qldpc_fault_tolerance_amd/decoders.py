@@ -125,10 +125,11 @@ class BPOSD_Decoder:
 
     def decode_batch(self, synd):
         """[B, m] syndromes -> osdw corrections [B, n] (int); also sets the batch's
-        ``osd0_batch``, ``bp_batch``, ``conv_batch``, ``iters_batch``, ``post_batch``."""
+        ``osd0_batch``, ``bp_batch``, ``conv_batch``, ``iters_batch``, ``post_batch`` (the
+        posteriors; a device tensor when the OSD ran on the GPU)."""
         s = np.atleast_2d(np.asarray(synd))
         if self.gpu_osd is not None:
-            ow, o0, corr, iters, conv, post = self.gpu_osd.bposd_batch(self.decoder, s)
+            ow, o0, corr, iters, conv, post = self.gpu_osd.bposd_batch(self.decoder, s, host_post=False)
         else:
             corr, iters, conv, post = self.decoder.decode_batch_soft(s)
             o0, ow = self.osd.decode_batch(s, post, conv, corr, threads=self.osd_threads)
@@ -141,7 +142,8 @@ class BPOSD_Decoder:
         self.bp_decoding = self.bp_batch[0]
         self.osd0_decoding = self.osd0_batch[0]
         self.osdw_decoding = ow[0]
-        self.log_prob_ratios = self.post_batch[0]
+        pb = self.post_batch
+        self.log_prob_ratios = pb[0] if isinstance(pb, np.ndarray) else pb[0].cpu().numpy()
         self.iter, self.converge = int(self.iters_batch[0]), int(self.conv_batch[0])
         return self.osdw_decoding
 

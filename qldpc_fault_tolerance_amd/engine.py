@@ -280,9 +280,10 @@ class DeviceOSD:
                                                          ptr(corr_dev), ptr(out0_dev), ptr(outw_dev), B, s),
                       "qldpc_osd_gpu_decode")
 
-    def bposd_batch(self, bp: "DeviceBP", synd):
+    def bposd_batch(self, bp: "DeviceBP", synd, host_post: bool = True):
         """Soft BP (``bp``, soft=True) then GPU OSD, all on the device: ``synd`` [B, m] ->
-        (osdw, osd0, bp_corr, iters, conv, post) as host arrays."""
+        (osdw, osd0, bp_corr, iters, conv, post) as host arrays (``post`` stays a device
+        tensor when ``host_post`` is False: 8 bytes per variable not worth copying back)."""
         torch = _torch()
         s = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.int64) % 2, dtype=np.uint8)
         B, n = s.shape[0], self.graph.n
@@ -302,7 +303,7 @@ class DeviceOSD:
         self.decode_device(sd, post, conv, corr, o0, ow, st)
         torch.cuda.synchronize(dev)
         return (ow.cpu().numpy(), o0.cpu().numpy(), corr.cpu().numpy().astype(np.int64), iters.cpu().numpy(),
-                conv.cpu().numpy().astype(bool), post.cpu().numpy())
+                conv.cpu().numpy().astype(bool), post.cpu().numpy() if host_post else post)
 
     def __del__(self):
         h = getattr(self, "handle", None)
