@@ -99,13 +99,20 @@ def _is_bposd(decoder) -> bool:
 
 
 def gf2_rows(csr, X):
-    """Rows of ``X`` [S, n] (0/1) times ``H^T`` mod 2 -> [S, m] uint8, for a :class:`~.codes.CSR` ``H``."""
+    """Rows of ``X`` [S, n] (0/1) times ``H^T`` mod 2 -> [S, m] uint8, for a :class:`~.codes.CSR` ``H``
+    (sparse x sparse: the error / residual rows are sparse)."""
     import scipy.sparse as sp
 
-    A = sp.csr_matrix((np.ones(len(csr.col_idx), np.int32), np.asarray(csr.col_idx), np.asarray(csr.row_ptr)),
-                      shape=(csr.m, csr.n))
-    X = np.asarray(X, dtype=np.int32)
-    return (np.asarray(A @ X.T).T % 2).astype(np.uint8)
+    Ht = getattr(csr, "_gf2_ht", None)
+    if Ht is None:
+        Ht = sp.csr_matrix((np.ones(len(csr.col_idx), np.int32), np.asarray(csr.col_idx), np.asarray(csr.row_ptr)),
+                           shape=(csr.m, csr.n)).T.tocsc()
+        csr._gf2_ht = Ht
+    X = np.asarray(X)
+    if X.shape[0] == 0:
+        return np.zeros((0, csr.m), dtype=np.uint8)
+    P = sp.csr_matrix(X.astype(np.int32, copy=False)) @ Ht
+    return (P.toarray() & 1).astype(np.uint8)
 
 
 class CodeSimulator_DataError:
