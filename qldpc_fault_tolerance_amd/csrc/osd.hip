@@ -357,6 +357,7 @@ struct OsdGpuArgs {
   int32_t* iws;            // per workgroup: pivrow [rank] | pivpos [rank] | swp [n]
   long long B;
   int m, n, W, RW, rank, method, order, NP;
+  int m_lds;  // 1: the matrix lives in LDS after the sort tables (flat addressing), else in the HBM slice
   long long ws_words, iws_ints;
 };
 
@@ -377,8 +378,11 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
   uint32_t* sb = used + (m + 31) / 32;                         // [ceil(m/32)] syndrome, reduced
   __shared__ int s_piv[2], s_npiv;  // s_piv double-buffered by position parity
   __shared__ u64 s_best;
-  u64* M = A.ws + (size_t)blockIdx.x * A.ws_words;
-  u64* X = M + (size_t)W * m;  // X[0] = S0, X[1 + j] = x(h_j)
+  u64* Mg = A.ws + (size_t)blockIdx.x * A.ws_words;
+  u64* X = Mg + (size_t)W * m;  // X[0] = S0, X[1 + j] = x(h_j)
+  // matrix: LDS when it fits (after the bit-vectors), else the per-workgroup HBM slice
+  u64* M = A.m_lds ? reinterpret_cast<u64*>(smem + (((size_t)NP * 12 + (size_t)n * 4 + (size_t)((m + 31) / 32) * 8 + 15) & ~(size_t)15))
+                   : Mg;
   int32_t* pivrow = A.iws + (size_t)blockIdx.x * A.iws_ints;
   int32_t* pivpos = pivrow + rank;
   int32_t* swp = pivpos + rank;
@@ -596,7 +600,7 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
 
 struct qldpc_osd_gpu {
   qldpc_osd host;  // shape, method, order, rank
-  int device = 0, grid = 0, W = 0, RW = 0, NP = 0, nh = 0;
+  int device = 0, grid = 0, W = 0, RW = 0, NP = 0, nh = 0, m_lds = 0;
   size_t lds = 0;
   long long ws_words = 0, iws_ints = 0;
   qldpc_rt::DevBuf rp, ci, ws, iws;
@@ -631,6 +635,13 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   while (G->NP < n) G->NP <<= 1;
   G->nh = G->host.method == 2 ? k : w;
   G->lds = (size_t)G->NP * 12 + (size_t)n * 4 + (size_t)((m + 31) / 32) * 8 + 64;
+  // QLDPC_OSD_LDS=1: the Gauss-Jordan image in LDS too when it fits (<= 144 KiB in all).  Off by
+  // default: measured slower (config-5 final round 244 vs 158 ms) — the image costs residency
+  // (1 workgroup per CU instead of ~6), and the HBM slice stays L2-resident anyway.
+  const size_t mbytes = (size_t)G->W * m * 8;
+  const char* lds_env = std::getenv("QLDPC_OSD_LDS");
+  G->m_lds = (lds_env && std::atoi(lds_env) == 1 && ((G->lds + 15) & ~(size_t)15) + mbytes <= 144 * 1024) ? 1 : 0;
+  if (G->m_lds) G->lds = ((G->lds + 15) & ~(size_t)15) + mbytes;
   G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW;
   G->iws_ints = 2ll * rank + n;
   auto fail = [&](int code) {
@@ -679,7 +690,7 @@ int qldpc_osd_gpu_decode(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double
   a.iws = static_cast<int32_t*>(osd->iws.p);
   a.B = B;
   a.m = osd->host.m; a.n = osd->host.n; a.W = osd->W; a.RW = osd->RW; a.rank = osd->host.rank;
-  a.method = osd->host.method; a.order = osd->host.order; a.NP = osd->NP;
+  a.method = osd->host.method; a.order = osd->host.order; a.NP = osd->NP; a.m_lds = osd->m_lds;
   a.ws_words = osd->ws_words; a.iws_ints = osd->iws_ints;
   const int grid = (int)std::min<long long>(B, osd->grid);
   hipLaunchKernelGGL(osd_gpu_kernel, dim3(grid), dim3(kOsdThreads), osd->lds, (hipStream_t)stream, a);
