@@ -376,7 +376,7 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
   int32_t* pos = sidx + NP;                                    // [n]  column -> sorted position
   uint32_t* used = reinterpret_cast<uint32_t*>(pos + n);       // [ceil(m/32)]
   uint32_t* sb = used + (m + 31) / 32;                         // [ceil(m/32)] syndrome, reduced
-  __shared__ int s_piv[2], s_npiv;  // s_piv double-buffered by position parity
+  __shared__ int s_piv[3], s_npiv;  // s_piv triple-buffered by position: reset two columns ahead
   __shared__ u64 s_best;
   u64* Mg = A.ws + (size_t)blockIdx.x * A.ws_words;
   u64* X = Mg + (size_t)W * m;  // X[0] = S0, X[1 + j] = x(h_j)
@@ -432,7 +432,10 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
       for (int t = 0; t < 32 && q * 32 + t < m; ++t) v |= (uint32_t)(synd[q * 32 + t] & 1u) << t;
       sb[q] = v;
     }
-    if (tid == 0) s_npiv = 0;
+    if (tid == 0) {
+      s_npiv = 0;
+      s_piv[0] = s_piv[1] = s_piv[2] = 0x7FFFFFFF;
+    }
     __syncthreads();
     // 2. H with permuted columns, word-major; each thread owns whole rows
     for (int i = tid; i < m; i += TB) {
@@ -443,34 +446,38 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
       }
     }
     __syncthreads();
-    // 3. Gauss-Jordan over positions in order (greedy pivots = ldpc's pivot set)
+    // 3. Gauss-Jordan over positions in order (greedy pivots = ldpc's pivot set).
+    // Barriers: one per dependent position, two per pivot.  Slot p%3 of s_piv collects
+    // column p's pivot row; thread 0 re-arms slot (p+2)%3 after this column's first
+    // barrier (its last reader, column p-1, is past that barrier; its next writer,
+    // column p+2, is behind column p+1's barrier).  used / pivrow / s_npiv change
+    // between the two barriers of a pivot column, while nobody reads them.
     for (int p = 0; p < n; ++p) {
       if (s_npiv >= rank) break;
-      if (tid == 0) s_piv[p & 1] = 0x7FFFFFFF;  // the other slot may still be read
-      __syncthreads();
       const u64* Mp = M + (size_t)(p >> 6) * m;
       const u64 bit = 1ull << (p & 63);
+      const int slot = p % 3;
       for (int i = tid; i < m; i += TB)
         if (!((used[i >> 5] >> (i & 31)) & 1u) && (Mp[i] & bit)) {
-          atomicMin(&s_piv[p & 1], i);
+          atomicMin(&s_piv[slot], i);
           break;
         }
       __syncthreads();
-      const int r = s_piv[p & 1];
+      const int r = s_piv[slot];
+      if (tid == 0) s_piv[(p + 2) % 3] = 0x7FFFFFFF;
       if (r == 0x7FFFFFFF) continue;  // dependent position (uniform)
       const uint32_t sr = (sb[r >> 5] >> (r & 31)) & 1u;
-      for (int i = tid; i < m; i += TB)
-        if (i != r && (Mp[i] & bit)) {
-          for (int q = 0; q < W; ++q) M[(size_t)q * m + i] ^= M[(size_t)q * m + r];
-          if (sr) atomicXor(&sb[i >> 5], 1u << (i & 31));
-        }
-      __syncthreads();
       if (tid == 0) {
         used[r >> 5] |= 1u << (r & 31);
         pivrow[s_npiv] = r;
         pivpos[s_npiv] = p;
         s_npiv = s_npiv + 1;
       }
+      for (int i = tid; i < m; i += TB)
+        if (i != r && (Mp[i] & bit)) {
+          for (int q = 0; q < W; ++q) M[(size_t)q * m + i] ^= M[(size_t)q * m + r];
+          if (sr) atomicXor(&sb[i >> 5], 1u << (i & 31));
+        }
       __syncthreads();
     }
     const int r = s_npiv;
