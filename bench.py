@@ -95,6 +95,11 @@ def kernel_name(dec):
     t = "float" if dec.precision == 32 else "double"
     mc = dec.graph.info()["max_col_deg"]
     dmax = 4 if mc <= 4 else (mc if g["engine"] == 3 and mc <= 6 and dec.precision == 32 else 8)
+    nch = (max(1, dec.graph.info()["max_row_deg"]) * (4 if dec.precision == 32 else 8) + 15) // 16
+    if g["engine"] == 3 and dec.precision == 64 and dmax == 4 and g["threads"] <= 256 and 4 <= g["vars_per_thread"] <= 8 \
+            and nch in (3, 4) and os.environ.get("QLDPC_F64W", "1") != "0":
+        # fp64 family for <= 256-thread workgroups (engine id 103, launch bounds 256, rows of nch chunks)
+        return f"qldpc::rmc_kernel<double, 4, {g['vars_per_thread']}, 103, {g['degree3_slots']}, 256, {nch}>"
     if g["engine"] >= 3:
         return f"qldpc::rmc_kernel<{t}, {dmax}, {g['vars_per_thread']}, {g['engine']}, {g['degree3_slots']}>"
     return f"qldpc::smc_kernel<{t}, {dmax}, 1> (engine {g['engine']})"

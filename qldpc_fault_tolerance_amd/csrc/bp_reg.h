@@ -36,9 +36,16 @@
 namespace qldpc {
 
 // Engine ids of this file: 3, 4, and 13 = engine 3 with dword-scaled edge
-// addresses (images of 64-256 KiB: the space-time graphs).
+// addresses (images of 64-256 KiB: the space-time graphs); + 100 = engine 3
+// keeping its own previous v2c in VGPRs in double precision too (the fp64
+// kernels built for <= 256-thread workgroups, whose register budget is 256).
 constexpr int eng_base(int E) { return E % 10; }
-constexpr int eng_sh(int E) { return E >= 10 ? 2 : 0; }
+constexpr int eng_sh(int E) { return (E / 10) % 10 ? 2 : 0; }
+constexpr bool eng_kv64(int E) { return (E / 100) % 10 != 0; }
+// launch bounds: LB threads per workgroup at most; 256-thread fp64 kernels are
+// built for 2 workgroups per CU (2 waves per SIMD: up to 256 VGPRs, no spills)
+template <typename T>
+constexpr int lb_waves(int LB) { return LB <= 256 ? (sizeof(T) == 8 ? 2 : 4) : 1; }
 template <int ENG>
 __device__ inline uint32_t ea_cs(uint32_t ea) { return (ea & 0xFFFFu) << eng_sh(ENG); }
 template <int ENG>
@@ -84,7 +91,16 @@ template <typename T>
 __device__ inline typename FT<T>::U canon2(T v) {
   using U = typename FT<T>::U;
   const U b = FT<T>::bits(v);
-  return b | ((b - (U)1) & ~b & FT<T>::kSign);
+  if constexpr (sizeof(T) == 8) {
+    // hi | (hi(b - 1) & sign): `& ~b` is implied (a set sign bit is kept anyway);
+    // one 64-bit add and one v_and_or
+    const U bm = b - (U)1;
+    uint32_t hi;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(bm >> 32)), "v"(0x80000000u), "v"((uint32_t)(b >> 32)));
+    return ((U)hi << 32) | (uint32_t)b;
+  } else {
+    return b | ((b - (U)1) & ~b & FT<T>::kSign);
+  }
 }
 
 // x is +0 or -0 (v_cmp_class_*: class bits 5 = -0, 6 = +0)
@@ -104,7 +120,7 @@ __device__ inline uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
 template <typename T, int DMAX, int VPL, int ENG = 3>
 struct RState {
   using U = typename FT<T>::U;
-  static constexpr bool kKeepV = eng_base(ENG) == 3 && sizeof(T) == 4;  // own v2c in VGPRs (engine 3, float)
+  static constexpr bool kKeepV = eng_base(ENG) == 3 && (sizeof(T) == 4 || eng_kv64(ENG));  // own v2c in VGPRs
   uint32_t ea[VPL][DMAX];
   T L[VPL];
   U ov[kKeepV ? VPL : 1][kKeepV ? DMAX : 1];
@@ -198,10 +214,25 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
           : "v"(d), "v"(0x60u), "v"(a), "v"(pr[t].b)
           : "vcc");
       sel &= ~kS;
+      c[t] = FT<T>::val(FT<T>::bits(FT<T>::val(sel) * alpha) ^ (d & kS));
     } else {
-      sel = (is_zero(FT<T>::val(d)) ? pr[t].b : a) & ~kS;
+      // double: the same class test on the 64-bit pair and two cndmasks; |sel| folds
+      // into v_mul_f64's source modifier; sign = hi(product) ^ (hi(d) & sign bit) in
+      // one v_bitop3 (truth table 0x6c = S1 ^ (S0 & S2))
+      uint32_t slo, shi;
+      asm("v_cmp_class_f64 vcc, %2, %3\n\ts_nop 1\n\tv_cndmask_b32 %0, %4, %5, vcc\n\tv_cndmask_b32 %1, %6, %7, vcc"
+          : "=&v"(slo), "=&v"(shi)
+          : "v"(FT<T>::val(d)), "v"(0x60u), "v"((uint32_t)a), "v"((uint32_t)pr[t].b), "v"((uint32_t)(a >> 32)),
+            "v"((uint32_t)(pr[t].b >> 32))
+          : "vcc");
+      sel = ((U)shi << 32) | slo;
+      const U pb = FT<T>::bits(__builtin_fabs(FT<T>::val(sel)) * alpha);
+      uint32_t hi;
+      asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c"
+          : "=v"(hi)
+          : "v"((uint32_t)(d >> 32)), "v"((uint32_t)(pb >> 32)), "v"(0x80000000u));
+      c[t] = FT<T>::val(((U)hi << 32) | (uint32_t)pb);
     }
-    c[t] = FT<T>::val(FT<T>::bits(FT<T>::val(sel) * alpha) ^ (d & kS));
   }
   // ldpc column pass: forward partial sums from the prior, then backward
   T f[ND];
@@ -339,6 +370,99 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
     st.a = m1 | (px & kS);
     st.b = m2;
     lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
+  }
+  return mism;
+}
+
+// Check phase with a compile-time row width of NCH 16-byte chunks (same
+// contract as r_check).  The next row's chunks and F word are loaded before the
+// current row is reduced, so each thread keeps one row of LDS reads in flight.
+// Double rows reduce on v_max_f64 / v_min_f64 with |x| source modifiers: on
+// non-negative, non-NaN doubles the float order is the bit order and the
+// results are inputs unchanged, i.e. the integer min / second min of |v2c| bits
+// (three instructions per edge instead of three 64-bit compares + six selects).
+template <typename T, bool FIRST, int NCH>
+__device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, int tid, int TB, uint32_t& sbits) {
+  using U = typename FT<T>::U;
+  using VT = typename V16<T>::type;
+  constexpr int NV = V16<T>::N;
+  constexpr U kS = FT<T>::kSign;
+  int mism = 0;
+  int q = 0;
+  const uint32_t rstride = (uint32_t)NCH * 16u;
+  VT cur[NCH];
+  uint32_t fcur = 0;
+  int i = tid;
+  if (i < m) {
+    const VT* row = reinterpret_cast<const VT*>(smem + Ly.v + 16 + (uint32_t)i * rstride);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) cur[c] = row[c];
+    fcur = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
+  }
+  for (; i < m; i += TB, ++q) {
+    VT nxt[NCH];
+    uint32_t fnxt = 0;
+    const int i2 = i + TB;
+    if (i2 < m) {
+      const VT* row = reinterpret_cast<const VT*>(smem + Ly.v + 16 + (uint32_t)i2 * rstride);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) nxt[c] = row[c];
+      fnxt = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i2 + 1));
+    }
+    uint32_t s;
+    if (FIRST) {
+      s = (fcur >> 1) & 1u;
+      sbits |= s << q;
+      lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1)) = 0;  // H x starts at 0; the variable phases keep it current
+    } else {
+      s = (sbits >> q) & 1u;
+      mism |= (int)((fcur ^ s) & 1u);
+    }
+    typename CSEntry<T>::type st;
+    if constexpr (sizeof(U) == 8) {
+      double f1 = FT<T>::val(FT<T>::kSent), f2 = f1;
+      uint32_t px = s ? 0x80000000u : 0u;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          const double x = V16<T>::get(cur[c], k);
+          double t;
+          asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x));
+          asm("v_min_f64 %0, %1, %2" : "=v"(f2) : "v"(f2), "v"(t));
+          asm("v_min_f64 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
+        }
+        uint32_t p;
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96"
+            : "=v"(p)
+            : "v"(px), "v"((uint32_t)(FT<T>::bits(cur[c].x) >> 32)), "v"((uint32_t)(FT<T>::bits(cur[c].y) >> 32)));
+        px = p;
+      }
+      st.a = FT<T>::bits(f1) | ((U)(px & 0x80000000u) << 32);
+      st.b = FT<T>::bits(f2);
+    } else {
+      float f1 = FT<T>::val(FT<T>::kSent), f2 = f1;
+      uint32_t px = s ? kS : 0u;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          const float x = V16<T>::get(cur[c], k);
+          f2 = __builtin_amdgcn_fmed3f(f1, f2, __builtin_fabsf(x));
+          asm("v_min_f32 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
+        }
+        uint32_t p01, p23;
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(p01) : "v"(px), "v"(FT<T>::bits(cur[c].x)), "v"(FT<T>::bits(cur[c].y)));
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(p23) : "v"(p01), "v"(FT<T>::bits(cur[c].z)), "v"(FT<T>::bits(cur[c].w)));
+        px = p23;
+      }
+      st.a = FT<T>::bits(f1) | (px & kS);
+      st.b = FT<T>::bits(f2);
+    }
+    lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) cur[c] = nxt[c];
+    fcur = fnxt;
   }
   return mism;
 }
@@ -496,7 +620,7 @@ __device__ inline int c_check_any(unsigned char* smem, const RLayout& Ly, int m,
 }
 
 // One sector pass over `cn` shots (chunk-relative), one decode in flight.
-template <typename T, int DMAX, int VPL, bool MC, int ENG, int D3K>
+template <typename T, int DMAX, int VPL, bool MC, int ENG, int D3K, int NCH = 0>
 __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned char* smem, const RLayout& Ly,
                        int vslots, int mmax, uint32_t* failmap, unsigned long long* cnt, const SMcArgs* A,
                        const SDecArgs* D, int tid, int TB) {
@@ -599,6 +723,8 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     // ---------------------------------------------------------- first check pass (CS / c2v from priors)
     if constexpr (eng_base(ENG) == 4)
       c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
+    else if constexpr (NCH > 0)
+      r_check_c<T, true, NCH>(smem, Ly, m, tid, TB, sb);
     else
       r_check<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     __syncthreads();
@@ -621,7 +747,10 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         __syncthreads();
         // check state for iteration it + 1 (float: pre-scaled by its alpha)
         const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
-        mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha_next);
+        if constexpr (NCH > 0)
+          mism = r_check_c<T, false, NCH>(smem, Ly, m, tid, TB, sb);
+        else
+          mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha_next);
       }
       if (__any(mism) && (tid & 63) == 0) flags[it & 1] = 1u;
       __syncthreads();
@@ -673,8 +802,8 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   __syncthreads();  // image reused by the next pass
 }
 
-template <typename T, int DMAX, int VPL, int ENG, int D3K>
-__global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
+template <typename T, int DMAX, int VPL, int ENG, int D3K, int LB = kMaxThreadsS, int NCH = 0>
+__global__ __launch_bounds__(LB, lb_waves<T>(LB)) void rmc_kernel(SMcArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = A.chunk;
@@ -705,7 +834,7 @@ __global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
     for (int qi = 0; qi < A.nsec; ++qi) {
       const SSector S = pick_ssector(A, qi);
       const int q = qi == 0 ? A.sec_id0 : A.sec_id1;
-      r_pass<T, DMAX, VPL, true, ENG, D3K>(S, q, c0, cn, smem, Ly, A.vslots, A.mmax, q == 0 ? fm0 : fm1, cnt, &A, nullptr,
+      r_pass<T, DMAX, VPL, true, ENG, D3K, NCH>(S, q, c0, cn, smem, Ly, A.vslots, A.mmax, q == 0 ? fm0 : fm1, cnt, &A, nullptr,
                                  tid, TB);
     }
     // combine the sectors per shot (eval_logical_type, src/Simulators.py:162-168)
@@ -728,8 +857,8 @@ __global__ __launch_bounds__(kMaxThreadsS) void rmc_kernel(SMcArgs A) {
   if (tid < kCntHist && cnt[tid]) atomicAdd(&A.counters[tid], cnt[tid]);
 }
 
-template <typename T, int DMAX, int VPL, int ENG, int D3K>
-__global__ __launch_bounds__(kMaxThreadsS) void rdec_kernel(SDecArgs D) {
+template <typename T, int DMAX, int VPL, int ENG, int D3K, int LB = kMaxThreadsS, int NCH = 0>
+__global__ __launch_bounds__(LB, lb_waves<T>(LB)) void rdec_kernel(SDecArgs D) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = D.chunk;
@@ -745,7 +874,7 @@ __global__ __launch_bounds__(kMaxThreadsS) void rdec_kernel(SDecArgs D) {
   while (ch < nchunks) {
     const long long c0 = ch * CH;
     const int cn = (int)(D.B - c0 < CH ? D.B - c0 : CH);
-    r_pass<T, DMAX, VPL, false, ENG, D3K>(D.sec, 0, c0, cn, smem, Ly, D.vslots, D.mmax, nullptr, nullptr, nullptr, &D, tid,
+    r_pass<T, DMAX, VPL, false, ENG, D3K, NCH>(D.sec, 0, c0, cn, smem, Ly, D.vslots, D.mmax, nullptr, nullptr, nullptr, &D, tid,
                                 TB);
     if (D.work) {  // r_pass ends with a barrier: every thread has read s_next
       if (tid == 0) s_next = (long long)atomicAdd(D.work, 1u);

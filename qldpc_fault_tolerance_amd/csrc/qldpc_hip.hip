@@ -66,8 +66,17 @@ SVariant get_rvariant(int engine, int precision, int vpl, int d3k, int dmax) {
   return precision == 32 ? get_rvariant_f32(vpl, d3k) : get_rvariant_f64(vpl);
 }
 
+// fp64 engine-3 kernels built for <= 256-thread workgroups (engine id 103:
+// 256-VGPR budget, own v2c in VGPRs, compile-time D3K); QLDPC_F64W=0 disables.
+bool use_f64w(int engine, int precision, int dmax, int tb, int vpl, int ea_shift, int nch) {
+  return engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && tb <= 256 && vpl >= 4 && vpl <= 8 &&
+         (nch == 3 || nch == 4) && env_int("QLDPC_F64W", 1) != 0;
+}
+
 // Slot-family kernels of an engine (2, 3 or 4).
-SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0) {
+SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
+                      int nch = 0) {
+  if (use_f64w(engine, precision, dmax, tb, vpl, ea_shift, nch)) return get_rvariant_f64_w(vpl, d3k, nch);
   if (engine == 3 && ea_shift == 2)
     return (precision == 32 && dmax == 4) ? get_rvariant_f32_big(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
   return engine >= 3 ? get_rvariant(engine, precision, vpl, d3k, dmax) : get_svariant(precision, dmax, ns);
@@ -555,9 +564,10 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     const int vbase_dw = (bp->engine == 3 && env_int("QLDPC_BANKOPT", 1) != 0)
                              ? (int)(r_layout(3, vslots2, g->m, tsize).v / 4)
                              : -1;
-    if (precision != 32) bp->d3k = 0;  // fp64 engine-3 kernels are built with D3K = 0 only
+    // fp64 engine-3 kernels are built with D3K = 0 only, except the <= 256-thread family
+    if (precision != 32 && !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch)) bp->d3k = 0;
     build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw);
-    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift).dec_k;
+    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch).dec_k;
   }
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
   if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)bp->VPL * bp->TB * tsize))) return fail(rc);
@@ -717,7 +727,7 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     }
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
-    SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift);
+    SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;
@@ -802,6 +812,9 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   // one kernel serves both sectors: only slots that hold degree <= 3 variables in both skip slot 4
   mc->d3k = std::min(dec_x ? dec_x->d3k : 1 << 20, dec_z ? dec_z->d3k : 1 << 20);
   mc->precision = d0->precision;
+  // compile-time row width (fp64 <= 256-thread family): one kernel serves both sectors
+  mc->nch = d0->nch;
+  if (dec_x && dec_z && dec_x->nch != dec_z->nch) mc->nch = 0;
   mc->mmax = std::max(dec_x ? dec_x->g->m : 0, dec_z ? dec_z->g->m : 0);
   const void* kern;
   if (mc->engine == 1) {
@@ -821,7 +834,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
       mc->NS = choose_ns(mc->img_bytes);
       mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
     }
-    kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift).mc_k;
+    kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch).mc_k;
   }
   if (mc->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB"));
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
@@ -927,7 +940,7 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.fail = d_fail; a.err = d_err; a.corr = d_corr; a.iters = d_iters;
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
-    SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift);
+    SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch);
     QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;

@@ -84,6 +84,7 @@ struct qldpc_mc {
   int engine = 2, TB = 0, VPL = 0, DMAX = 0, NS = 1, precision = 64, lds_bytes = 0, blocks_per_cu = 0, cus = 0;
   int mmax = 0, vslots = 0, img_bytes = 0;
   int d3k = 0;  // engine 3: compile-time degree-3 slot count of the kernel (min over sectors)
+  int nch = 0;  // 16-byte chunks per check row when both sectors agree (else 0)
   int ea_shift = 0;
   // staged pipeline (staged.hip): product-sum decoders, or QLDPC_MC_STAGED=1
   bool staged = false;

@@ -42,6 +42,9 @@ SVariant get_rvariant_f32_big(int vpl, int d3k);  // kern_r_f32_big.hip: images 
 SVariant get_rvariant_f32_d5(int vpl, int d3k);  // kern_r_f32_d56.hip: column degree 5
 SVariant get_rvariant_f32_d6(int vpl, int d3k);  //                      column degree 6
 SVariant get_rvariant_f64(int vpl);
+SVariant get_rvariant_f64_w(int vpl, int d3k, int nch);  // kern_r_f64_w{3,4}.hip: <= 256 threads, own v2c in VGPRs, D3K
+SVariant get_rvariant_f64_w3(int vpl, int d3k);
+SVariant get_rvariant_f64_w4(int vpl, int d3k);
 SVariant get_r4variant_f32(int vpl);
 SVariant get_r4variant_f64(int vpl);
 SVariant get_svariant_f32_d4(int ns);
@@ -109,21 +112,21 @@ SVariant pick_sns(int ns) {
   }
 }
 
-template <typename T, int VPL, int ENG, int D3K, int DM = 4>
+template <typename T, int VPL, int ENG, int D3K, int DM = 4, int LB = kMaxThreadsS, int NCH = 0>
 hipError_t rlaunch_dec(dim3 g, dim3 b, size_t lds, hipStream_t s, const SDecArgs& a) {
-  hipLaunchKernelGGL((rdec_kernel<T, DM, VPL, ENG, D3K>), g, b, lds, s, a);
+  hipLaunchKernelGGL((rdec_kernel<T, DM, VPL, ENG, D3K, LB, NCH>), g, b, lds, s, a);
   return hipGetLastError();
 }
-template <typename T, int VPL, int ENG, int D3K, int DM = 4>
+template <typename T, int VPL, int ENG, int D3K, int DM = 4, int LB = kMaxThreadsS, int NCH = 0>
 hipError_t rlaunch_mc(dim3 g, dim3 b, size_t lds, hipStream_t s, const SMcArgs& a) {
-  hipLaunchKernelGGL((rmc_kernel<T, DM, VPL, ENG, D3K>), g, b, lds, s, a);
+  hipLaunchKernelGGL((rmc_kernel<T, DM, VPL, ENG, D3K, LB, NCH>), g, b, lds, s, a);
   return hipGetLastError();
 }
-template <typename T, int VPL, int ENG, int D3K, int DM = 4>
+template <typename T, int VPL, int ENG, int D3K, int DM = 4, int LB = kMaxThreadsS, int NCH = 0>
 SVariant make_rvariant() {
-  return SVariant{&rlaunch_dec<T, VPL, ENG, D3K, DM>, &rlaunch_mc<T, VPL, ENG, D3K, DM>,
-                  reinterpret_cast<const void*>(&rdec_kernel<T, DM, VPL, ENG, D3K>),
-                  reinterpret_cast<const void*>(&rmc_kernel<T, DM, VPL, ENG, D3K>)};
+  return SVariant{&rlaunch_dec<T, VPL, ENG, D3K, DM, LB, NCH>, &rlaunch_mc<T, VPL, ENG, D3K, DM, LB, NCH>,
+                  reinterpret_cast<const void*>(&rdec_kernel<T, DM, VPL, ENG, D3K, LB, NCH>),
+                  reinterpret_cast<const void*>(&rmc_kernel<T, DM, VPL, ENG, D3K, LB, NCH>)};
 }
 // D3K = 0 only (fp64 and engine 4)
 template <typename T, int ENG>
@@ -141,18 +144,18 @@ SVariant pick_rvpl(int vpl) {
   }
 }
 // every D3K in 0..VPL for one VPL (DM = edge slots per variable: 4, or 5/6 for degree-5/6 columns)
-template <typename T, int VPL, int ENG, int DM = 4>
+template <typename T, int VPL, int ENG, int DM = 4, int LB = kMaxThreadsS, int NCH = 0>
 SVariant pick_rd3k(int d3k) {
   switch (d3k < 0 ? 0 : d3k > VPL ? VPL : d3k) {
-    case 0: return make_rvariant<T, VPL, ENG, 0, DM>();
-    case 1: return make_rvariant<T, VPL, ENG, (1 <= VPL ? 1 : 0), DM>();
-    case 2: return make_rvariant<T, VPL, ENG, (2 <= VPL ? 2 : 0), DM>();
-    case 3: return make_rvariant<T, VPL, ENG, (3 <= VPL ? 3 : 0), DM>();
-    case 4: return make_rvariant<T, VPL, ENG, (4 <= VPL ? 4 : 0), DM>();
-    case 5: return make_rvariant<T, VPL, ENG, (5 <= VPL ? 5 : 0), DM>();
-    case 6: return make_rvariant<T, VPL, ENG, (6 <= VPL ? 6 : 0), DM>();
-    case 7: return make_rvariant<T, VPL, ENG, (7 <= VPL ? 7 : 0), DM>();
-    default: return make_rvariant<T, VPL, ENG, (8 <= VPL ? 8 : 0), DM>();
+    case 0: return make_rvariant<T, VPL, ENG, 0, DM, LB, NCH>();
+    case 1: return make_rvariant<T, VPL, ENG, (1 <= VPL ? 1 : 0), DM, LB, NCH>();
+    case 2: return make_rvariant<T, VPL, ENG, (2 <= VPL ? 2 : 0), DM, LB, NCH>();
+    case 3: return make_rvariant<T, VPL, ENG, (3 <= VPL ? 3 : 0), DM, LB, NCH>();
+    case 4: return make_rvariant<T, VPL, ENG, (4 <= VPL ? 4 : 0), DM, LB, NCH>();
+    case 5: return make_rvariant<T, VPL, ENG, (5 <= VPL ? 5 : 0), DM, LB, NCH>();
+    case 6: return make_rvariant<T, VPL, ENG, (6 <= VPL ? 6 : 0), DM, LB, NCH>();
+    case 7: return make_rvariant<T, VPL, ENG, (7 <= VPL ? 7 : 0), DM, LB, NCH>();
+    default: return make_rvariant<T, VPL, ENG, (8 <= VPL ? 8 : 0), DM, LB, NCH>();
   }
 }
 #endif
