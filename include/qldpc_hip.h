@@ -240,8 +240,16 @@ int qldpc_bp_engine(const qldpc_bp *bp, int32_t *engine);
 
 /* Engine 3: leading variable slots per thread that hold only variables of
  * column degree <= 3 (variables are host-sorted by degree; those slots skip the
- * 4th edge slot at compile time).  0 for the other engines and for fp64. */
+ * 4th edge slot at compile time).  0 for the other engines and for the fp64
+ * kernels of workgroups wider than 256 threads. */
 int qldpc_bp_degree3_slots(const qldpc_bp *bp, int32_t *d3k);
+
+/* Engine 3: extra LDS cycles of one variable-phase pass's CS gathers (summed
+ * over gather instructions and lane groups: distinct checks on one bank beyond
+ * the first) with the identity check order (`before`) and with the labels the
+ * decoder uses (`after`, host-side label search at create time; QLDPC_LABEL=0
+ * disables it).  0 / 0 for the other engines. */
+int qldpc_bp_bank_stats(const qldpc_bp *bp, int32_t *before, int32_t *after);
 
 #ifdef __cplusplus
 }

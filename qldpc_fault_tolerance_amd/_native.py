@@ -23,6 +23,7 @@ EXPORTED = [
     "qldpc_phenl_trace_len", "qldpc_phenl_launch", "qldpc_bp_degree3_slots", "qldpc_bp_create_soft",
     "qldpc_bp_decode_batch_soft", "qldpc_osd_create", "qldpc_osd_destroy", "qldpc_osd_rank",
     "qldpc_osd_decode_batch", "qldpc_osd_gpu_create", "qldpc_osd_gpu_destroy", "qldpc_osd_gpu_decode", "qldpc_phenl_set_final_osd",
+    "qldpc_bp_bank_stats",
 ]
 
 
@@ -114,6 +115,8 @@ def _declare(L):
     L.qldpc_bp_geometry.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 4
     L.qldpc_bp_engine.restype = ctypes.c_int
     L.qldpc_bp_engine.argtypes = [_vp, ctypes.POINTER(_i32)]
+    L.qldpc_bp_bank_stats.restype = ctypes.c_int
+    L.qldpc_bp_bank_stats.argtypes = [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]
     L.qldpc_bp_degree3_slots.restype = ctypes.c_int
     L.qldpc_bp_degree3_slots.argtypes = [_vp, ctypes.POINTER(_i32)]
     L.qldpc_phenl_create.restype = ctypes.c_int

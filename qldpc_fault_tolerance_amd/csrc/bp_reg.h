@@ -44,8 +44,11 @@ constexpr int eng_sh(int E) { return (E / 10) % 10 ? 2 : 0; }
 constexpr bool eng_kv64(int E) { return (E / 100) % 10 != 0; }
 // launch bounds: LB threads per workgroup at most; 256-thread fp64 kernels are
 // built for 2 workgroups per CU (2 waves per SIMD: up to 256 VGPRs, no spills)
-template <typename T>
-constexpr int lb_waves(int LB) { return LB <= 256 ? (sizeof(T) == 8 ? 2 : 4) : 1; }
+template <typename T, int ENG>
+constexpr int lb_waves(int LB) {
+  // engine 4 fp64 images (no CS array) fit 3 workgroups per CU: <= 168 VGPRs
+  return LB <= 256 ? (sizeof(T) == 8 ? (eng_base(ENG) == 4 ? 3 : 2) : 4) : 1;
+}
 template <int ENG>
 __device__ inline uint32_t ea_cs(uint32_t ea) { return (ea & 0xFFFFu) << eng_sh(ENG); }
 template <int ENG>
@@ -688,9 +691,10 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         }
       } else {
         const uint8_t* srow = D->synd + (c0 + sh) * (long long)m;
-        for (int i = tidl; i < m; i += TB) {
+        for (int i = tidl; i < m; i += TB) {  // i = check label (engine 3: S.rperm maps it to the check)
           uint32_t& F = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
-          F = (eng_base(ENG) == 4 ? (F & 0xFFFF0000u) : 0u) | ((uint32_t)(srow[i] & 1u) << 1);
+          const int oi = S.rperm ? S.rperm[i] : i;
+          F = (eng_base(ENG) == 4 ? (F & 0xFFFF0000u) : 0u) | ((uint32_t)(srow[oi] & 1u) << 1);
         }
       }
     }
@@ -803,7 +807,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
 }
 
 template <typename T, int DMAX, int VPL, int ENG, int D3K, int LB = kMaxThreadsS, int NCH = 0>
-__global__ __launch_bounds__(LB, lb_waves<T>(LB)) void rmc_kernel(SMcArgs A) {
+__global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rmc_kernel(SMcArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = A.chunk;
@@ -858,7 +862,7 @@ __global__ __launch_bounds__(LB, lb_waves<T>(LB)) void rmc_kernel(SMcArgs A) {
 }
 
 template <typename T, int DMAX, int VPL, int ENG, int D3K, int LB = kMaxThreadsS, int NCH = 0>
-__global__ __launch_bounds__(LB, lb_waves<T>(LB)) void rdec_kernel(SDecArgs D) {
+__global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rdec_kernel(SDecArgs D) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = D.chunk;

@@ -45,6 +45,7 @@ struct SSector {
   const unsigned long long* lmask;  // [n][kw] logical-row masks per column (MC only)
   const uint8_t* rdeg;              // [m] row degrees (engine 4 only)
   const int32_t* perm;              // [VPL][TB] variable of each slot, -1 = padding (engines 3/4)
+  const int32_t* rperm;             // [m] original check of each check label (engine 3), NULL = identity
   int m, n, kw, max_iter, nch, vpl; // nch = 16-byte chunks per row; vpl = variables per thread
   int d3k;                          // engine 3: slots k < d3k hold variables of degree <= 3 only
   double alpha;                     // 0 => 1 - 2^-iter
@@ -468,6 +469,7 @@ __device__ inline SSector pick_ssector(const SMcArgs& A, int qi) {
   S.lmask = b ? A.sec[1].lmask : A.sec[0].lmask;
   S.rdeg = b ? A.sec[1].rdeg : A.sec[0].rdeg;
   S.perm = b ? A.sec[1].perm : A.sec[0].perm;
+  S.rperm = b ? A.sec[1].rperm : A.sec[0].rperm;
   S.d3k = b ? A.sec[1].d3k : A.sec[0].d3k;
   S.m = b ? A.sec[1].m : A.sec[0].m;
   S.n = b ? A.sec[1].n : A.sec[0].n;

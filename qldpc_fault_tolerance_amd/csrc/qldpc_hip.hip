@@ -77,6 +77,7 @@ bool use_f64w(int engine, int precision, int dmax, int tb, int vpl, int ea_shift
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
                       int nch = 0) {
   if (use_f64w(engine, precision, dmax, tb, vpl, ea_shift, nch)) return get_rvariant_f64_w(vpl, d3k, nch);
+  if (engine == 4 && precision == 64 && tb <= 256 && vpl >= 4) return get_r4variant_f64_w(vpl);
   if (engine == 3 && ea_shift == 2)
     return (precision == 32 && dmax == 4) ? get_rvariant_f32_big(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
   return engine >= 3 ? get_rvariant(engine, precision, vpl, d3k, dmax) : get_svariant(precision, dmax, ns);
@@ -315,13 +316,23 @@ static int upload_llr(qldpc_bp* bp) {
 // wave), to spread its 32 stores over the 32 banks: at most 2 per bank, which
 // ds_write_b32 absorbs for free (MI355X_MICROARCH.md §LDS).  vbase_dw < 0
 // keeps the ascending-column order (engine 4 relies on it).
+//
+// `lab` (engine 3, may be empty = identity) relabels the checks: check i keeps
+// its CS entry at lab[i] + 1 and its row at position lab[i] of V (see
+// label_checks below).  The F words and the check phase follow the labels; the
+// decode path maps syndromes through the inverse permutation (bp->rperm).
 static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
-                             const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1) {
+                             const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1,
+                             const std::vector<int>& lab = {}) {
   const int nv = 16 / tsize;  // messages per 16-byte chunk
   const int rw = nch * nv;
   const int swz_mask = (nch == 2) ? 1 : (nch == 4) ? 3 : 0;
   const int swz_shift = (nch == 2) ? 3 : 2;
-  auto phys = [&](int i, int ls) { return nv + i * rw + ((ls / nv) ^ ((i >> swz_shift) & swz_mask)) * nv + ls % nv; };
+  auto L = [&](int i) { return lab.empty() ? i : lab[i]; };
+  auto phys = [&](int i, int ls) {
+    const int r = L(i);
+    return nv + r * rw + ((ls / nv) ^ ((r >> swz_shift) & swz_mask)) * nv + ls % nv;
+  };
   // logical slot of every edge (CSR order); default = ascending column position
   std::vector<int> lslot(g->nnz);
   for (int i = 0; i < g->m; ++i)
@@ -331,27 +342,32 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
     const int32_t* e = g->col_idx.data() + g->row_ptr[i + 1];
     return (int)(std::lower_bound(b, e, (int32_t)j) - g->col_idx.data());
   };
-  if (vbase_dw >= 0 && tsize == 4 && rw <= 32) {
+  // v2c store instructions: ds_write_b32 (float) = 2 groups of 32 lanes over 32
+  // banks; ds_write_b64 (double) = 4 groups of 16 contiguous lanes, an 8-byte
+  // slot s on bank pair s mod 16 (MI355X_MICROARCH.md §LDS)
+  const int sg = tsize == 4 ? 32 : 16, nb = tsize == 4 ? 32 : 16;
+  const int vbase_u = vbase_dw < 0 ? 0 : (tsize == 4 ? vbase_dw : vbase_dw / 2);
+  if (vbase_dw >= 0 && rw <= 32) {
     std::vector<uint32_t> used(g->m, 0u);
     for (int k = 0; k < VPL; ++k)
       for (int d = 0; d < DM; ++d)
-        for (int h0 = 0; h0 < TB; h0 += 32) {
+        for (int h0 = 0; h0 < TB; h0 += sg) {
           int cnt[32] = {0};
-          for (int t = h0; t < h0 + 32 && t < TB; ++t) {
+          for (int t = h0; t < h0 + sg && t < TB; ++t) {
             const int j = slot_var[(size_t)k * TB + t];
             if (j < 0 || d >= (int)g->col_rows[j].size()) continue;
             const int i = g->col_rows[j][d];
             int best = -1, bc = 1 << 30;
             for (int ls = 0; ls < rw; ++ls) {
               if ((used[i] >> ls) & 1u) continue;
-              const int c = cnt[(vbase_dw + phys(i, ls)) & 31];
+              const int c = cnt[(vbase_u + phys(i, ls)) % nb];
               if (c < bc) {
                 bc = c;
                 best = ls;
               }
             }
             used[i] |= 1u << best;
-            cnt[(vbase_dw + phys(i, best)) & 31]++;
+            cnt[(vbase_u + phys(i, best)) % nb]++;
             lslot[edge_of(i, j)] = best;
           }
         }
@@ -365,9 +381,149 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
       for (int d = 0; d < (int)rows.size(); ++d) {
         const int i = rows[d];
         const int slot = phys(i, lslot[edge_of(i, j)]);
-        out[((size_t)k * DM + d) * TB + t] = (uint32_t)(i + 1) | ((uint32_t)slot << 16);
+        out[((size_t)k * DM + d) * TB + t] = (uint32_t)(L(i) + 1) | ((uint32_t)slot << 16);
       }
     }
+}
+
+// Engine-3 check labelling against LDS bank conflicts.  The variable phase
+// gathers CS[lab[i] + 1] for the d-th check of each lane's variable: one
+// ds_read_b64 (float: 8-byte entries, 2 groups of 32 lanes, bank pair = entry
+// mod 32) or ds_read_b128 (double: 16-byte entries, the 4 lane groups of 16 of
+// MI355X_MICROARCH.md §LDS, bank quad = entry mod 16) per (slot k, edge d).
+// Distinct checks of one lane group that share a colour (entry mod NC) cost an
+// extra LDS cycle each (one check gathered by several lanes broadcasts).  The
+// labels are a permutation; a seeded local search swaps the labels of two
+// checks whenever that does not increase Σ_groups Σ_colours count² (= the group
+// size exactly when every group is conflict free).  For double it also balances
+// each 16-lane v2c store group over the two row-label parities (ds_write_b64:
+// a row of 8 slots covers half of the 16 bank pairs), so build_slot_edges's
+// in-row placement can make the stores conflict free too.  Pure host work, done
+// once per decoder; the arithmetic is untouched (labels only move storage).
+static std::vector<int> label_checks(const qldpc_graph* g, const std::vector<int32_t>& slot_var, int TB, int VPL,
+                                     int DM, int tsize, int* cost_before = nullptr, int* cost_after = nullptr) {
+  const int m = g->m;
+  std::vector<int> lab(m);
+  for (int i = 0; i < m; ++i) lab[i] = i;
+  if (m < 2) return lab;
+  const int NC = tsize == 4 ? 32 : 16;
+  static const int kB128[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                   {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                   {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                   {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+  // groups (gather groups first, then double's store groups), as check lists
+  std::vector<int> gs{0}, gm;
+  std::vector<char> gstore;
+  auto add_group = [&](int k, int d, int w, const int* lanes, int nl, bool store) {
+    const size_t start = gm.size();
+    for (int q = 0; q < nl; ++q) {
+      const int t = w * 64 + lanes[q];
+      if (t >= TB) continue;
+      const int j = slot_var[(size_t)k * TB + t];
+      if (j < 0 || d >= (int)g->col_rows[j].size()) continue;
+      const int i = g->col_rows[j][d];
+      if (std::find(gm.begin() + start, gm.end(), i) == gm.end()) gm.push_back(i);
+    }
+    if (gm.size() - start >= 2) {
+      gs.push_back((int)gm.size());
+      gstore.push_back(store ? 1 : 0);
+    } else {
+      gm.resize(start);
+    }
+  };
+  int lanes32[2][32], lanes16[4][16];
+  for (int q = 0; q < 64; ++q) {
+    lanes32[q / 32][q % 32] = q;
+    lanes16[q / 16][q % 16] = q;
+  }
+  for (int k = 0; k < VPL; ++k)
+    for (int d = 0; d < DM; ++d)
+      for (int w = 0; w * 64 < TB; ++w) {
+        if (tsize == 4) {
+          for (int h = 0; h < 2; ++h) add_group(k, d, w, lanes32[h], 32, false);
+        } else {
+          for (int h = 0; h < 4; ++h) add_group(k, d, w, kB128[h], 16, false);
+          for (int h = 0; h < 4; ++h) add_group(k, d, w, lanes16[h], 16, true);
+        }
+      }
+  const int ng = (int)gstore.size();
+  if (ng == 0) return lab;
+  std::vector<std::vector<int>> of(m);  // groups of each check
+  for (int q = 0; q < ng; ++q)
+    for (int e = gs[q]; e < gs[q + 1]; ++e) of[gm[e]].push_back(q);
+  // colour of a label in a group: gathers (label + 1) mod NC, stores the row parity
+  auto col = [&](int q, int l) { return gstore[q] ? (l & 1) : (l + 1) % NC; };
+  const int W = 32;
+  // weights of the two kinds of groups in the objective (double: the stores
+  // conflict far more than the gathers of structured codes)
+  const int wg = env_int("QLDPC_LABEL_WG", tsize == 4 ? 1 : 1), ws = env_int("QLDPC_LABEL_WS", 4);
+  std::vector<int> gw(ng);
+  for (int q = 0; q < ng; ++q) gw[q] = gstore[q] ? ws : wg;
+  std::vector<int> cnt((size_t)ng * W, 0);
+  long long cost = 0;
+  for (int q = 0; q < ng; ++q)
+    for (int e = gs[q]; e < gs[q + 1]; ++e) {
+      int& c = cnt[(size_t)q * W + col(q, lab[gm[e]])];
+      cost += (long long)gw[q] * (2 * c + 1);
+      ++c;
+    }
+  auto conflicts = [&]() {  // extra gather cycles: Σ (max count - 1) over gather groups
+    int tot = 0;
+    for (int q = 0; q < ng; ++q) {
+      if (gstore[q]) continue;
+      int mx = 0;
+      for (int c = 0; c < W; ++c) mx = std::max(mx, cnt[(size_t)q * W + c]);
+      tot += mx - 1;
+    }
+    return tot;
+  };
+  if (cost_before) *cost_before = conflicts();
+  uint64_t rs = 0x9E3779B97F4A7C15ull ^ (uint64_t)m * 0x100000001B3ull;
+  auto rnd = [&]() {
+    rs ^= rs << 13;
+    rs ^= rs >> 7;
+    rs ^= rs << 17;
+    return rs;
+  };
+  const long long iters = std::min<long long>(4000000LL, (long long)m * env_int("QLDPC_LABEL_IT", 600));
+  for (long long it = 0; it < iters; ++it) {
+    const int a = (int)(rnd() % (uint64_t)m), b = (int)(rnd() % (uint64_t)m);
+    if (a == b) continue;
+    const int la = lab[a], lb = lab[b];
+    // delta of Σ count² when a takes label lb and b takes la
+    long long delta = 0;
+    auto move = [&](int q, int from, int to) {
+      const int cf = col(q, from), ct = col(q, to);
+      if (cf == ct) return;
+      int& x = cnt[(size_t)q * W + cf];
+      int& y = cnt[(size_t)q * W + ct];
+      delta += (long long)gw[q] * ((2 * y + 1) - (2 * x - 1));
+      --x;
+      ++y;
+    };
+    for (int q : of[a]) move(q, la, lb);
+    for (int q : of[b]) move(q, lb, la);
+    if (delta <= 0 && (delta < 0 || (rnd() & 3) == 0)) {
+      lab[a] = lb;
+      lab[b] = la;
+      cost += delta;
+    } else {  // undo (reverse order)
+      for (int q : of[b]) {
+        const int cf = col(q, lb), ct = col(q, la);
+        if (cf == ct) continue;
+        ++cnt[(size_t)q * W + cf];
+        --cnt[(size_t)q * W + ct];
+      }
+      for (int q : of[a]) {
+        const int cf = col(q, la), ct = col(q, lb);
+        if (cf == ct) continue;
+        ++cnt[(size_t)q * W + cf];
+        --cnt[(size_t)q * W + ct];
+      }
+    }
+  }
+  if (cost_after) *cost_after = conflicts();
+  return lab;
 }
 
 // Engine 5 (product-sum): the row-ordered / column-ordered products need the
@@ -472,6 +628,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     bp->llr.release();
     bp->rdeg.release();
     bp->perm.release();
+    bp->rperm.release();
     delete bp;
     return code;
   };
@@ -566,7 +723,18 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
                              : -1;
     // fp64 engine-3 kernels are built with D3K = 0 only, except the <= 256-thread family
     if (precision != 32 && !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch)) bp->d3k = 0;
-    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw);
+    std::vector<int> lab;
+    // fp64 (measured +3 % with the bank-aware fp64 v2c placement); fp32 gathers of the
+    // structured codes are already near conflict-free (QLDPC_LABEL=1 forces it on)
+    if (bp->engine == 3 && env_int("QLDPC_LABEL", precision == 64 ? 1 : 0) != 0) {
+      lab = label_checks(g, bp->slot_var, bp->TB, bp->VPL, DM, tsize, &bp->gather_conf[0], &bp->gather_conf[1]);
+      std::vector<int32_t> inv(g->m);
+      for (int i = 0; i < g->m; ++i) inv[lab[i]] = i;
+      if ((rc = bp->rperm.alloc((size_t)std::max(1, g->m) * 4))) return fail(rc);
+      if (g->m && hipMemcpy(bp->rperm.p, inv.data(), (size_t)g->m * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(set_err(QLDPC_EHIP, "upload check labels"));
+    }
+    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab);
     kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch).dec_k;
   }
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
@@ -596,7 +764,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
 
 int qldpc_bp_destroy(qldpc_bp* bp) {
   if (!bp) return 0;
-  for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->work, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp,
+  for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->rperm, &bp->work, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp,
                     &bp->ps_ce, &bp->ps_ws})
     d->release();
   delete bp;
@@ -612,6 +780,13 @@ int qldpc_bp_set_channel_probs(qldpc_bp* bp, const double* channel_probs) {
 int qldpc_bp_degree3_slots(const qldpc_bp* bp, int32_t* d3k) {
   if (!bp || !d3k) return set_err(QLDPC_EINVAL, "NULL argument");
   *d3k = bp->engine == 3 ? bp->d3k : 0;
+  return 0;
+}
+
+int qldpc_bp_bank_stats(const qldpc_bp* bp, int32_t* before, int32_t* after) {
+  if (!bp) return set_err(QLDPC_EINVAL, "NULL decoder");
+  if (before) *before = bp->gather_conf[0];
+  if (after) *after = bp->gather_conf[1];
   return 0;
 }
 
@@ -651,6 +826,7 @@ static SSector ssector_of(const qldpc_bp* bp, const unsigned long long* lmask, i
   s.lmask = lmask;
   s.rdeg = static_cast<const uint8_t*>(bp->rdeg.p);
   s.perm = static_cast<const int32_t*>(bp->perm.p);
+  s.rperm = static_cast<const int32_t*>(bp->rperm.p);
   s.d3k = bp->d3k;
   s.m = bp->g->m;
   s.n = bp->g->n;

@@ -68,6 +68,8 @@ struct qldpc_bp {
   // degree <= 3 variables first so that slots k < d3k skip the 4th edge slot.
   std::vector<int32_t> slot_var;
   qldpc_rt::DevBuf perm;
+  qldpc_rt::DevBuf rperm;  // engine 3: original check of each check label (label_checks)
+  int gather_conf[2] = {0, 0};  // engine 3: extra gather cycles per pass before / after labelling
   int d3k = 0;
   int ea_shift = 0;  // engine 3: 2 = dword-scaled LDS addresses in the edge words (images > 64 KiB)
   // engine 5 (product-sum, bp_ps.hip): CSR / CSC on the device, optional HBM message workspace

@@ -47,6 +47,7 @@ SVariant get_rvariant_f64_w3(int vpl, int d3k);
 SVariant get_rvariant_f64_w4(int vpl, int d3k);
 SVariant get_r4variant_f32(int vpl);
 SVariant get_r4variant_f64(int vpl);
+SVariant get_r4variant_f64_w(int vpl);  // <= 256 threads
 SVariant get_svariant_f32_d4(int ns);
 SVariant get_svariant_f32_d8(int ns);
 SVariant get_svariant_f64_d4(int ns);

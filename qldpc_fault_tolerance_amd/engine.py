@@ -120,6 +120,10 @@ class DeviceBP:
         d = ctypes.c_int32()
         _native.check(_native.lib().qldpc_bp_degree3_slots(self.handle, ctypes.byref(d)), "bp_degree3_slots")
         g["degree3_slots"] = d.value
+        b0, b1 = ctypes.c_int32(), ctypes.c_int32()
+        _native.check(_native.lib().qldpc_bp_bank_stats(self.handle, ctypes.byref(b0), ctypes.byref(b1)),
+                      "bp_bank_stats")
+        g["gather_conflicts"] = (b0.value, b1.value)
         return g
 
     def decode_batch_device(self, synd_dev, corr_dev, iters_dev=None, conv_dev=None, stream=None):
