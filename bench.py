@@ -46,7 +46,12 @@ def parse():
     ap.add_argument("--code", default="hgp_34_n1600")
     ap.add_argument("--p", type=float, default=DEFAULT_P)
     ap.add_argument("--shots", type=int, default=1 << 18, help="shots per GPU per step")
-    ap.add_argument("--precision", type=int, default=32, choices=(32, 64))
+    ap.add_argument("--precision", type=int, default=64, choices=(32, 64),
+                    help="64 = ldpc's float64 arithmetic (the reference; headline), 32 = fast mode (not the reference)")
+    ap.add_argument("--fp32-line", type=int, default=1,
+                    help="also time the fp32 fast mode on the same workload (reported beside the headline, N=1)")
+    ap.add_argument("--pmc-traffic", type=int, default=1,
+                    help="measure HBM bytes per launch with rocprofv3 PMC passes of this build (N=1, before GPU init)")
     ap.add_argument("--max-iter-ratio", type=float, default=10)
     ap.add_argument("--logical", default="Total", choices=("X", "Z", "Total"))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
@@ -105,15 +110,73 @@ def kernel_name(dec):
     return f"qldpc::smc_kernel<{t}, {dmax}, 1> (engine {g['engine']})"
 
 
-def measured_traffic(code, p, shots, logical, precision):
-    """HBM bytes per launch measured by rocprofv3 PMC passes for this exact config (profiles/traffic.json)."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
-            t = json.load(f)
-    except (OSError, ValueError):
+def pmc_traffic(a):
+    """HBM bytes per launch of the headline kernel, measured now on this build and config.
+
+    Two rocprofv3 ``--pmc`` passes (FETCH_SIZE, WRITE_SIZE: separate runs, as gfx950 needs) over
+    ``tools/prof_one.py``, which builds the same decoders and issues ONE launch of the same
+    workload (code, p, shots, both sectors, precision, seed).  Runs as child processes BEFORE this
+    process touches the GPU.  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE x2,
+    WRITE_SIZE as is; KB = 1024 B.  Returns a dict (bytes per launch, raw counters) or None.
+    """
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
         return None
-    e = t.get(f"{code}|{p}|{shots}|{logical}|{precision}")
-    return e["bytes"] if e else None
+    out = {}
+    with tempfile.TemporaryDirectory(prefix="qldpc_pmc_", dir="/tmp") as td:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(td, counter)
+            cmd = ["timeout", "-s", "KILL", "120", prof, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "p",
+                   "--", sys.executable, os.path.join(ROOT, "tools", "prof_one.py"), a.code, str(a.p), str(a.shots), "0",
+                   str(a.precision), a.logical, str(SEED), str(a.max_iter_ratio)]
+            try:
+                r = subprocess.run(cmd, cwd="/tmp", stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=150,
+                                   env=dict(os.environ, TMPDIR="/tmp"))
+            except (OSError, subprocess.SubprocessError):
+                return None
+            if r.returncode != 0:
+                return None
+            vals, kern = [], None
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for row in csv.DictReader(open(f)):
+                    if "mc_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                        vals.append(float(row["Counter_Value"]))
+                        kern = row["Kernel_Name"]
+            if len(vals) != 1:
+                return None
+            out[counter] = vals[0]
+            out["kernel"] = kern
+    fetch_b = out["FETCH_SIZE"] * 2 * 1024
+    write_b = out["WRITE_SIZE"] * 1024
+    return {"bytes": int(fetch_b + write_b), "fetch_bytes_x2": int(fetch_b), "write_bytes": int(write_b),
+            "fetch_size_kb_raw": out["FETCH_SIZE"], "write_size_kb_raw": out["WRITE_SIZE"], "kernel": out["kernel"],
+            "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate runs) over tools/prof_one.py: one launch of this "
+                   "workload; FETCH_SIZE x2 (gfx950), KB = 1024 B"}
+
+
+def spawn_ranks(n):
+    """``bench.py --gpus N`` without torchrun: N child ranks, one per GPU, started before this
+    process touches any GPU (no exec from a GPU process); rank 0's JSON line is the output."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
 
 
 def phenl_main(a, torch, dist, world, rank, dev):
@@ -255,10 +318,15 @@ def bposd_main(a, torch, dist, world, rank, dev):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    traffic = None
+    if a.workload == "data" and world == 1 and a.pmc_traffic:
+        traffic = pmc_traffic(a)  # child processes, before this process initialises the GPU
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; QLDPC_SHARE_GPU=1 lets ranks share the visible GPUs (multi-rank rehearsal on a
@@ -279,6 +347,77 @@ def main():
         return bposd_main(a, torch, dist, world, rank, dev)
 
     from qldpc_fault_tolerance_amd import codes
+
+    code = codes.get_code(a.code)
+    r = time_data(a, a.precision, torch, dist, world, rank, dev)
+    n = code.N
+    max_iter = int(n / a.max_iter_ratio)
+    p = a.p
+    E = int(code.hz.sum())
+    mh, nh = code.hz.shape
+    # SURVEY.md §8d algorithmic bytes: 16 B (fp32) / 32 B (fp64) per edge-iteration of two-phase
+    # flooding + per decode ceil(m/8)+ceil(n/8)+16 B of syndrome / decision / counters.
+    bpe = 16 if a.precision == 32 else 32
+    bytes_per_launch = (bpe * E * r["iters"] + r["decodes"] * ((mh + 7) // 8 + (nh + 7) // 8 + 16)) / (a.steps * world)
+    achieved = bytes_per_launch / (r["kern_ms"] * 1e-3) / 1e9
+    tb = traffic["bytes"] if traffic else None
+    out = {
+        "metric": "BP-decoded shots/sec (node) on hgp_34_n1600 + % of HBM/LDS roofline",
+        "value": r["value"],
+        "unit": "shots/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": r["elapsed"] / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if a.precision == 32 else "f64",
+        "data": "synthetic: Philox-sampled depolarizing errors on the synthesized [[1600,64]] HGP stand-in "
+                "(the reference's hgp_34_n1600.pkl is missing; DESIGN.md)",
+        "config": {"workload": f"{a.code} code-capacity BP shot loop, eval_p={p}, min-sum alpha=0.625, "
+                               f"max_iter={max_iter}, eval_logical_type={a.logical}, "
+                               + ("float64 messages = ldpc's arithmetic" if a.precision == 64 else
+                                  "float32 fast mode (NOT the reference arithmetic)"),
+                   "code": a.code, "p": p, "shots_per_gpu_step": a.shots, "max_iter": max_iter,
+                   "decodes_per_shot": int(a.logical != "Z") + int(a.logical != "X"),
+                   "parallelism": f"shot-sharded x{world}"},
+        "decodes_per_s": r["decodes"] / r["elapsed"],
+        "mean_iters_per_decode": r["iters"] / max(r["decodes"], 1),
+        "nonconverged_frac": r["nonconv"] / max(r["decodes"], 1),
+        "logical_error_rate": r["failures"] / max(r["shots"], 1),
+        "roofline": {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / LDS_PEAK_GBS, "traffic": tb,
+                     "kernel": r["kernel"], "kernel_ms": r["kern_ms"],
+                     "bytes_per_launch": bytes_per_launch,
+                     # HBM carries only the edge tables (L2-resident) and the counters
+                     "hbm": {"achieved": (tb / (r["kern_ms"] * 1e-3) / 1e9) if tb else None,
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "pmc": traffic}},
+    }
+    if world == 1 and a.precision == 64 and a.fp32_line:
+        # fp32 fast mode on the same workload: reported beside the headline, never as `value`
+        r32 = time_data(a, 32, torch, dist, world, rank, dev)
+        out["fp32_fast_mode"] = {
+            "value": r32["value"], "unit": "shots/s", "ms_per_step": r32["elapsed"] / a.steps * 1e3,
+            "kernel": r32["kernel"], "kernel_ms": r32["kern_ms"],
+            "roofline_frac": (16 * E * r32["iters"] / a.steps + r32["decodes"] / a.steps * ((mh + 7) // 8 + (nh + 7) // 8 + 16))
+            / (r32["kern_ms"] * 1e-3) / 1e9 / LDS_PEAK_GBS,
+            "logical_error_rate": r32["failures"] / max(r32["shots"], 1),
+            "note": "float32 messages: NOT ldpc's float64 arithmetic (decoded-vector agreement with fp64 is "
+                    "measured in tests/test_gpu_agreement.py)"}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(code, p, max_iter, a.logical, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def time_data(a, precision, torch, dist, world, rank, dev):
+    """BASELINE config 2: W warmup launches, then K timed launches of ``--shots`` shots per GPU
+    bracketed by barrier + synchronize, max over ranks; HIP events on the launch stream time the
+    kernel.  Returns the all-reduced counters and the timings."""
+    from qldpc_fault_tolerance_amd import codes
     from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceMC
 
     code = codes.get_code(a.code)
@@ -289,11 +428,11 @@ def main():
     need_x, need_z = a.logical != "Z", a.logical != "X"
     # decoders as EvalWER builds them: p_data = eval_p on hz (X errors) and hx (Z errors)
     dx = DeviceBP(code.hz, p * np.ones(n), max_iter=max_iter, bp_method="minimum_sum", ms_scaling_factor=0.625,
-                  precision=a.precision, device=dev.index) if need_x else None
+                  precision=precision, device=dev.index) if need_x else None
     # the Z-sector decoder takes the X sector's geometry (one fused kernel serves both)
     vpl = dx.geometry()["vars_per_thread"] if dx is not None and not os.environ.get("QLDPC_TB") else 0
     dz = DeviceBP(code.hx, p * np.ones(n), max_iter=max_iter, bp_method="minimum_sum", ms_scaling_factor=0.625,
-                  precision=a.precision, device=dev.index, vars_per_thread=vpl) if need_z else None
+                  precision=precision, device=dev.index, vars_per_thread=vpl) if need_z else None
     mc = DeviceMC(code, dx, dz)
     S = int(a.shots)
     stream = torch.cuda.current_stream(dev)
@@ -330,59 +469,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-
     w = cnt.cpu().numpy()
     shots = int(w[0])
     if shots != S * a.steps * world:
         raise RuntimeError(f"counter mismatch: {shots} shots != {S} x {a.steps} x {world}")
-    decodes = int(w[2] + w[3])
-    iters = int(w[4] + w[5])
-    nonconv = int(w[6] + w[7])
-    E = int(code.hz.sum())
-    mh, nh = code.hz.shape
-    # SURVEY.md §8d algorithmic bytes: 16 B (fp32) / 32 B (fp64) per edge-iteration of two-phase
-    # flooding + per decode ceil(m/8)+ceil(n/8)+16 B of syndrome / decision / counters.
-    bpe = 16 if a.precision == 32 else 32
-    bytes_per_launch = (bpe * E * iters + decodes * ((mh + 7) // 8 + (nh + 7) // 8 + 16)) / (a.steps * world)
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = measured_traffic(a.code, p, S, a.logical, a.precision)
-    value = shots / elapsed
-    out = {
-        "metric": "BP-decoded shots/sec (node) on hgp_34_n1600 + % of HBM/LDS roofline",
-        "value": value,
-        "unit": "shots/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": elapsed / a.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32" if a.precision == 32 else "f64",
-        "data": "synthetic: Philox-sampled depolarizing errors on the synthesized [[1600,64]] HGP stand-in "
-                "(the reference's hgp_34_n1600.pkl is missing; DESIGN.md)",
-        "config": {"workload": f"{a.code} code-capacity BP shot loop, eval_p={p}, min-sum alpha=0.625, "
-                               f"max_iter={max_iter}, eval_logical_type={a.logical}",
-                   "code": a.code, "p": p, "shots_per_gpu_step": S, "max_iter": max_iter,
-                   "decodes_per_shot": int(need_x) + int(need_z), "parallelism": f"shot-sharded x{world}"},
-        "decodes_per_s": decodes / elapsed,
-        "mean_iters_per_decode": iters / max(decodes, 1),
-        "nonconverged_frac": nonconv / max(decodes, 1),
-        "logical_error_rate": int(w[1]) / max(shots, 1),
-        "roofline": {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / LDS_PEAK_GBS, "traffic": traffic,
-                     "kernel": kernel_name(dx or dz), "kernel_ms": kern_ms,
-                     "bytes_per_launch": bytes_per_launch,
-                     # HBM carries only the edge tables (L2-resident) and the counters
-                     "hbm": {"achieved": (traffic / (kern_ms * 1e-3) / 1e9) if traffic else None,
-                             "peak": HBM_PEAK_GBS, "unit": "GB/s"}},
-    }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(code, p, max_iter, a.logical, a.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    return {"value": shots / elapsed, "elapsed": elapsed, "kern_ms": kern_ms, "shots": shots, "failures": int(w[1]),
+            "decodes": int(w[2] + w[3]), "iters": int(w[4] + w[5]), "nonconv": int(w[6] + w[7]),
+            "kernel": kernel_name(dx or dz)}
 
 
 if __name__ == "__main__":

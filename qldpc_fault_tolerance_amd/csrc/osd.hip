@@ -613,6 +613,13 @@ struct qldpc_osd_gpu {
   qldpc_rt::DevBuf rp, ci, ws, iws;
 };
 
+namespace qldpc_rt {
+// true when the GPU OSD handle was built on exactly this graph (shape and edges)
+bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g) {
+  return o && g && o->host.m == g->m && o->host.n == g->n && o->host.col_rows == g->col_rows;
+}
+}  // namespace qldpc_rt
+
 extern "C" {
 
 int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int32_t osd_method, int32_t osd_order,

@@ -104,6 +104,9 @@ const void* ps_kernel(int precision);
 int ps_decode_launch(const qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int32_t* iters, uint8_t* conv, int64_t B,
                      hipStream_t stream);
 
+// GPU OSD handle built on this graph? (osd.hip; qldpc_phenl_set_final_osd checks it)
+bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g);
+
 // staged data-error shot loop (staged.hip): bit-sliced sampling / syndromes /
 // checks around qldpc_bp_decode_batch, for decoders the fused kernels do not serve
 int staged_mc_prepare(qldpc_mc* mc, const qldpc_graph* logical_x, const qldpc_graph* logical_z);

@@ -362,6 +362,10 @@ int qldpc_phenl_set_final_osd(qldpc_phenl* P, qldpc_osd_gpu* osd_x, qldpc_osd_gp
     int32_t eng = 0;
     qldpc_bp_engine(P->d2[q], &eng);
     if (eng != 1) return set_err(QLDPC_ENOTSUP, "BP+OSD final round needs dec2 from qldpc_bp_create_soft");
+    // the OSD stage reads dec2's syndromes (row stride m) and eliminates its H: same graph only
+    if (!osd_gpu_matches(o[q], P->d2[q]->g))
+      return set_err(QLDPC_EINVAL, q == 0 ? "X-sector OSD handle was built on a different graph than dec2_x"
+                                          : "Z-sector OSD handle was built on a different graph than dec2_z");
   }
   if ((osd_x || osd_z) && !P->post.p) {
     QLDPC_HIP(hipSetDevice(P->device));

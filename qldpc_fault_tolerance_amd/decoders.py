@@ -5,7 +5,9 @@ Mirrors ``src/Decoders.py`` and the space-time part of
 ``ldpc.bp_decoder`` (``src/Decoders.py:77-90``), these classes wrap the MI355X
 BP engine (:class:`engine.DeviceBP`): same constructor arguments, same
 ``decode(synd) -> ndarray[int]`` contract, plus ``decode_batch`` for many
-syndromes per launch.  ``DecoderClass.GetDecoder(params)`` keeps the reference's
+syndromes per launch.  ``device=None`` (the default everywhere) resolves to this
+process's GPU: ``LOCAL_RANK`` under ``torch.distributed.run`` (one rank per GPU),
+else 0 (:func:`.parallel.local_device_index`).  ``DecoderClass.GetDecoder(params)`` keeps the reference's
 dict keys and assertions (``:94-172``; ``src/Decoders_SpaceTime.py:227-257``).
 
 BP+OSD (``BPOSD_Decoder``): GPU BP with soft output, then
@@ -31,7 +33,7 @@ class BPDecoder:
     """``BPDecoder(h, channel_probs, max_iter, bp_method, ms_scaling_factor)`` (``src/Decoders.py:77-90``)."""
 
     def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, precision: int = 64,
-                 device: int = 0, vars_per_thread: int = 0):
+                 device: int | None = None, vars_per_thread: int = 0):
         from .engine import DeviceBP
 
         self.h = h
@@ -61,7 +63,7 @@ class FirstMinBPDecoder:
     """Repeated one-iteration BP while the syndrome weight does not grow (``src/Decoders.py:49-74``)."""
 
     def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, precision: int = 64,
-                 device: int = 0):
+                 device: int | None = None):
         self.h = np.asarray(h)
         self.max_iter = max_iter
         self._bp = BPDecoder(h, channel_probs, 1, bp_method, ms_scaling_factor, precision=precision, device=device)
@@ -105,7 +107,7 @@ class BPOSD_Decoder:
     """
 
     def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, osd_method, osd_order,
-                 precision: int = 64, device: int = 0, osd_threads: int = 0, use_gpu_osd: bool = True):
+                 precision: int = 64, device: int | None = None, osd_threads: int = 0, use_gpu_osd: bool = True):
         from .engine import DeviceBP, DeviceOSD, HostOSD
 
         self.h = h
@@ -160,7 +162,7 @@ class BP_Decoder_Class(DecoderClass):
     """``src/Decoders.py:141-172``: factory keyed by ``{'h', 'p_data'[, 'p_syndrome']}``."""
 
     def __init__(self, max_iter_ratio: int, bp_method: str, ms_scaling_factor: float, precision: int = 64,
-                 device: int = 0):
+                 device: int | None = None):
         self.decoder_default_params = {"max_iter_ratio": max_iter_ratio, "bp_method": bp_method,
                                        "ms_scaling_factor": ms_scaling_factor}
         self.precision = precision
@@ -193,7 +195,7 @@ class BPOSD_Decoder_Class(DecoderClass):
     """``src/Decoders.py:100-138``: BP+OSD factory keyed like :class:`BP_Decoder_Class`."""
 
     def __init__(self, max_iter_ratio: int, bp_method: str, ms_scaling_factor: float, osd_method: str,
-                 osd_order: int, precision: int = 64, device: int = 0):
+                 osd_order: int, precision: int = 64, device: int | None = None):
         self.decoder_default_params = {"max_iter_ratio": max_iter_ratio, "bp_method": bp_method,
                                        "ms_scaling_factor": ms_scaling_factor, "osd_method": osd_method,
                                        "osd_order": osd_order}
@@ -232,7 +234,7 @@ class ST_BP_Decoder_syndrome:
     """BP on the stacked space-time graph (``src/Decoders_SpaceTime.py:200-223``)."""
 
     def __init__(self, h, p_data: float, p_synd: float, max_iter: int, bp_method: str, ms_scaling_factor,
-                 num_rep: int, precision: int = 64, device: int = 0):
+                 num_rep: int, precision: int = 64, device: int | None = None):
         from .engine import DeviceBP
 
         H = np.asarray(h)
@@ -267,7 +269,7 @@ class ST_BP_Decoder_Class(DecoderClass):
     """``src/Decoders_SpaceTime.py:227-257`` (keeps quirk Q4: p_synd = p_data when p_syndrome is given)."""
 
     def __init__(self, max_iter_ratio: int, bp_method: str, ms_scaling_factor: float, precision: int = 64,
-                 device: int = 0):
+                 device: int | None = None):
         self.decoder_default_params = {"max_iter_ratio": max_iter_ratio, "bp_method": bp_method,
                                        "ms_scaling_factor": ms_scaling_factor}
         self.precision = precision

@@ -42,8 +42,12 @@ def bp_method_code(bp_method) -> int:
 class DeviceGraph:
     """A parity-check matrix uploaded once (``qldpc_graph_create``)."""
 
-    def __init__(self, H, device: int = 0):
+    def __init__(self, H, device: int | None = None):
         c = H if isinstance(H, CSR) else CSR.from_dense(H)
+        if device is None:  # this rank's GPU (LOCAL_RANK under torch.distributed.run)
+            from .parallel import local_device_index
+
+            device = local_device_index()
         self.csr = c
         self.m, self.n = c.m, c.n
         self.device = device
@@ -72,7 +76,7 @@ class DeviceBP:
     """``ldpc.bp_decoder`` equivalent on the GPU (``qldpc_bp_create``)."""
 
     def __init__(self, H, channel_probs, max_iter: int = 0, bp_method="minimum_sum", ms_scaling_factor=0.625,
-                 precision: int = 64, vars_per_thread: int = 0, device: int = 0, graph: DeviceGraph | None = None,
+                 precision: int = 64, vars_per_thread: int = 0, device: int | None = None, graph: DeviceGraph | None = None,
                  min_col_slots: int = 0, soft: bool = False):
         self.graph = graph if graph is not None else DeviceGraph(H, device=device)
         n = self.graph.n

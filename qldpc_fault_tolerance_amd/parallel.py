@@ -51,5 +51,11 @@ def allreduce_counters(counters):
 
 
 def local_device_index() -> int:
-    """This rank's GPU (LOCAL_RANK from torch.distributed.run, else 0)."""
-    return int(os.environ.get("LOCAL_RANK", "0"))
+    """This rank's GPU: LOCAL_RANK from torch.distributed.run (else 0), modulo the visible
+    device count when ``QLDPC_SHARE_GPU=1`` (multi-rank rehearsal on fewer GPUs)."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("QLDPC_SHARE_GPU") == "1":
+        import torch
+
+        local %= max(1, torch.cuda.device_count())
+    return local

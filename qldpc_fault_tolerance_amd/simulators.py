@@ -406,10 +406,15 @@ class CodeSimulator_Phenon:
         d1 = (self.decoder1_x, self.decoder1_z)
         if not all(isinstance(d, BPDecoder) for d in d1):
             return None
-        b2 = (_engine_bp(self.decoder2_x), _engine_bp(self.decoder2_z))
+        # decoder2 = engine BPDecoder, or BPOSD_Decoder with GPU OSD (the Threshold notebook's
+        # BPDecoder + BPOSD_Decoder osd_e(10) pair): its soft BP feeds qldpc_phenl_set_final_osd
+        b2 = tuple(_final_round_bp(d) for d in (self.decoder2_x, self.decoder2_z))
         if any(b is None for b in b2):
             return None
         return d1[0].decoder, d1[1].decoder, b2[0], b2[1]
+
+    def _final_osd(self):
+        return tuple(getattr(d, "gpu_osd", None) for d in (self.decoder2_x, self.decoder2_z))
 
     def fused_counts(self, num_rounds: int, num_samples: int):
         parts = self._engine_parts()
@@ -422,6 +427,9 @@ class CodeSimulator_Phenon:
             self.seed = random.getrandbits(64)
         if self._ph is None:
             self._ph = DevicePhenl(self.code, *parts, num_rep=1, max_batch=self.max_batch)
+            ox, oz = self._final_osd()
+            if ox is not None or oz is not None:
+                self._ph.set_final_osd(ox, oz)
         rank, ws = parallel.world()
         b, c = parallel.shard_range(num_samples, rank, ws, begin=self._shot_offset)
         self._shot_offset += int(num_samples)
