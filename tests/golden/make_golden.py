@@ -4,6 +4,7 @@ Run in the build container only (``/root/reference`` is not on the GPU box):
 
     python tests/golden/make_golden.py          # reference_harness_n225.npz
     python tests/golden/make_golden.py phen     # reference_harness_phen_n225.npz
+    python tests/golden/make_golden.py configs  # reference_harness_configs.npz (configs 2-5)
 
 The reference modules import third-party packages that are absent here
 (``graph_tools``, ``ldpc``, ``bposd``, ``stim``, …), so empty stub
@@ -297,8 +298,102 @@ def main_phen():
     print("wrote", os.path.join(HERE, "reference_harness_phen_n225.npz"), len(out), "arrays")
 
 
+CONFIG_CODES = ["hgp_34_n1600", "LP_Matg8_L30_Dmin20", "GenBicycleA1", "GenBicycleA2", "GenBicycleA3", "GenBicycleA4"]
+
+
+def main_configs():
+    """Harness goldens on the BASELINE config codes -> tests/golden/reference_harness_configs.npz.
+
+    For each data-error config code (the synthesized [[1600,64]] HGP stand-in, the reference's own
+    LP_Matg8_L30_Dmin20 and GenBicycleA1-A4 matrices): ``_generate_error`` outputs and
+    ``_single_run`` failure flags (X / Z / Total) of the reference's CodeSimulator_DataError with the
+    reference's BP_Decoder_Class (BP = the oracle stub), and for config 5 (hgp_34_n1225_q3 stand-in,
+    num_rep = 3) the detector histories, final syndromes and failures of
+    CodeSimulator_Phenon_SpaceTime._single_run.  Uniforms are NOT stored: each shot re-seeds CPython's
+    ``random`` (seed recorded), so a test regenerates the identical stream.  Bits are packed
+    (np.packbits along the last axis).
+    """
+    install_stubs()
+    import Decoders
+    import Decoders_SpaceTime
+    import Simulators
+    import Simulators_SpaceTime
+
+    Simulators.parmap = lambda f, X, nprocs=1: [f(x) for x in X]
+    out = {}
+    cls = Decoders.BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    for name in CONFIG_CODES:
+        code = codes.get_code(name)
+        n = code.N
+        tag = name
+        # ---- A5: _generate_error at [p/2]*3 (p = 0.08) and an asymmetric split
+        for gtag, probs in (("dep08", [0.04] * 3), ("asym", [0.03, 0.01, 0.07])):
+            E_x, E_z = [], []
+            sim = Simulators.CodeSimulator_DataError(code=code, decoder_x=None, decoder_z=None,
+                                                     pauli_error_probs=probs, eval_logical_type="Total")
+            for s in range(8):
+                random.seed(31000 + s)
+                ex, ez = sim._generate_error()
+                E_x.append(ex.copy())
+                E_z.append(ez.copy())
+            out[f"{tag}_gen_{gtag}_probs"] = np.array(probs)
+            out[f"{tag}_gen_{gtag}_seed0"] = np.array([31000])
+            out[f"{tag}_gen_{gtag}_ex"] = np.packbits(np.array(E_x, dtype=np.uint8), axis=-1)
+            out[f"{tag}_gen_{gtag}_ez"] = np.packbits(np.array(E_z, dtype=np.uint8), axis=-1)
+        # ---- A1-A3, A6-A8: _single_run with the reference decoder factory (EvalWER data branch)
+        S = 24 if n > 1000 else 40
+        for p in (0.04, 0.08):
+            dx = cls.GetDecoder({"h": code.hz, "p_data": p})
+            dz = cls.GetDecoder({"h": code.hx, "p_data": p})
+            for mode in ("X", "Z", "Total"):
+                sim = Simulators.CodeSimulator_DataError(code=code, decoder_x=dx, decoder_z=dz,
+                                                         pauli_error_probs=[p / 2] * 3, eval_logical_type=mode)
+                flags = []
+                for s in range(S):
+                    random.seed(41000 + s)
+                    flags.append(int(sim._single_run()))
+                out[f"{tag}_run_p{int(round(p * 100))}_{mode}_fail"] = np.array(flags, dtype=np.uint8)
+            out[f"{tag}_run_p{int(round(p * 100))}_seed0"] = np.array([41000])
+        print(name, "done", flush=True)
+
+    # ---- config 5: CodeSimulator_Phenon_SpaceTime on the 1764 x 5439 space-time graph
+    class Capture:
+        def __init__(self, inner):
+            self.inner, self.seen = inner, []
+
+        def decode(self, x):
+            self.seen.append(np.array(x, dtype=np.uint8))
+            return self.inner.decode(x)
+
+    code = codes.get_code("hgp_34_n1225_q3")
+    p = 0.01
+    stc = Decoders_SpaceTime.ST_BP_Decoder_Class(max_iter_ratio=10, bp_method="minimum_sum", ms_scaling_factor=0.625)
+    d1x = Capture(stc.GetDecoder({"h": code.hz, "p_data": p, "p_syndrome": p, "num_rep": 3}))
+    d1z = Capture(stc.GetDecoder({"h": code.hx, "p_data": p, "p_syndrome": p, "num_rep": 3}))
+    d2x = Capture(cls.GetDecoder({"h": code.hz, "p_data": p}))
+    d2z = Capture(cls.GetDecoder({"h": code.hx, "p_data": p}))
+    sim = Simulators_SpaceTime.CodeSimulator_Phenon_SpaceTime(
+        code=code, decoder1_x=d1x, decoder1_z=d1z, decoder2_x=d2x, decoder2_z=d2z,
+        pauli_error_probs=[p / 2] * 3, q=p, eval_logical_type="Total", num_rep=3)
+    flags = []
+    for s in range(6):
+        random.seed(51000 + s)
+        flags.append(int(sim._single_run(3)))  # 2 noisy rounds of 3 repetitions + the perfect round
+    out["st1225_seed0"] = np.array([51000])
+    out["st1225_fail"] = np.array(flags, dtype=np.uint8)
+    out["st1225_d1z_hist"] = np.packbits(np.array(d1z.seen), axis=-1)
+    out["st1225_d1x_hist"] = np.packbits(np.array(d1x.seen), axis=-1)
+    out["st1225_d2z_synd"] = np.packbits(np.array(d2z.seen), axis=-1)
+    out["st1225_d2x_synd"] = np.packbits(np.array(d2x.seen), axis=-1)
+    path = os.path.join(HERE, "reference_harness_configs.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, len(out), "arrays")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "phen":
         main_phen()
+    elif len(sys.argv) > 1 and sys.argv[1] == "configs":
+        main_configs()
     else:
         main()

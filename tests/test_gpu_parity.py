@@ -51,7 +51,8 @@ def test_decode_adaptive_alpha_matches_oracle(gpu, oracle):
 
 
 @pytest.mark.parametrize("precision", [64, 32])
-@pytest.mark.parametrize("name", ["hgp_34_n225", "hgp_34_n1600", "LP_Matg8_L30_Dmin20", "GenBicycleA4"])
+@pytest.mark.parametrize("name", ["hgp_34_n225", "hgp_34_n1600", "LP_Matg8_L30_Dmin20", "GenBicycleA1", "GenBicycleA3",
+                                  "GenBicycleA4"])
 def test_mc_per_shot_matches_oracle(gpu, oracle, precision, name):
     from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceMC
 
