@@ -234,7 +234,8 @@ int qldpc_bp_geometry(const qldpc_bp *bp, int32_t *threads, int32_t *vars_per_th
 /* Kernel engine serving a decoder: 3 = register-resident variables (default
  * when the graph fits: column degree <= 4, <= 8 variables per thread, image
  * < 64 KiB), 2 = streamed variables, 1 = LDS-atomic check state, 4 = engine 3
- * with c2v computed by the check phase, 5 = product-sum (bp_method 0).
+ * with c2v computed by the check phase, 5 = product-sum (bp_method 0), 6 = HBM-resident
+ * messages (qldpc_bp_create_hbm; automatic for images over 160 KiB).
  * QLDPC_ENGINE in the environment selects 1, 2 or 4 explicitly. */
 int qldpc_bp_engine(const qldpc_bp *bp, int32_t *engine);
 
@@ -243,6 +244,16 @@ int qldpc_bp_engine(const qldpc_bp *bp, int32_t *engine);
  * 4th edge slot at compile time).  0 for the other engines and for the fp64
  * kernels of workgroups wider than 256 threads. */
 int qldpc_bp_degree3_slots(const qldpc_bp *bp, int32_t *d3k);
+
+/* Min-sum decoder on engine 6 (bp_hbm.hip): messages in HBM as coalesced
+ * [edge][lane] arrays, one decode per lane, waves independent.  The engine every
+ * create call falls back to when no LDS engine holds a decode's image (> 160
+ * KiB: e.g. the fp64 space-time graph of hgp_34_n1225_q3 at num_rep 3) or a
+ * column degree exceeds 8; this entry point forces it for any graph (row and
+ * column degree <= 16).  Same decode contract as qldpc_bp_create (the ldpc
+ * bp_decoder replacement, src/Decoders.py:80-84); min-sum only. */
+int qldpc_bp_create_hbm(qldpc_graph *g, const double *channel_probs, int32_t max_iter, double ms_scaling_factor,
+                        int32_t precision, qldpc_bp **out);
 
 /* Engine 3: extra LDS cycles of one variable-phase pass's CS gathers (summed
  * over gather instructions and lane groups: distinct checks on one bank beyond

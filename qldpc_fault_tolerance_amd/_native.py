@@ -23,7 +23,7 @@ EXPORTED = [
     "qldpc_phenl_trace_len", "qldpc_phenl_launch", "qldpc_bp_degree3_slots", "qldpc_bp_create_soft",
     "qldpc_bp_decode_batch_soft", "qldpc_osd_create", "qldpc_osd_destroy", "qldpc_osd_rank",
     "qldpc_osd_decode_batch", "qldpc_osd_gpu_create", "qldpc_osd_gpu_destroy", "qldpc_osd_gpu_decode", "qldpc_phenl_set_final_osd",
-    "qldpc_bp_bank_stats",
+    "qldpc_bp_bank_stats", "qldpc_bp_create_hbm",
 ]
 
 
@@ -82,6 +82,8 @@ def _declare(L):
     L.qldpc_bp_set_channel_probs.argtypes = [_vp, _vp]
     L.qldpc_bp_decode_batch.restype = ctypes.c_int
     L.qldpc_bp_decode_batch.argtypes = [_vp, _vp, _vp, _vp, _vp, _i64, _vp]
+    L.qldpc_bp_create_hbm.restype = ctypes.c_int
+    L.qldpc_bp_create_hbm.argtypes = [_vp, _vp, _i32, _dbl, _i32, _pp]
     L.qldpc_bp_create_soft.restype = ctypes.c_int
     L.qldpc_bp_create_soft.argtypes = [_vp, _vp, _i32, _dbl, _i32, _pp]
     L.qldpc_bp_decode_batch_soft.restype = ctypes.c_int

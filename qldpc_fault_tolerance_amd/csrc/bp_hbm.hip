@@ -1,0 +1,296 @@
+// bp_hbm.hip — engine 6: min-sum BP with HBM-resident messages, one decode per lane.
+//
+// For Tanner graphs whose per-decode LDS image exceeds the 160 KiB of a CU (the
+// fp64 space-time graph of config 5: 1764 x 5439, E = 15,288, ~176 KB) and on
+// request (QLDPC_ENGINE=6 / qldpc_bp_create_hbm) for any graph.  Each lane of a
+// wave decodes its own syndrome; the 64 lanes of a wave walk the graph in
+// lock step, so every graph index is wave-uniform (scalar loads of the edge
+// tables) and every message access is one coalesced 512-byte (fp64) / 256-byte
+// (fp32) segment of an [edge][lane] array in HBM:
+//   V [E][64]   v2c, canonical bits (sign := v2c <= 0), row-major edge order
+//   C [E][64]   c2v, column-major edge order (rows ascending per column)
+//   X [n][64]   decisions (u8),  S [m][64] syndrome (u8, transposed per chunk)
+// One flooding iteration = a check sweep (rows: read V, min / second min /
+// parity, write every edge's c2v = (-1)^sgn alpha min_{others}|v2c| into C at
+// its column-major position; the H x == s test of the previous iteration's
+// decisions rides along) and a variable sweep (columns: read C, ldpc's forward
+// / backward sums in row order, write canonical v2c back into V, the decision
+// into X).  Per edge and iteration that is one read and one write of each of V
+// and C: 32 B (fp64) / 16 B (fp32) of HBM traffic, exactly SURVEY.md §8d's
+// algorithmic bytes, plus 1 B of decision per edge.  No barrier, no LDS: waves
+// are independent and take 64-syndrome chunks from a device work queue.
+//
+// Arithmetic is ldpc 0.1.x's minimum_sum operation for operation (oracle
+// bp_ms_*): the check phase's {min over the others, parity} is order
+// independent, the variable phase keeps ldpc's summation order, both with
+// -ffp-contract=off, so fp64 results are bit-identical to the oracle and fp32 to
+// its float mode.  A converged lane idles (exec-masked) until its wave's 64
+// decodes are done.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "bp_kernels.h"
+#include "runtime.h"
+
+namespace {
+
+using namespace qldpc;
+
+constexpr int kHRow = 16;  // max row degree (compile-time register block)
+constexpr int kHCol = 16;  // max column degree
+constexpr int kHThreads = 256;
+
+struct HArgs {
+  const int32_t* rp;     // [m+1] CSR row pointers (row-major edge ids)
+  const int32_t* rcol;   // [m][kHRow] variable of each row edge
+  const int32_t* rcpos;  // [m][kHRow] column-major position of each row edge
+  const int32_t* cp;     // [n+1] CSC column pointers (column-major edge ids)
+  const int32_t* crpos;  // [n][kHCol] row-major position of each column edge (rows ascending)
+  const void* llr;       // T [n] log((1-p)/p)
+  void* ws;              // per wave: V, C (T [E][64]) then X [n][64], S [m][64] (u8)
+  unsigned long long ws_wave_bytes;
+  const uint8_t* synd;   // [B][m]
+  uint8_t* corr;         // [B][n]
+  int32_t* iters;        // [B] or NULL
+  uint8_t* conv;         // [B] or NULL
+  unsigned int* work;    // chunk-queue head (zeroed per launch)
+  long long B;
+  int m, n, E, max_iter;
+  double alpha;          // 0 => 1 - 2^-iter
+};
+
+template <typename T>
+__device__ inline typename FT<T>::U hcanon(T v) {
+  using U = typename FT<T>::U;
+  const U b = FT<T>::bits(v);
+  return b | ((b - (U)1) & ~b & FT<T>::kSign);  // sign bit := v <= 0 (only +0 changes)
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kHThreads) hdec_kernel(HArgs A) {
+  using U = typename FT<T>::U;
+  constexpr U kS = FT<T>::kSign;
+  const int lane = threadIdx.x & 63;
+  const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  unsigned char* wb = static_cast<unsigned char*>(A.ws) + (size_t)wave * A.ws_wave_bytes;
+  U* V = reinterpret_cast<U*>(wb) + lane;
+  U* C = V + (size_t)A.E * 64;
+  uint8_t* X = reinterpret_cast<uint8_t*>(reinterpret_cast<U*>(wb) + (size_t)2 * A.E * 64) + lane;
+  uint8_t* S = X + (size_t)A.n * 64;
+  const T* L = static_cast<const T*>(A.llr);
+  const int m = A.m, n = A.n;
+  const bool adaptive = A.alpha == 0.0;
+  const long long nchunks = (A.B + 63) / 64;
+  while (true) {
+    int chi = 0;
+    if (lane == 0) chi = (int)atomicAdd(A.work, 1u);
+    const long long ch = (long long)__builtin_amdgcn_readfirstlane(chi);
+    if (ch >= nchunks) break;
+    const long long shot = ch * 64 + lane;
+    const bool live = shot < A.B;
+    // this lane's syndrome, transposed to [m][64] (coalesced in the sweeps)
+    const uint8_t* srow = A.synd + (live ? shot : 0) * (long long)m;
+    for (int i = 0; i < m; ++i) S[(size_t)i * 64] = live ? (uint8_t)(srow[i] & 1u) : (uint8_t)0;
+    bool done = !live;
+    int conv = 0, iters = 0;
+    for (int it = 0;; ++it) {
+      // ---------------------------------------- check sweep (+ the H x == s test of iteration it)
+      const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : (T)A.alpha;
+      uint32_t mism = 0;
+      for (int i = 0; i < m; ++i) {
+        const int e0 = A.rp[i], d = A.rp[i + 1] - e0;
+        const int32_t* rc = A.rcol + (size_t)i * kHRow;
+        const int32_t* rq = A.rcpos + (size_t)i * kHRow;
+        const uint32_t s = done ? 0u : S[(size_t)i * 64];
+        U v[kHRow];
+        uint32_t hx = 0;
+#pragma unroll
+        for (int k = 0; k < kHRow; ++k) {
+          if (k < d && !done) {
+            if (it == 0) {
+              v[k] = hcanon<T>(L[rc[k]]);  // ldpc's first check update reads the channel LLRs
+            } else {
+              v[k] = V[(size_t)(e0 + k) * 64];
+              hx ^= X[(size_t)rc[k] * 64];
+            }
+          }
+        }
+        mism |= (hx ^ s) & 1u;
+        U m1 = FT<T>::kSent, m2 = FT<T>::kSent, px = s ? kS : (U)0;
+#pragma unroll
+        for (int k = 0; k < kHRow; ++k) {
+          if (k < d) {
+            const U a = v[k] & ~kS;
+            const U hi = m1 > a ? m1 : a;
+            m2 = m2 < hi ? m2 : hi;
+            m1 = m1 < a ? m1 : a;
+            px ^= v[k];
+          }
+        }
+        const U b1 = FT<T>::bits(FT<T>::val(m1) * alpha), b2 = FT<T>::bits(FT<T>::val(m2) * alpha);
+#pragma unroll
+        for (int k = 0; k < kHRow; ++k) {
+          if (k < d) {
+            // min over the others (m2 if this edge holds m1), sign = syndrome ^ parity of the others
+            const U mag = (v[k] & ~kS) == m1 ? b2 : b1;
+            if (!done) C[(size_t)rq[k] * 64] = mag ^ ((px ^ v[k]) & kS);
+          }
+        }
+      }
+      if (!done && it > 0) {
+        if (!mism) {
+          done = true;
+          conv = 1;
+          iters = it;
+        } else if (it >= A.max_iter) {
+          done = true;
+          iters = A.max_iter;
+        }
+      }
+      if (__all(done ? 1 : 0)) break;
+      // ---------------------------------------- variable sweep (ldpc's column order)
+      for (int j = 0; j < n; ++j) {
+        const int k0 = A.cp[j], d = A.cp[j + 1] - k0;
+        const int32_t* cr = A.crpos + (size_t)j * kHCol;
+        T c[kHCol];
+#pragma unroll
+        for (int t = 0; t < kHCol; ++t)
+          if (t < d && !done) c[t] = FT<T>::val(C[(size_t)(k0 + t) * 64]);
+        T f[kHCol];
+        T acc = L[j];
+#pragma unroll
+        for (int t = 0; t < kHCol; ++t) {
+          if (t < d) {
+            f[t] = acc;
+            acc = acc + c[t];
+          }
+        }
+        if (!done) {
+          X[(size_t)j * 64] = acc <= (T)0 ? 1 : 0;
+          // backward sums: v2c_t = f_t + ((c_last + ...) + c_{t+1}); the redundant `0 + c`
+          // and `f + 0` of ldpc's loop change at most the sign of a zero (erased by hcanon)
+          T b = (T)0;
+#pragma unroll
+          for (int t = kHCol - 1; t >= 0; --t) {
+            if (t < d) {
+              const T vv = (t == d - 1) ? f[t] : f[t] + b;
+              b = (t == d - 1) ? c[t] : b + c[t];
+              V[(size_t)cr[t] * 64] = hcanon<T>(vv);
+            }
+          }
+        }
+      }
+    }
+    if (live) {
+      for (int j = 0; j < n; ++j) A.corr[shot * (long long)n + j] = X[(size_t)j * 64];
+      if (A.iters) A.iters[shot] = iters;
+      if (A.conv) A.conv[shot] = (uint8_t)conv;
+    }
+  }
+}
+
+}  // namespace
+
+namespace qldpc_rt {
+
+// Host tables of engine 6 (fixed-stride row / column records, uniform loads).
+int hbm_prepare(qldpc_bp* bp) {
+  const qldpc_graph* g = bp->g;
+  const int m = g->m, n = g->n, E = g->nnz;
+  if (g->max_row > kHRow || g->max_col > kHCol)
+    return set_err(QLDPC_ENOTSUP, "HBM engine: row or column degree above 16");
+  std::vector<int32_t> rcol((size_t)std::max(1, m) * kHRow, 0), rcpos((size_t)std::max(1, m) * kHRow, 0);
+  std::vector<int32_t> cp(n + 1, 0), crpos((size_t)n * kHCol, 0);
+  // column-major numbering: columns ascending, rows ascending within a column (ldpc's order)
+  std::vector<int32_t> cpos_of(std::max(1, E));
+  for (int j = 0; j < n; ++j) cp[j + 1] = cp[j] + (int)g->col_rows[j].size();
+  std::vector<int> fill(n, 0);
+  for (int i = 0; i < m; ++i)
+    for (int e = g->row_ptr[i]; e < g->row_ptr[i + 1]; ++e) {
+      const int j = g->col_idx[e];
+      const int t = fill[j]++;  // rows visited ascending: t-th row of column j
+      cpos_of[e] = cp[j] + t;
+      crpos[(size_t)j * kHCol + t] = e;
+      rcol[(size_t)i * kHRow + (e - g->row_ptr[i])] = j;
+      rcpos[(size_t)i * kHRow + (e - g->row_ptr[i])] = cp[j] + t;
+    }
+  int rc;
+  if ((rc = bp->h_rp.alloc((size_t)(m + 1) * 4)) || (rc = bp->h_rcol.alloc(rcol.size() * 4)) ||
+      (rc = bp->h_rcpos.alloc(rcpos.size() * 4)) || (rc = bp->h_cp.alloc(cp.size() * 4)) ||
+      (rc = bp->h_crpos.alloc(std::max<size_t>(1, crpos.size()) * 4)) || (rc = bp->work.alloc(16)))
+    return rc;
+  if (hipMemcpy(bp->h_rp.p, g->row_ptr.data(), (size_t)(m + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(bp->h_rcol.p, rcol.data(), rcol.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(bp->h_rcpos.p, rcpos.data(), rcpos.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(bp->h_cp.p, cp.data(), cp.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      (!crpos.empty() && hipMemcpy(bp->h_crpos.p, crpos.data(), crpos.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+    return set_err(QLDPC_EHIP, "upload HBM-engine tables");
+  bp->TB = kHThreads;
+  bp->VPL = 1;
+  bp->lds_bytes = 0;
+  return 0;
+}
+
+size_t hbm_wave_bytes(const qldpc_bp* bp) {
+  const size_t tsize = bp->precision == 32 ? 4 : 8;
+  const size_t b = (size_t)2 * bp->g->nnz * 64 * tsize + (size_t)(bp->g->n + bp->g->m) * 64;
+  return (b + 255) & ~(size_t)255;
+}
+
+const void* hbm_kernel(int precision) {
+  return precision == 32 ? reinterpret_cast<const void*>(&hdec_kernel<float>)
+                         : reinterpret_cast<const void*>(&hdec_kernel<double>);
+}
+
+int hbm_decode_launch(qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int32_t* iters, uint8_t* conv, int64_t B,
+                      hipStream_t stream) {
+  // resident waves: enough to keep HBM busy, bounded by the batch and by a
+  // workspace budget (QLDPC_HBM_WS_GB, default 16 GiB of the 288 GB)
+  const size_t wb = hbm_wave_bytes(bp);
+  const char* e = std::getenv("QLDPC_HBM_WS_GB");
+  const double gb = (e && *e) ? std::atof(e) : 16.0;
+  const char* ew = std::getenv("QLDPC_HBM_WAVES");  // resident waves per CU (default 8)
+  const long long wpc = (ew && *ew) ? std::max(1, std::atoi(ew)) : 8;
+  long long waves = std::min<long long>((long long)bp->cus * wpc, (B + 63) / 64);
+  waves = std::min<long long>(waves, std::max<long long>(1, (long long)(gb * (1ull << 30) / (double)wb)));
+  const int wpb = kHThreads / 64;
+  const long long blocks = (waves + wpb - 1) / wpb;
+  const size_t need = (size_t)blocks * wpb * wb;
+  if (bp->h_ws.bytes < need) {
+    bp->h_ws.release();
+    int rc = bp->h_ws.alloc(need);
+    if (rc) return rc;
+  }
+  HArgs a;
+  a.rp = static_cast<const int32_t*>(bp->h_rp.p);
+  a.rcol = static_cast<const int32_t*>(bp->h_rcol.p);
+  a.rcpos = static_cast<const int32_t*>(bp->h_rcpos.p);
+  a.cp = static_cast<const int32_t*>(bp->h_cp.p);
+  a.crpos = static_cast<const int32_t*>(bp->h_crpos.p);
+  a.llr = bp->llr.p;
+  a.ws = bp->h_ws.p;
+  a.ws_wave_bytes = wb;
+  a.synd = synd;
+  a.corr = corr;
+  a.iters = iters;
+  a.conv = conv;
+  a.work = static_cast<unsigned int*>(bp->work.p);
+  a.B = B;
+  a.m = bp->g->m;
+  a.n = bp->g->n;
+  a.E = bp->g->nnz;
+  a.max_iter = bp->max_iter;
+  a.alpha = bp->alpha;
+  QLDPC_HIP(hipMemsetAsync(bp->work.p, 0, 4, stream));
+  if (bp->precision == 32)
+    hipLaunchKernelGGL(hdec_kernel<float>, dim3((unsigned)blocks), dim3(kHThreads), 0, stream, a);
+  else
+    hipLaunchKernelGGL(hdec_kernel<double>, dim3((unsigned)blocks), dim3(kHThreads), 0, stream, a);
+  QLDPC_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace qldpc_rt

@@ -274,6 +274,17 @@ int qldpc_graph_info(const qldpc_graph* g, int32_t* m, int32_t* n, int32_t* nnz,
 
 static int upload_llr(qldpc_bp* bp) {
   const int TB = bp->TB, VPL = bp->VPL, n = bp->g->n;
+  if (bp->engine == 6) {  // HBM engine: log((1-p)/p) per variable, variable order
+    std::vector<double> l64(n);
+    for (int j = 0; j < n; ++j) l64[j] = std::log((1.0 - bp->probs[j]) / bp->probs[j]);  // glibc log, as Cython
+    if (bp->precision == 32) {
+      std::vector<float> l32(l64.begin(), l64.end());
+      QLDPC_HIP(hipMemcpy(bp->llr.p, l32.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    } else {
+      QLDPC_HIP(hipMemcpy(bp->llr.p, l64.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+    }
+    return 0;
+  }
   if (bp->engine == 5) {  // product-sum priors: ratio p / (1 - p), computed in double (oracle ws_priors)
     std::vector<double> r64(n);
     for (int j = 0; j < n; ++j) r64[j] = bp->probs[j] / (1.0 - bp->probs[j]);
@@ -593,6 +604,13 @@ int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_ite
                         min_col_slots, 0, out);
 }
 
+// Engine 6: HBM-resident messages, one decode per lane (any graph; chosen automatically when
+// no LDS engine holds the per-decode image).
+int qldpc_bp_create_hbm(qldpc_graph* g, const double* channel_probs, int32_t max_iter, double ms_scaling_factor,
+                        int32_t precision, qldpc_bp** out) {
+  return create_min_sum(g, channel_probs, max_iter, QLDPC_MIN_SUM, ms_scaling_factor, precision, 0, 0, 6, out);
+}
+
 // Engine 1 is the one whose decode kernel can hand back the final posteriors.
 int qldpc_bp_create_soft(qldpc_graph* g, const double* channel_probs, int32_t max_iter, double ms_scaling_factor,
                          int32_t precision, qldpc_bp** out) {
@@ -608,11 +626,18 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     return set_err(QLDPC_EINVAL, "bp_method must be 0 (product_sum) or 1 (minimum_sum)");
   QLDPC_HIP(hipSetDevice(g->device));
   if (bp_method == QLDPC_PRODUCT_SUM) return create_ps(g, channel_probs, max_iter, precision, out);
-  if (g->max_col > 8 || min_col_slots > 8) return set_err(QLDPC_ENOTSUP, "column degree > 8");
+  const int want_engine = forced_engine ? forced_engine : env_int("QLDPC_ENGINE", 3);
   auto* bp = new qldpc_bp();
   bp->g = g;
-  const int want_engine = forced_engine ? forced_engine : env_int("QLDPC_ENGINE", 3);
-  bp->engine = (want_engine >= 1 && want_engine <= 4) ? want_engine : 3;
+  bp->engine = ((want_engine >= 1 && want_engine <= 4) || want_engine == 6) ? want_engine : 3;
+  // column degree > 8: beyond the LDS engines' edge slots -> engine 6 (degree <= 16); soft BP stays engine 1
+  if ((g->max_col > 8 || min_col_slots > 8) && bp->engine != 6) {
+    if (bp->engine == 1) {
+      delete bp;
+      return set_err(QLDPC_ENOTSUP, "column degree > 8");
+    }
+    bp->engine = 6;
+  }
   bp->max_iter = max_iter > 0 ? max_iter : g->n;
   bp->method = bp_method;
   bp->alpha = ms_scaling_factor;
@@ -624,14 +649,30 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     bp->DMAX = colmax;
   bp->probs.assign(channel_probs, channel_probs + g->n);
   auto fail = [&](int code) {
-    bp->vchk.release();
-    bp->llr.release();
-    bp->rdeg.release();
-    bp->perm.release();
-    bp->rperm.release();
+    for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->rperm, &bp->work, &bp->h_rp, &bp->h_rcol,
+                      &bp->h_rcpos, &bp->h_cp, &bp->h_crpos, &bp->h_ws})
+      d->release();
     delete bp;
     return code;
   };
+  // engine 6: messages in HBM, one decode per lane (bp_hbm.hip) -- requested, or below when the
+  // per-decode LDS image of every LDS engine exceeds the 160 KiB of a CU
+  auto setup_hbm = [&]() {
+    bp->engine = 6;
+    bp->ea_shift = 0;
+    bp->slot_var.clear();
+    int rc6 = hbm_prepare(bp);
+    if (rc6) return fail(rc6);
+    bp->llr.release();
+    if ((rc6 = bp->llr.alloc((size_t)g->n * (precision == 32 ? 4 : 8))) || (rc6 = upload_llr(bp))) return fail(rc6);
+    int nb6 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb6, hbm_kernel(precision), bp->TB, 0) != hipSuccess) nb6 = 1;
+    bp->blocks_per_cu = std::max(1, nb6);
+    if ((rc6 = device_cus(g->device, bp->cus))) return fail(rc6);
+    *out = bp;
+    return 0;
+  };
+  if (bp->engine == 6) return setup_hbm();
   const int tsize = precision == 32 ? 4 : 8;
   int DM = bp->DMAX;
   std::vector<uint32_t> vchk;
@@ -696,7 +737,11 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         }
       }
     }
-    if (bp->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB (use precision 32)"));
+    if (bp->lds_bytes > kLdsMax) {  // no LDS engine holds this decode: HBM-resident messages
+      if (env_int("QLDPC_HBM_FALLBACK", 1) == 0)
+        return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB (QLDPC_HBM_FALLBACK=0)"));
+      return setup_hbm();
+    }
     // slot -> variable map: identity, or (engine 3) degree <= 3 variables first
     const int TB = bp->TB, VPL = bp->VPL;
     std::vector<int32_t> order;
@@ -765,7 +810,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
 int qldpc_bp_destroy(qldpc_bp* bp) {
   if (!bp) return 0;
   for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->rperm, &bp->work, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp,
-                    &bp->ps_ce, &bp->ps_ws})
+                    &bp->ps_ce, &bp->ps_ws, &bp->h_rp, &bp->h_rcol, &bp->h_rcpos, &bp->h_cp, &bp->h_crpos, &bp->h_ws})
     d->release();
   delete bp;
   return 0;
@@ -868,6 +913,7 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
   if (B == 0) return 0;
   QLDPC_HIP(hipSetDevice(bp->g->device));
   if (bp->engine == 5) return ps_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
+  if (bp->engine == 6) return hbm_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
   const long long cap = (long long)bp->blocks_per_cu * bp->cus;
   if (bp->engine == 1) {
     DecArgs a;
@@ -932,7 +978,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
                     qldpc_mc** out) {
   if (!out || (!dec_x && !dec_z)) return set_err(QLDPC_EINVAL, "need at least one sector decoder");
   qldpc_bp* d0 = dec_x ? dec_x : dec_z;
-  const bool staged = (dec_x && dec_x->engine == 5) || (dec_z && dec_z->engine == 5) ||
+  const bool staged = (dec_x && dec_x->engine >= 5) || (dec_z && dec_z->engine >= 5) ||
                       env_int("QLDPC_MC_STAGED", 0) == 1;
   if (staged) {  // staged pipeline around decode_batch (staged.hip): any decoder pair
     if (dec_x && dec_z && (dec_x->g->n != dec_z->g->n || dec_x->g->device != dec_z->g->device))

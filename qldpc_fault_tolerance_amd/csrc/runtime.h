@@ -75,6 +75,8 @@ struct qldpc_bp {
   // engine 5 (product-sum, bp_ps.hip): CSR / CSC on the device, optional HBM message workspace
   qldpc_rt::DevBuf ps_rp, ps_ci, ps_cp, ps_ce, ps_ws;
   long long ps_grid = 0;
+  // engine 6 (HBM-resident messages, bp_hbm.hip): uniform edge tables and the message workspace
+  qldpc_rt::DevBuf h_rp, h_rcol, h_rcpos, h_cp, h_crpos, h_ws;
 };
 
 struct qldpc_mc {
@@ -106,6 +108,12 @@ int ps_decode_launch(const qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int
 
 // GPU OSD handle built on this graph? (osd.hip; qldpc_phenl_set_final_osd checks it)
 bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g);
+
+// engine 6 (bp_hbm.hip)
+int hbm_prepare(qldpc_bp* bp);
+const void* hbm_kernel(int precision);
+int hbm_decode_launch(qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int32_t* iters, uint8_t* conv, int64_t B,
+                      hipStream_t stream);
 
 // staged data-error shot loop (staged.hip): bit-sliced sampling / syndromes /
 // checks around qldpc_bp_decode_batch, for decoders the fused kernels do not serve

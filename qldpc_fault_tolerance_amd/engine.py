@@ -77,7 +77,7 @@ class DeviceBP:
 
     def __init__(self, H, channel_probs, max_iter: int = 0, bp_method="minimum_sum", ms_scaling_factor=0.625,
                  precision: int = 64, vars_per_thread: int = 0, device: int | None = None, graph: DeviceGraph | None = None,
-                 min_col_slots: int = 0, soft: bool = False):
+                 min_col_slots: int = 0, soft: bool = False, hbm: bool = False):
         self.graph = graph if graph is not None else DeviceGraph(H, device=device)
         n = self.graph.n
         probs = np.asarray(channel_probs, dtype=np.float64)
@@ -92,7 +92,14 @@ class DeviceBP:
         self.precision = int(precision)
         self.soft = bool(soft)
         h = ctypes.c_void_p()
-        if self.soft:
+        if hbm:
+            # engine 6: HBM-resident messages (automatic when no LDS engine holds the image)
+            if self.bp_method != 1:
+                raise NotImplementedError("the HBM-resident engine implements minimum_sum")
+            _native.check(_native.lib().qldpc_bp_create_hbm(
+                self.graph.handle, self.channel_probs.ctypes.data_as(ctypes.c_void_p), self.max_iter,
+                self.ms_scaling_factor, self.precision, ctypes.byref(h)), "qldpc_bp_create_hbm")
+        elif self.soft:
             # BP+OSD: engine 1 hands back the final posteriors (qldpc_bp_create_soft)
             if self.bp_method != 1:
                 raise NotImplementedError("soft-output BP (BP+OSD) is implemented for minimum_sum")
