@@ -98,6 +98,8 @@ def kernel_name(dec):
     """Name of the fused MC kernel the decoder's geometry selects (as rocprofv3 reports it)."""
     g = dec.geometry()
     t = "float" if dec.precision == 32 else "double"
+    if g["engine"] == 6:  # HBM-resident messages: staged pipeline around the per-lane decode kernel
+        return f"(anonymous namespace)::hdec_kernel<{t}> (engine 6, staged shot loop)"
     mc = dec.graph.info()["max_col_deg"]
     dmax = 4 if mc <= 4 else (mc if g["engine"] == 3 and mc <= 6 and dec.precision == 32 else 8)
     nch = (max(1, dec.graph.info()["max_row_deg"]) * (4 if dec.precision == 32 else 8) + 15) // 16
@@ -145,12 +147,15 @@ def pmc_traffic(a):
             vals, kern = [], None
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 for row in csv.DictReader(open(f)):
-                    if "mc_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    k = row.get("Kernel_Name", "")
+                    # every kernel of the launch (the fused kernel, or the staged pipeline's kernels)
+                    if row.get("Counter_Name") == counter and "at::native" not in k and "__amd_rocclr" not in k:
                         vals.append(float(row["Counter_Value"]))
-                        kern = row["Kernel_Name"]
-            if len(vals) != 1:
+                        if "mc_kernel" in k or "hdec_kernel" in k:
+                            kern = k
+            if not vals:
                 return None
-            out[counter] = vals[0]
+            out[counter] = sum(vals)
             out["kernel"] = kern
     fetch_b = out["FETCH_SIZE"] * 2 * 1024
     write_b = out["WRITE_SIZE"] * 1024
@@ -240,6 +245,8 @@ def phenl_main(a, torch, dist, world, rank, dev):
     frac_st = (R - 1) / R
     bytes_total = bpe * iters * (frac_st * E_st + (1 - frac_st) * E2)
     achieved = bytes_total / elapsed / 1e9 / world
+    st_engine = ph.decoders[0].geometry()["engine"]
+    bound, peak = ("hbm", HBM_PEAK_GBS) if st_engine == 6 else ("lds", LDS_PEAK_GBS)
     out = {
         "metric": "phenomenological space-time samples/sec (BASELINE config 5; not the headline)",
         "value": shots / elapsed, "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -252,9 +259,9 @@ def phenl_main(a, torch, dist, world, rank, dev):
                    "shots_per_gpu_step": S, "parallelism": f"sample-sharded x{world}"},
         "decodes_per_s": decodes / elapsed, "mean_iters_per_decode": iters / max(decodes, 1),
         "nonconverged_frac": int(w[6] + w[7]) / max(decodes, 1), "logical_error_rate": int(w[1]) / max(shots, 1),
-        "roofline": {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / LDS_PEAK_GBS, "traffic": None,
-                     "kernel": "whole staged pipeline (wall clock, per GPU)"},
+        "roofline": {"bound": bound, "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": None,
+                     "kernel": f"whole staged pipeline (wall clock, per GPU); space-time decoder engine {st_engine}"},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -361,6 +368,8 @@ def main():
     bytes_per_launch = (bpe * E * r["iters"] + r["decodes"] * ((mh + 7) // 8 + (nh + 7) // 8 + 16)) / (a.steps * world)
     achieved = bytes_per_launch / (r["kern_ms"] * 1e-3) / 1e9
     tb = traffic["bytes"] if traffic else None
+    # engine 6 keeps the messages in HBM: the same algorithmic bytes are HBM bytes
+    bound, peak = ("hbm", HBM_PEAK_GBS) if r["engine"] == 6 else ("lds", LDS_PEAK_GBS)
     out = {
         "metric": "BP-decoded shots/sec (node) on hgp_34_n1600 + % of HBM/LDS roofline",
         "value": r["value"],
@@ -386,8 +395,8 @@ def main():
         "mean_iters_per_decode": r["iters"] / max(r["decodes"], 1),
         "nonconverged_frac": r["nonconv"] / max(r["decodes"], 1),
         "logical_error_rate": r["failures"] / max(r["shots"], 1),
-        "roofline": {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / LDS_PEAK_GBS, "traffic": tb,
+        "roofline": {"bound": bound, "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": tb,
                      "kernel": r["kernel"], "kernel_ms": r["kern_ms"],
                      "bytes_per_launch": bytes_per_launch,
                      # HBM carries only the edge tables (L2-resident) and the counters
@@ -475,7 +484,7 @@ def time_data(a, precision, torch, dist, world, rank, dev):
         raise RuntimeError(f"counter mismatch: {shots} shots != {S} x {a.steps} x {world}")
     return {"value": shots / elapsed, "elapsed": elapsed, "kern_ms": kern_ms, "shots": shots, "failures": int(w[1]),
             "decodes": int(w[2] + w[3]), "iters": int(w[4] + w[5]), "nonconv": int(w[6] + w[7]),
-            "kernel": kernel_name(dx or dz)}
+            "kernel": kernel_name(dx or dz), "engine": (dx or dz).geometry()["engine"]}
 
 
 if __name__ == "__main__":

@@ -9,7 +9,7 @@
 // (fp32) segment of an [edge][lane] array in HBM:
 //   V [E][64]   v2c, canonical bits (sign := v2c <= 0), row-major edge order
 //   C [E][64]   c2v, column-major edge order (rows ascending per column)
-//   X [n][64]   decisions (u8),  S [m][64] syndrome (u8, transposed per chunk)
+//   X [n][64]   decisions (u8); syndromes are read straight from the [B][m] input
 // One flooding iteration = a check sweep (rows: read V, min / second min /
 // parity, write every edge's c2v = (-1)^sgn alpha min_{others}|v2c| into C at
 // its column-major position; the H x == s test of the previous iteration's
@@ -18,14 +18,16 @@
 // into X).  Per edge and iteration that is one read and one write of each of V
 // and C: 32 B (fp64) / 16 B (fp32) of HBM traffic, exactly SURVEY.md §8d's
 // algorithmic bytes, plus 1 B of decision per edge.  No barrier, no LDS: waves
-// are independent and take 64-syndrome chunks from a device work queue.
+// are independent; a lane whose decode ends takes the next syndrome from a device
+// queue at the next sweep boundary, so lanes of different iteration counts never
+// wait for each other.  The next row's / column's messages are loaded while the
+// current one is reduced (two rows or columns of loads in flight per lane).
 //
 // Arithmetic is ldpc 0.1.x's minimum_sum operation for operation (oracle
 // bp_ms_*): the check phase's {min over the others, parity} is order
 // independent, the variable phase keeps ldpc's summation order, both with
 // -ffp-contract=off, so fp64 results are bit-identical to the oracle and fp32 to
-// its float mode.  A converged lane idles (exec-masked) until its wave's 64
-// decodes are done.
+// its float mode.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,8 +41,8 @@ namespace {
 
 using namespace qldpc;
 
-constexpr int kHRow = 16;  // max row degree (compile-time register block)
-constexpr int kHCol = 16;  // max column degree
+constexpr int kHRow = 12;  // max row degree (compile-time register block)
+constexpr int kHCol = 12;  // max column degree
 constexpr int kHThreads = 256;
 
 struct HArgs {
@@ -50,7 +52,7 @@ struct HArgs {
   const int32_t* cp;     // [n+1] CSC column pointers (column-major edge ids)
   const int32_t* crpos;  // [n][kHCol] row-major position of each column edge (rows ascending)
   const void* llr;       // T [n] log((1-p)/p)
-  void* ws;              // per wave: V, C (T [E][64]) then X [n][64], S [m][64] (u8)
+  void* ws;              // per wave: V, C (T [E][64]) then X [n][64] (u8)
   unsigned long long ws_wave_bytes;
   const uint8_t* synd;   // [B][m]
   uint8_t* corr;         // [B][n]
@@ -69,126 +71,204 @@ __device__ inline typename FT<T>::U hcanon(T v) {
   return b | ((b - (U)1) & ~b & FT<T>::kSign);  // sign bit := v <= 0 (only +0 changes)
 }
 
+// Row / column records of the uniform edge tables, prefetched one ahead of use.
 template <typename T>
-__global__ void __launch_bounds__(kHThreads) hdec_kernel(HArgs A) {
+struct HRow {
+  typename FT<T>::U v[kHRow];
+  uint8_t x[kHRow];
+  int e0, d;
+};
+
+// The edge tables come in as separate __restrict__ kernel arguments: never written by the
+// kernel, so the backend may read them with scalar loads (uniform addresses) instead of one
+// vector load per lane.
+template <typename T>
+__global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32_t* __restrict__ rp,
+                                                         const int32_t* __restrict__ rcol,
+                                                         const int32_t* __restrict__ rcpos,
+                                                         const int32_t* __restrict__ cp,
+                                                         const int32_t* __restrict__ crpos,
+                                                         const void* __restrict__ llr) {
   using U = typename FT<T>::U;
   constexpr U kS = FT<T>::kSign;
   const int lane = threadIdx.x & 63;
   const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   unsigned char* wb = static_cast<unsigned char*>(A.ws) + (size_t)wave * A.ws_wave_bytes;
-  U* V = reinterpret_cast<U*>(wb) + lane;
-  U* C = V + (size_t)A.E * 64;
-  uint8_t* X = reinterpret_cast<uint8_t*>(reinterpret_cast<U*>(wb) + (size_t)2 * A.E * 64) + lane;
-  uint8_t* S = X + (size_t)A.n * 64;
-  const T* L = static_cast<const T*>(A.llr);
+  U* __restrict__ V = reinterpret_cast<U*>(wb) + lane;
+  U* __restrict__ C = reinterpret_cast<U*>(wb) + (size_t)A.E * 64 + lane;
+  uint8_t* __restrict__ X = reinterpret_cast<uint8_t*>(reinterpret_cast<U*>(wb) + (size_t)2 * A.E * 64) + lane;
+  const T* __restrict__ L = static_cast<const T*>(llr);
   const int m = A.m, n = A.n;
   const bool adaptive = A.alpha == 0.0;
-  const long long nchunks = (A.B + 63) / 64;
+  // per-lane decode state: lanes refill from the shot queue as soon as their decode ends, so
+  // a wave never idles behind its slowest lane (iteration counts differ per lane)
+  long long shot = -1;   // this lane's syndrome, -1 = none
+  int it = 0;            // iterations completed by this lane's decode
+  bool idle = false;     // queue drained for this lane
   while (true) {
-    int chi = 0;
-    if (lane == 0) chi = (int)atomicAdd(A.work, 1u);
-    const long long ch = (long long)__builtin_amdgcn_readfirstlane(chi);
-    if (ch >= nchunks) break;
-    const long long shot = ch * 64 + lane;
-    const bool live = shot < A.B;
-    // this lane's syndrome, transposed to [m][64] (coalesced in the sweeps)
-    const uint8_t* srow = A.synd + (live ? shot : 0) * (long long)m;
-    for (int i = 0; i < m; ++i) S[(size_t)i * 64] = live ? (uint8_t)(srow[i] & 1u) : (uint8_t)0;
-    bool done = !live;
-    int conv = 0, iters = 0;
-    for (int it = 0;; ++it) {
-      // ---------------------------------------- check sweep (+ the H x == s test of iteration it)
-      const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : (T)A.alpha;
-      uint32_t mism = 0;
-      for (int i = 0; i < m; ++i) {
-        const int e0 = A.rp[i], d = A.rp[i + 1] - e0;
-        const int32_t* rc = A.rcol + (size_t)i * kHRow;
-        const int32_t* rq = A.rcpos + (size_t)i * kHRow;
-        const uint32_t s = done ? 0u : S[(size_t)i * 64];
-        U v[kHRow];
-        uint32_t hx = 0;
+    // ---------------------------------------- refill lanes without a decode
+    const bool need = shot < 0 && !idle;
+    const unsigned long long nb = __ballot(need);
+    if (nb) {
+      const int cnt = __popcll(nb);
+      int base = 0;
+      if (lane == __ffsll((long long)nb) - 1) base = (int)atomicAdd(A.work, (unsigned)cnt);
+      base = __builtin_amdgcn_readfirstlane(__shfl(base, __ffsll((long long)nb) - 1));
+      if (need) {
+        const long long s = (long long)base + __popcll(nb & ((1ull << lane) - 1ull));
+        if (s < A.B) {
+          shot = s;
+          it = 0;
+        } else {
+          idle = true;
+        }
+      }
+    }
+    const bool active = shot >= 0;
+    if (!__any(active)) break;
+    const uint8_t* srow = A.synd + (active ? shot : 0) * (long long)m;
+    const bool first = it == 0;
+    // ---------------------------------------- check sweep (+ the H x == s test of iteration it)
+    const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : (T)A.alpha;
+    uint32_t mism = 0;
+    auto load_row = [&](int i, HRow<T>& r) {
+      // the row record (uniform) is read in uniform control flow: scalar loads
+      r.e0 = rp[i];
+      r.d = rp[i + 1] - r.e0;
+      const int32_t* rc = rcol + (size_t)i * kHRow;
+      int jv[kHRow];
 #pragma unroll
-        for (int k = 0; k < kHRow; ++k) {
-          if (k < d && !done) {
-            if (it == 0) {
-              v[k] = hcanon<T>(L[rc[k]]);  // ldpc's first check update reads the channel LLRs
+      for (int k = 0; k < kHRow; ++k) jv[k] = rc[k];  // padded records: index 0 beyond the degree
+#pragma unroll
+      for (int k = 0; k < kHRow; ++k) {
+        if (k < r.d) {
+          const T lj = L[jv[k]];
+          if (active) {
+            if (first) {
+              r.v[k] = hcanon<T>(lj);  // ldpc's first check update reads the channel LLRs
+              r.x[k] = 0;
             } else {
-              v[k] = V[(size_t)(e0 + k) * 64];
-              hx ^= X[(size_t)rc[k] * 64];
+              r.v[k] = V[(size_t)(r.e0 + k) * 64];
+              r.x[k] = X[(size_t)jv[k] * 64];
             }
           }
         }
-        mism |= (hx ^ s) & 1u;
-        U m1 = FT<T>::kSent, m2 = FT<T>::kSent, px = s ? kS : (U)0;
+      }
+    };
+    // two rows of loads in flight ahead of the row being reduced
+    HRow<T> cur, nx1;
+    load_row(0, cur);
+    if (1 < m) load_row(1, nx1);
+    for (int i = 0; i < m; ++i) {
+      HRow<T> nx2;
+      if (i + 2 < m) load_row(i + 2, nx2);
+      const int d = cur.d;
+      const int32_t* rqp = rcpos + (size_t)i * kHRow;
+      int rq[kHRow];
 #pragma unroll
-        for (int k = 0; k < kHRow; ++k) {
-          if (k < d) {
-            const U a = v[k] & ~kS;
-            const U hi = m1 > a ? m1 : a;
-            m2 = m2 < hi ? m2 : hi;
-            m1 = m1 < a ? m1 : a;
-            px ^= v[k];
-          }
-        }
-        const U b1 = FT<T>::bits(FT<T>::val(m1) * alpha), b2 = FT<T>::bits(FT<T>::val(m2) * alpha);
+      for (int k = 0; k < kHRow; ++k) rq[k] = rqp[k];
+      const uint32_t s = active ? (srow[i] & 1u) : 0u;
+      uint32_t hx = 0;
+      U m1 = FT<T>::kSent, m2 = FT<T>::kSent, px = s ? kS : (U)0;
 #pragma unroll
-        for (int k = 0; k < kHRow; ++k) {
-          if (k < d) {
-            // min over the others (m2 if this edge holds m1), sign = syndrome ^ parity of the others
-            const U mag = (v[k] & ~kS) == m1 ? b2 : b1;
-            if (!done) C[(size_t)rq[k] * 64] = mag ^ ((px ^ v[k]) & kS);
-          }
+      for (int k = 0; k < kHRow; ++k) {
+        if (k < d) {
+          hx ^= cur.x[k];
+          const U a = cur.v[k] & ~kS;
+          const U hi = m1 > a ? m1 : a;
+          m2 = m2 < hi ? m2 : hi;
+          m1 = m1 < a ? m1 : a;
+          px ^= cur.v[k];
         }
       }
-      if (!done && it > 0) {
-        if (!mism) {
-          done = true;
-          conv = 1;
-          iters = it;
-        } else if (it >= A.max_iter) {
-          done = true;
-          iters = A.max_iter;
+      mism |= (hx ^ s) & 1u;
+      const U b1 = FT<T>::bits(FT<T>::val(m1) * alpha), b2 = FT<T>::bits(FT<T>::val(m2) * alpha);
+#pragma unroll
+      for (int k = 0; k < kHRow; ++k) {
+        if (k < d && active) {
+          // min over the others (m2 if this edge holds m1), sign = syndrome ^ parity of the others
+          const U mag = (cur.v[k] & ~kS) == m1 ? b2 : b1;
+          C[(size_t)rq[k] * 64] = mag ^ ((px ^ cur.v[k]) & kS);
         }
       }
-      if (__all(done ? 1 : 0)) break;
-      // ---------------------------------------- variable sweep (ldpc's column order)
-      for (int j = 0; j < n; ++j) {
-        const int k0 = A.cp[j], d = A.cp[j + 1] - k0;
-        const int32_t* cr = A.crpos + (size_t)j * kHCol;
-        T c[kHCol];
+      cur = nx1;
+      nx1 = nx2;
+    }
+    // ---------------------------------------- end of this lane's decode?
+    bool fin = false;
+    int conv = 0;
+    if (active && !first) {
+      if (!mism) {
+        fin = true;
+        conv = 1;
+      } else if (it >= A.max_iter) {
+        fin = true;
+      }
+    }
+    if (__any(fin)) {
+      if (fin) {
+        for (int j = 0; j < n; ++j) A.corr[shot * (long long)n + j] = X[(size_t)j * 64];
+        if (A.iters) A.iters[shot] = conv ? it : A.max_iter;
+        if (A.conv) A.conv[shot] = (uint8_t)conv;
+        shot = -1;
+      }
+    }
+    const bool run = shot >= 0;  // lanes continuing into iteration it + 1
+    if (!__any(run)) continue;
+    // ---------------------------------------- variable sweep (ldpc's column order)
+    // two columns of c2v loads in flight ahead of the column being summed
+    T c1[kHCol], c2[kHCol];
+    int d1 = cp[1] - cp[0], d2 = n > 1 ? cp[2] - cp[1] : 0;
+#pragma unroll
+    for (int t = 0; t < kHCol; ++t) {
+      if (t < d1 && run) c1[t] = FT<T>::val(C[(size_t)(cp[0] + t) * 64]);
+      if (t < d2 && run) c2[t] = FT<T>::val(C[(size_t)(cp[1] + t) * 64]);
+    }
+    for (int j = 0; j < n; ++j) {
+      T c[kHCol];
+      const int d = d1;
+#pragma unroll
+      for (int t = 0; t < kHCol; ++t) {
+        c[t] = c1[t];
+        c1[t] = c2[t];
+      }
+      d1 = d2;
+      if (j + 2 < n) {  // the column after next: its c2v in flight under two columns of sums
+        const int k0n = cp[j + 2];
+        d2 = cp[j + 3] - k0n;
 #pragma unroll
         for (int t = 0; t < kHCol; ++t)
-          if (t < d && !done) c[t] = FT<T>::val(C[(size_t)(k0 + t) * 64]);
-        T f[kHCol];
-        T acc = L[j];
+          if (t < d2 && run) c2[t] = FT<T>::val(C[(size_t)(k0n + t) * 64]);
+      }
+      const int32_t* crp = crpos + (size_t)j * kHCol;
+      int cr[kHCol];
 #pragma unroll
-        for (int t = 0; t < kHCol; ++t) {
-          if (t < d) {
-            f[t] = acc;
-            acc = acc + c[t];
-          }
+      for (int t = 0; t < kHCol; ++t) cr[t] = crp[t];
+      T f[kHCol];
+      T acc = L[j];
+#pragma unroll
+      for (int t = 0; t < kHCol; ++t) {
+        if (t < d) {
+          f[t] = acc;
+          acc = acc + c[t];
         }
-        if (!done) {
-          X[(size_t)j * 64] = acc <= (T)0 ? 1 : 0;
-          // backward sums: v2c_t = f_t + ((c_last + ...) + c_{t+1}); the redundant `0 + c`
-          // and `f + 0` of ldpc's loop change at most the sign of a zero (erased by hcanon)
-          T b = (T)0;
+      }
+      if (run) {
+        X[(size_t)j * 64] = acc <= (T)0 ? 1 : 0;
+        // backward sums: v2c_t = f_t + ((c_last + ...) + c_{t+1}); the redundant `0 + c`
+        // and `f + 0` of ldpc's loop change at most the sign of a zero (erased by hcanon)
+        T b = (T)0;
 #pragma unroll
-          for (int t = kHCol - 1; t >= 0; --t) {
-            if (t < d) {
-              const T vv = (t == d - 1) ? f[t] : f[t] + b;
-              b = (t == d - 1) ? c[t] : b + c[t];
-              V[(size_t)cr[t] * 64] = hcanon<T>(vv);
-            }
+        for (int t = kHCol - 1; t >= 0; --t) {
+          if (t < d) {
+            const T vv = (t == d - 1) ? f[t] : f[t] + b;
+            b = (t == d - 1) ? c[t] : b + c[t];
+            V[(size_t)cr[t] * 64] = hcanon<T>(vv);
           }
         }
       }
     }
-    if (live) {
-      for (int j = 0; j < n; ++j) A.corr[shot * (long long)n + j] = X[(size_t)j * 64];
-      if (A.iters) A.iters[shot] = iters;
-      if (A.conv) A.conv[shot] = (uint8_t)conv;
-    }
+    if (run) ++it;
   }
 }
 
@@ -201,7 +281,7 @@ int hbm_prepare(qldpc_bp* bp) {
   const qldpc_graph* g = bp->g;
   const int m = g->m, n = g->n, E = g->nnz;
   if (g->max_row > kHRow || g->max_col > kHCol)
-    return set_err(QLDPC_ENOTSUP, "HBM engine: row or column degree above 16");
+    return set_err(QLDPC_ENOTSUP, "HBM engine: row or column degree above 12");
   std::vector<int32_t> rcol((size_t)std::max(1, m) * kHRow, 0), rcpos((size_t)std::max(1, m) * kHRow, 0);
   std::vector<int32_t> cp(n + 1, 0), crpos((size_t)n * kHCol, 0);
   // column-major numbering: columns ascending, rows ascending within a column (ldpc's order)
@@ -236,7 +316,7 @@ int hbm_prepare(qldpc_bp* bp) {
 
 size_t hbm_wave_bytes(const qldpc_bp* bp) {
   const size_t tsize = bp->precision == 32 ? 4 : 8;
-  const size_t b = (size_t)2 * bp->g->nnz * 64 * tsize + (size_t)(bp->g->n + bp->g->m) * 64;
+  const size_t b = (size_t)2 * bp->g->nnz * 64 * tsize + (size_t)bp->g->n * 64;
   return (b + 255) & ~(size_t)255;
 }
 
@@ -286,9 +366,11 @@ int hbm_decode_launch(qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int32_t*
   a.alpha = bp->alpha;
   QLDPC_HIP(hipMemsetAsync(bp->work.p, 0, 4, stream));
   if (bp->precision == 32)
-    hipLaunchKernelGGL(hdec_kernel<float>, dim3((unsigned)blocks), dim3(kHThreads), 0, stream, a);
+    hipLaunchKernelGGL(hdec_kernel<float>, dim3((unsigned)blocks), dim3(kHThreads), 0, stream, a, a.rp, a.rcol, a.rcpos,
+                       a.cp, a.crpos, a.llr);
   else
-    hipLaunchKernelGGL(hdec_kernel<double>, dim3((unsigned)blocks), dim3(kHThreads), 0, stream, a);
+    hipLaunchKernelGGL(hdec_kernel<double>, dim3((unsigned)blocks), dim3(kHThreads), 0, stream, a, a.rp, a.rcol,
+                       a.rcpos, a.cp, a.crpos, a.llr);
   QLDPC_HIP(hipGetLastError());
   return 0;
 }

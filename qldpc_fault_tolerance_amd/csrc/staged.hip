@@ -565,7 +565,11 @@ int staged_mc_prepare(qldpc_mc* mc, const qldpc_graph* logical_x, const qldpc_gr
   const qldpc_graph* L[2] = {logical_x, logical_z};
   const qldpc_bp* d0 = mc->dec[0] ? mc->dec[0] : mc->dec[1];
   const int n = d0->g->n;
-  const long long B = kStagedBatch;
+  // the HBM engine decodes one syndrome per lane: a batch of many syndromes per resident lane
+  // keeps its lanes refilled instead of waiting on the batch's slowest decode
+  const bool hbm = (mc->dec[0] && mc->dec[0]->engine == 6) || (mc->dec[1] && mc->dec[1]->engine == 6);
+  const char* eb = std::getenv("QLDPC_STAGED_BATCH");
+  long long B = (eb && *eb) ? std::max(64LL, std::atoll(eb) / 64 * 64) : (hbm ? kStagedBatch * 16 : kStagedBatch);
   const size_t W = (size_t)(B / 64);
   int mm = 1, rc;
   for (int q = 0; q < 2; ++q) {
