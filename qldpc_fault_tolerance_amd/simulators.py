@@ -661,6 +661,55 @@ class CodeFamily:
                                       data_synd_noise_ratio, circuit_type, circuit_error_params, if_plot=False)
         return ThresholdEst_extrapolation(eval_p_list, eval_wer_array, if_plot)
 
+    def EvalSustainableThreshold(self, noise_model: str, eval_logical_type: str, eval_method: str,
+                                 est_threshold: float, num_samples_per_cycle: int, num_cycles_list: list,
+                                 data_synd_noise_ratio=1, circuit_type="coloration", circuit_error_params=None,
+                                 if_plot=False):
+        """``src/Simulators.py:927-948``: the threshold at each cycle count (``num_samples_per_cycle /
+        num_cycles`` samples each), then ``FitSusThreshold`` -> the sustainable threshold p_sus."""
+        return _sustainable_threshold(self, noise_model, eval_logical_type, eval_method, est_threshold,
+                                      num_samples_per_cycle, num_cycles_list, data_synd_noise_ratio, circuit_type,
+                                      circuit_error_params, if_plot)
+
+    def EvalEffectiveDistances(self, noise_model: str, eval_logical_type: str, eval_method: str, est_threshold: float,
+                               num_samples: int, num_cycles=1, data_synd_noise_ratio=1, circuit_type="coloration",
+                               if_plot=False):
+        """``src/Simulators.py:951-963``: 5 log-spaced p in [p_th/6, p_th/4], then :func:`DistanceEst`."""
+        assert noise_model in ["data", "phenl", "circuit"], "noise_model should be one of [data, phenl, circuit]"
+        assert eval_logical_type in ["X", "Z", "Total"], "eval_type should be one of [X, Y, Total]"
+        assert eval_method in ["extrapolation"], "eval_method should be one of [extrapolation]"
+        eval_p_list = 10 ** (np.linspace(np.log10(est_threshold / 6), np.log10(est_threshold / 4), 5))
+        eval_wer_array = self.EvalWER(noise_model, eval_logical_type, eval_p_list, num_samples, num_cycles,
+                                      data_synd_noise_ratio, circuit_type, if_plot=False)
+        return DistanceEst(eval_p_list, eval_wer_array, if_plot)
+
+
+def FitSusThreshold(N, p_sus, p_0, gamma):
+    """Sustainable-threshold model of ``EvalSustainableThreshold`` (``src/Simulators.py:936-938``)."""
+    return p_sus * (1 - (1 - p_0 / p_sus) * np.exp(-gamma * N))
+
+
+def _sustainable_threshold(fam, noise_model, eval_logical_type, eval_method, est_threshold, num_samples_per_cycle,
+                           num_cycles_list, data_synd_noise_ratio, circuit_type, circuit_error_params, if_plot):
+    from scipy.optimize import curve_fit
+
+    sweep = [fam.EvalThreshold(noise_model=noise_model, eval_logical_type=eval_logical_type, eval_method=eval_method,
+                               est_threshold=est_threshold, num_samples=int(num_samples_per_cycle / c), num_cycles=c,
+                               data_synd_noise_ratio=data_synd_noise_ratio, circuit_type=circuit_type,
+                               circuit_error_params=circuit_error_params, if_plot=if_plot) for c in num_cycles_list]
+    popt, _ = curve_fit(FitSusThreshold, np.array(num_cycles_list), np.array(sweep), p0=(0.01, 0.05, 0.05))
+    if if_plot:
+        try:
+            import matplotlib.pyplot as plt
+
+            plt.figure()
+            plt.plot(num_cycles_list, sweep, "D")
+            plt.plot(num_cycles_list, FitSusThreshold(np.array(num_cycles_list), *popt), "-")
+            plt.close()
+        except ImportError:
+            pass
+    return popt[0]
+
 
 class CodeFamily_SpaceTime:
     """``src/Simulators_SpaceTime.py:1152-1309`` for the ``'data'`` and ``'phenl'`` noise models.
@@ -717,6 +766,43 @@ class CodeFamily_SpaceTime:
             eval_p_adapt_list.append(np.array(eval_p_list))
         return eval_wer_list, eval_p_adapt_list
 
+    def EvalThreshold(self, noise_model: str, eval_logical_type: str, eval_method: str, est_threshold: float,
+                      num_samples: int, num_cycles=1, data_synd_noise_ratio=1, circuit_type="coloration",
+                      circuit_error_params=None, if_plot=False):
+        """``src/Simulators_SpaceTime.py:1311-1324``.  As in the reference, ``data_synd_noise_ratio`` is
+        passed positionally into EvalWER's ``num_rep`` slot (quirk Q7); the WER list (first element of
+        EvalWER's pair; the reference hands the pair itself to the fit, which cannot work) is fitted."""
+        assert noise_model in ["data", "phenl", "circuit"], "noise_model should be one of [data, phenl, circuit]"
+        assert eval_logical_type in ["X", "Z", "Total"], "eval_type should be one of [X, Y, Total]"
+        assert eval_method in ["extrapolation"], "eval_method should be one of [extrapolation]"
+        eval_p_list = 10 ** (np.linspace(np.log10(est_threshold * 0.4), np.log10(est_threshold * 0.8), 6))
+        res = self.EvalWER(noise_model, eval_logical_type, eval_p_list, num_samples, num_cycles, data_synd_noise_ratio,
+                           circuit_type, circuit_error_params, if_plot=False)
+        wer = res[0] if isinstance(res, tuple) else res
+        return ThresholdEst_extrapolation(eval_p_list, np.array(wer), if_plot)
+
+    def EvalSustainableThreshold(self, noise_model: str, eval_logical_type: str, eval_method: str,
+                                 est_threshold: float, num_samples_per_cycle: int, num_cycles_list: list,
+                                 data_synd_noise_ratio=1, circuit_type="coloration", circuit_error_params=None,
+                                 if_plot=False):
+        """``src/Simulators_SpaceTime.py:1326-1347`` (same as CodeFamily's)."""
+        return _sustainable_threshold(self, noise_model, eval_logical_type, eval_method, est_threshold,
+                                      num_samples_per_cycle, num_cycles_list, data_synd_noise_ratio, circuit_type,
+                                      circuit_error_params, if_plot)
+
+    def EvalEffectiveDistances(self, noise_model: str, eval_logical_type: str, eval_method: str, est_threshold: float,
+                               num_samples: int, num_cycles=1, data_synd_noise_ratio=1, circuit_type="coloration",
+                               if_plot=False):
+        """``src/Simulators_SpaceTime.py:1350-1362`` (``data_synd_noise_ratio`` lands in ``num_rep``, Q7)."""
+        assert noise_model in ["data", "phenl", "circuit"], "noise_model should be one of [data, phenl, circuit]"
+        assert eval_logical_type in ["X", "Z", "Total"], "eval_type should be one of [X, Y, Total]"
+        assert eval_method in ["extrapolation"], "eval_method should be one of [extrapolation]"
+        eval_p_list = 10 ** (np.linspace(np.log10(est_threshold / 6), np.log10(est_threshold / 4), 5))
+        res = self.EvalWER(noise_model, eval_logical_type, eval_p_list, num_samples, num_cycles, data_synd_noise_ratio,
+                           circuit_type, if_plot=False)
+        wer = res[0] if isinstance(res, tuple) else res
+        return DistanceEst(eval_p_list, np.array(wer), if_plot)
+
 
 def _plot_wer(code_list, eval_p_list, eval_wer_array, num_cycles):
     try:
@@ -740,6 +826,13 @@ def _plot_wer(code_list, eval_p_list, eval_wer_array, num_cycles):
 
 
 # ------------------------------------------------------- threshold fitting
+
+
+def CriticalExponentFit(xdata_tuple, pc, nu, A, B, C):
+    """``src/Simulators.py:674-678`` (unused by the reference's estimators; kept for the API)."""
+    p, d = xdata_tuple
+    x = (p - pc) * d ** (1 / nu)
+    return A + B * x + C * x ** 2
 
 
 def EmpericalFit(xdata_tuple, pc, A):

@@ -5,6 +5,7 @@ Run in the build container only (``/root/reference`` is not on the GPU box):
     python tests/golden/make_golden.py          # reference_harness_n225.npz
     python tests/golden/make_golden.py phen     # reference_harness_phen_n225.npz
     python tests/golden/make_golden.py configs  # reference_harness_configs.npz (configs 2-5)
+    python tests/golden/make_golden.py fits     # reference_fits.npz (threshold tooling)
 
 The reference modules import third-party packages that are absent here
 (``graph_tools``, ``ldpc``, ``bposd``, ``stim``, …), so empty stub
@@ -390,10 +391,84 @@ def main_configs():
     print("wrote", path, len(out), "arrays")
 
 
+def main_fits():
+    """Threshold tooling -> tests/golden/reference_fits.npz.
+
+    Runs the reference's own fit functions (src/Simulators.py:675-741, 912-963;
+    src/Simulators_SpaceTime.py:1080-1149, 1311-1362) on fixed injected WER arrays: DistanceEst,
+    ThresholdEst_extrapolation, and CodeFamily{,_SpaceTime}.EvalThreshold / EvalSustainableThreshold /
+    EvalEffectiveDistances with EvalWER / EvalThreshold replaced by recorders returning the injected
+    data (the p grids they were called with are recorded too).
+    """
+    install_stubs()
+    import Simulators
+    import Simulators_SpaceTime
+    import matplotlib.pyplot as plt
+
+    plt.show = lambda *a, **k: None
+    out = {}
+    rng = np.random.default_rng(123)
+    d_true = np.array([4.0, 6.0, 8.0])
+    pc_true, A_true = 0.08, 0.3
+    # WER arrays [codes x p] from the extrapolation model, with 3 % multiplicative noise
+    p_thr = 10 ** np.linspace(np.log10(0.08 * 0.4), np.log10(0.08 * 0.8), 6)
+    wer_thr = np.array([A_true * (p_thr / pc_true) ** (d / 2) for d in d_true]) * (1 + 0.03 * rng.standard_normal((3, 6)))
+    p_dist = 10 ** np.linspace(np.log10(0.08 / 6), np.log10(0.08 / 4), 5)
+    wer_dist = np.array([0.5 * p_dist ** (d / 2) for d in d_true]) * (1 + 0.03 * rng.standard_normal((3, 5)))
+    out["thr_p"], out["thr_wer"], out["dist_p"], out["dist_wer"] = p_thr, wer_thr, p_dist, wer_dist
+    for mod, tag in ((Simulators, "sim"), (Simulators_SpaceTime, "st")):
+        out[f"{tag}_distance_est"] = np.array(mod.DistanceEst(p_thr, wer_thr))
+        out[f"{tag}_threshold_extrap"] = np.array([mod.ThresholdEst_extrapolation(p_thr, wer_thr)])
+    # CodeFamily.EvalThreshold / EvalEffectiveDistances with a recording EvalWER
+    seen = []
+
+    def rec_evalwer(data):
+        def f(self, noise_model, eval_logical_type, eval_p_list, *a, **k):
+            seen.append(np.array(eval_p_list, dtype=np.float64))
+            return data
+        return f
+
+    fam = Simulators.CodeFamily([], None, None)
+    Simulators.CodeFamily.EvalWER = rec_evalwer(wer_thr)
+    out["fam_eval_threshold"] = np.array([fam.EvalThreshold("data", "Total", "extrapolation", 0.08, 100)])
+    out["fam_eval_threshold_p"] = seen[-1]
+    Simulators.CodeFamily.EvalWER = rec_evalwer(wer_dist)
+    out["fam_eval_distances"] = np.array(fam.EvalEffectiveDistances("data", "Total", "extrapolation", 0.08, 100))
+    out["fam_eval_distances_p"] = seen[-1]
+    # EvalSustainableThreshold: EvalThreshold replaced by thresholds that saturate with the cycle count
+    cycles = np.array([1, 3, 5, 9, 15, 25])
+    thr = 0.03 * (1 - (1 - 0.06 / 0.03) * np.exp(-0.2 * cycles)) * (1 + 0.01 * rng.standard_normal(6))
+    calls = []
+
+    def rec_thr(self, noise_model, eval_logical_type, eval_method, est_threshold, num_samples, num_cycles=1, **k):
+        calls.append([num_samples, num_cycles])
+        return float(thr[list(cycles).index(num_cycles)])
+
+    out["sus_cycles"], out["sus_thr"] = cycles, thr
+    Simulators.CodeFamily.EvalThreshold = rec_thr
+    out["fam_sus"] = np.array([fam.EvalSustainableThreshold("phenl", "Total", "extrapolation", 0.05, 12000,
+                                                             list(cycles))])
+    out["fam_sus_calls"] = np.array(calls)
+    calls.clear()
+    stfam = Simulators_SpaceTime.CodeFamily_SpaceTime([], None, None)
+    Simulators_SpaceTime.CodeFamily_SpaceTime.EvalThreshold = rec_thr
+    out["st_sus"] = np.array([stfam.EvalSustainableThreshold("phenl", "Total", "extrapolation", 0.05, 12000,
+                                                              list(cycles))])
+    out["st_sus_calls"] = np.array(calls)
+    Simulators_SpaceTime.CodeFamily_SpaceTime.EvalWER = rec_evalwer(wer_dist)
+    out["st_eval_distances"] = np.array(stfam.EvalEffectiveDistances("phenl", "Total", "extrapolation", 0.08, 100))
+    out["st_eval_distances_p"] = seen[-1]
+    path = os.path.join(HERE, "reference_fits.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, len(out), "arrays")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "phen":
         main_phen()
     elif len(sys.argv) > 1 and sys.argv[1] == "configs":
         main_configs()
+    elif len(sys.argv) > 1 and sys.argv[1] == "fits":
+        main_fits()
     else:
         main()

@@ -215,3 +215,63 @@ def test_phenl_space_time_with_bposd_final_round(gpu):
     assert sim._engine_parts() is not None and all(o is not None for o in sim._final_osd())
     res = sim.fused_counts(rounds, 512)
     assert res.shots == 512
+
+
+def test_phen_single_shot_bpdecoder_bposd_notebook_config(gpu, oracle):
+    """The Threshold notebook's CodeFamilyPhenlThreshold pair: decoder1 = BPDecoder on [h | I],
+    decoder2 = BPOSD_Decoder osd_e(10).  CodeSimulator_Phenon routes it onto the fused
+    pipeline (qldpc_phenl_set_final_osd): the detector trace equals the oracle's (num_rep = 1) and
+    the BP-final-round run's, and per sample BP+OSD fails only where BP fails."""
+    from qldpc_fault_tolerance_amd.decoders import BP_Decoder_Class, BPOSD_Decoder_Class
+    from qldpc_fault_tolerance_amd.simulators import CodeSimulator_Phenon
+
+    code = codes.get_code("hgp_34_n225")
+    p, rounds, S = 0.02, 3, 1500
+    ext = lambda h: np.hstack([h, np.identity(h.shape[0])])  # noqa: E731
+    b1 = BP_Decoder_Class(10, "minimum_sum", 0.625)
+    d1 = {"p_data": p, "p_syndrome": p}
+
+    def sim(dec2_cls):
+        return CodeSimulator_Phenon(code, b1.GetDecoder({**d1, "h": ext(code.hz)}), b1.GetDecoder({**d1, "h": ext(code.hx)}),
+                                    dec2_cls.GetDecoder({"h": code.hz, "p_data": p}),
+                                    dec2_cls.GetDecoder({"h": code.hx, "p_data": p}), pauli_error_probs=[p / 2] * 3,
+                                    q=p, eval_logical_type="Total", seed=31)
+
+    s_osd = sim(BPOSD_Decoder_Class(10, "minimum_sum", 0.625, "osd_e", 10))
+    assert s_osd._engine_parts() is not None and all(o is not None for o in s_osd._final_osd())
+    s_bp = sim(b1)
+    from qldpc_fault_tolerance_amd.engine import DevicePhenl
+
+    runs = []
+    for s in (s_bp, s_osd):
+        ph = DevicePhenl(code, *s._engine_parts(), num_rep=1)
+        ox, oz = s._final_osd()
+        if ox is not None:
+            ph.set_final_osd(ox, oz)
+        runs.append(ph.run(p / 2, p / 2, p / 2, p, 31, 0, S, rounds, "Total", per_shot=True))
+    bp, bo = runs
+    ref = oracle.phenl_run(code, p / 2, p / 2, p / 2, p, 31, 0, S, rounds, 1, "Total", p_data=p, p_synd=p,
+                           per_shot=True)
+    assert np.array_equal(bp.trace, ref["trace"]) and np.array_equal(bp.fail, ref["fail"])
+    assert np.array_equal(bo.trace, bp.trace)
+    assert not np.any((bo.fail != 0) & (bp.fail == 0))
+    assert bo.failures <= bp.failures
+    # the drop-in's fused path returns the same count as the device run of the same stream
+    assert s_osd.fused_counts(rounds, S).failures == bo.failures
+
+
+def test_final_osd_graph_mismatch_is_rejected(gpu):
+    """qldpc_phenl_set_final_osd refuses an OSD handle built on another graph."""
+    from qldpc_fault_tolerance_amd import _native
+    from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceOSD, DevicePhenl
+
+    code = codes.get_code("hgp_34_n225")
+    p, n = 0.02, code.N
+    st = [DeviceBP(codes.space_time_csr(h, 1), np.full(n + h.shape[0], p), max_iter=22) for h in (code.hz, code.hx)]
+    d2x = DeviceBP(code.hz, p, max_iter=22, soft=True)
+    d2z = DeviceBP(code.hx, p, max_iter=22, soft=True)
+    ph = DevicePhenl(code, st[0], st[1], d2x, d2z, num_rep=1)
+    ox, oz = DeviceOSD(d2x.graph, np.full(n, p), "osd_e", 4), DeviceOSD(d2z.graph, np.full(n, p), "osd_e", 4)
+    with pytest.raises(_native.QldpcError, match="different graph"):
+        ph.set_final_osd(oz, ox)  # swapped sectors
+    ph.set_final_osd(ox, oz)

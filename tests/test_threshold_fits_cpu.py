@@ -1,0 +1,63 @@
+"""Threshold tooling against the reference's own fit functions.
+
+tests/golden/reference_fits.npz was produced by running the reference's DistanceEst,
+ThresholdEst_extrapolation and CodeFamily{,_SpaceTime}.EvalThreshold / EvalSustainableThreshold /
+EvalEffectiveDistances (src/Simulators.py:675-741, 912-963; src/Simulators_SpaceTime.py:1080-1149,
+1311-1362) on fixed injected WER arrays, with EvalWER / EvalThreshold replaced by recorders.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from qldpc_fault_tolerance_amd import simulators
+
+FITS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_fits.npz")
+
+
+@pytest.fixture(scope="module")
+def g():
+    return np.load(FITS, allow_pickle=False)
+
+
+def test_distance_and_threshold_extrapolation(g):
+    np.testing.assert_allclose(simulators.DistanceEst(g["thr_p"], g["thr_wer"]), g["sim_distance_est"], rtol=1e-9)
+    np.testing.assert_allclose(simulators.ThresholdEst_extrapolation(g["thr_p"], g["thr_wer"]),
+                               g["sim_threshold_extrap"][0], rtol=1e-9)
+
+
+def _recording(data, seen):
+    def f(self, noise_model, eval_logical_type, eval_p_list, *a, **k):
+        seen.append(np.array(eval_p_list, dtype=np.float64))
+        return data
+    return f
+
+
+@pytest.mark.parametrize("cls", [simulators.CodeFamily, simulators.CodeFamily_SpaceTime])
+def test_eval_threshold_and_effective_distances(g, monkeypatch, cls):
+    seen = []
+    st = cls is simulators.CodeFamily_SpaceTime
+    fam = cls([], None, None)
+    monkeypatch.setattr(cls, "EvalWER", _recording((list(g["thr_wer"]), None) if st else g["thr_wer"], seen))
+    np.testing.assert_allclose(fam.EvalThreshold("data", "Total", "extrapolation", 0.08, 100),
+                               g["fam_eval_threshold"][0], rtol=1e-9)
+    np.testing.assert_allclose(seen[-1], g["fam_eval_threshold_p"], rtol=0, atol=0)
+    monkeypatch.setattr(cls, "EvalWER", _recording((list(g["dist_wer"]), None) if st else g["dist_wer"], seen))
+    want = g["st_eval_distances"] if st else g["fam_eval_distances"]
+    np.testing.assert_allclose(fam.EvalEffectiveDistances("data", "Total", "extrapolation", 0.08, 100), want, rtol=1e-9)
+    np.testing.assert_allclose(seen[-1], g["st_eval_distances_p" if st else "fam_eval_distances_p"], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("cls,key", [(simulators.CodeFamily, "fam"), (simulators.CodeFamily_SpaceTime, "st")])
+def test_sustainable_threshold(g, monkeypatch, cls, key):
+    cycles, thr = list(g["sus_cycles"]), g["sus_thr"]
+    calls = []
+
+    def rec(self, noise_model, eval_logical_type, eval_method, est_threshold, num_samples, num_cycles=1, **k):
+        calls.append([num_samples, num_cycles])
+        return float(thr[cycles.index(num_cycles)])
+
+    monkeypatch.setattr(cls, "EvalThreshold", rec)
+    p_sus = cls([], None, None).EvalSustainableThreshold("phenl", "Total", "extrapolation", 0.05, 12000, cycles)
+    np.testing.assert_allclose(p_sus, g[f"{key}_sus"][0], rtol=1e-9)
+    assert calls == g[f"{key}_sus_calls"].tolist()
