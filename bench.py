@@ -272,8 +272,9 @@ def phenl_main(a, torch, dist, world, rank, dev):
 def bposd_main(a, torch, dist, world, rank, dev):
     """BP+OSD shot loop (not the headline): CodeSimulator_DataError with
     BPOSD_Decoder_Class(max_iter_ratio, "minimum_sum", 0.625, "osd_e", 10) sectors, as the notebooks
-    build them.  One step = ``--shots`` shots per GPU through ``bposd_counts``: the fused GPU shot
-    loop, then GPU soft BP + the native OSD stage on the non-converged shots (host threads)."""
+    build them.  One step = ``--shots`` shots per GPU through ``bposd_counts``: one fused engine-3
+    launch per batch that captures the non-converged decodes on the device, the GPU OSD stage on
+    those and the device re-check of their failures (no host round trips but the candidate count)."""
     from qldpc_fault_tolerance_amd import codes
     from qldpc_fault_tolerance_amd.decoders import BPOSD_Decoder_Class
     from qldpc_fault_tolerance_amd.simulators import CodeSimulator_DataError
@@ -315,7 +316,9 @@ def bposd_main(a, torch, dist, world, rank, dev):
         "osd_decodes": osd_n, "osd_frac_of_decodes": osd_n / max(1, 2 * shots),
         "logical_error_rate": fails / max(shots, 1),
         "roofline": None,
-        "note": "wall clock of fused GPU MC + GPU soft BP + GPU OSD (osd_gpu_kernel) on the non-converged decodes + host bookkeeping",
+        "note": "wall clock of the device-resident BP+OSD loop: fused engine-3 MC capturing the decodes that reach "
+                "max_iter (posteriors, syndrome, error), GPU OSD (osd_gpu_kernel) on those, device re-check of their "
+                "residuals (qldpc_mc_set_osd)",
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

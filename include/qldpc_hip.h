@@ -255,6 +255,15 @@ int qldpc_bp_degree3_slots(const qldpc_bp *bp, int32_t *d3k);
 int qldpc_bp_create_hbm(qldpc_graph *g, const double *channel_probs, int32_t max_iter, double ms_scaling_factor,
                         int32_t precision, qldpc_bp **out);
 
+/* BP+OSD in the fused shot loop (bposd_decoder per sector, src/Decoders.py:26-41, inside
+ * _single_run, src/Simulators.py:117-168): after qldpc_mc_set_osd, qldpc_mc_launch captures
+ * every decode that reaches max_iter (its last-iteration posteriors, syndrome and sampled
+ * error) on the device, runs the GPU OSD stage (qldpc_osd_gpu) on those, re-checks their
+ * residual against H and the logicals, and corrects the per-shot fail flags and the failure
+ * counters -- no host copies beyond the per-sector candidate counts.  Engine-3 MC handles
+ * only; each OSD handle must be built on its sector decoder's graph (NULL = plain BP). */
+int qldpc_mc_set_osd(qldpc_mc *mc, qldpc_osd_gpu *osd_x, qldpc_osd_gpu *osd_z);
+
 /* Engine 3: extra LDS cycles of one variable-phase pass's CS gathers (summed
  * over gather instructions and lane groups: distinct checks on one bank beyond
  * the first) with the identity check order (`before`) and with the labels the

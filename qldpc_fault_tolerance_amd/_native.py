@@ -23,7 +23,7 @@ EXPORTED = [
     "qldpc_phenl_trace_len", "qldpc_phenl_launch", "qldpc_bp_degree3_slots", "qldpc_bp_create_soft",
     "qldpc_bp_decode_batch_soft", "qldpc_osd_create", "qldpc_osd_destroy", "qldpc_osd_rank",
     "qldpc_osd_decode_batch", "qldpc_osd_gpu_create", "qldpc_osd_gpu_destroy", "qldpc_osd_gpu_decode", "qldpc_phenl_set_final_osd",
-    "qldpc_bp_bank_stats", "qldpc_bp_create_hbm",
+    "qldpc_bp_bank_stats", "qldpc_bp_create_hbm", "qldpc_mc_set_osd",
 ]
 
 
@@ -106,6 +106,8 @@ def _declare(L):
     L.qldpc_phenl_set_final_osd.argtypes = [_vp, _vp, _vp]
     L.qldpc_mc_create.restype = ctypes.c_int
     L.qldpc_mc_create.argtypes = [_vp, _vp, _vp, _vp, _pp]
+    L.qldpc_mc_set_osd.restype = ctypes.c_int
+    L.qldpc_mc_set_osd.argtypes = [_vp, _vp, _vp]
     L.qldpc_mc_destroy.restype = ctypes.c_int
     L.qldpc_mc_destroy.argtypes = [_vp]
     L.qldpc_mc_launch.restype = ctypes.c_int

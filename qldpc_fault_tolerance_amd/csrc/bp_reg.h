@@ -192,7 +192,8 @@ __device__ inline void r_gather(unsigned char* smem, const RState<T, DMAX, VPL, 
 template <typename T, int DMAX, int VPL, int ND, int ENG>
 __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, int k,
                                  const typename CSEntry<T>::type (&pr)[DMAX],
-                                 const typename FT<T>::U (&o)[DMAX], uint32_t fdelta, T alpha, bool xprev) {
+                                 const typename FT<T>::U (&o)[DMAX], uint32_t fdelta, T alpha, bool xprev,
+                                 double* post, const int32_t* perm) {
   using U = typename FT<T>::U;
   constexpr U kS = FT<T>::kSign;
   constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
@@ -246,6 +247,10 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     acc = acc + c[t];
   }
   const bool x = acc <= (T)0;
+  if (post) {  // BP+OSD capture (last iteration): ldpc's log_prob_ratios, the OSD sort key
+    const int j = *perm;
+    if (j >= 0) post[j] = (double)acc;
+  }
   T b = c[ND - 1];
   U nv[ND];
   nv[ND - 1] = canon2<T>(f[ND - 1]);
@@ -269,7 +274,8 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
 
 template <typename T, int DMAX, int VPL, int D3K, int ENG>
 __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, uint32_t fdelta, T alpha,
-                                 uint32_t xprev, bool last_live) {
+                                 uint32_t xprev, bool last_live, double* post = nullptr, const int32_t* perm = nullptr,
+                                 int TB = 0) {
   using U = typename FT<T>::U;
   constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
   constexpr int N3 = DMAX > 3 ? 3 : DMAX;  // low-degree slots use 3 edge slots
@@ -298,8 +304,9 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     }
     if (k == VPL - 1 && !last_live) break;  // every lane of this wave holds padding
     const bool xp = ((xprev >> k) & 1u) != 0;
-    const bool x = k < D3K ? r_var_one<T, DMAX, VPL, N3, ENG>(smem, R, k, pr, o, fdelta, alpha, xp)
-                           : r_var_one<T, DMAX, VPL, DMAX, ENG>(smem, R, k, pr, o, fdelta, alpha, xp);
+    const int32_t* pk = perm ? perm + k * TB : nullptr;
+    const bool x = k < D3K ? r_var_one<T, DMAX, VPL, N3, ENG>(smem, R, k, pr, o, fdelta, alpha, xp, post, pk)
+                           : r_var_one<T, DMAX, VPL, DMAX, ENG>(smem, R, k, pr, o, fdelta, alpha, xp, post, pk);
     xbits |= (x ? 1u : 0u) << k;
   }
   return xbits;
@@ -737,8 +744,19 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     int it = 1;
     bool conv = false;
     uint32_t xb = 0;
+    long long cslot = -1;  // BP+OSD capture slot of this decode (claimed at its last iteration)
     while (true) {
       int mism;
+      double* cpost = nullptr;
+      if constexpr (MC && eng_base(ENG) == 3) {
+        if (A->c_n && A->c_post[q] && it >= S.max_iter) {  // uniform: the last iteration may end unconverged
+          __shared__ unsigned int s_cslot;
+          if (tid == 0) s_cslot = atomicAdd(&A->c_n[q], 1u);
+          __syncthreads();
+          cslot = (long long)s_cslot;
+          if (cslot < A->c_cap) cpost = A->c_post[q] + cslot * (long long)n;
+        }
+      }
       if constexpr (eng_base(ENG) == 4) {
         xb = c_var<T, DMAX, VPL>(smem, R, M, last_live);
         __syncthreads();
@@ -747,7 +765,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         mism = c_check_any<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha);
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
-        xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live);
+        xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
         __syncthreads();
         // check state for iteration it + 1 (float: pre-scaled by its alpha)
         const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
@@ -765,6 +783,21 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       ++it;
     }
     const long long sl = c0 + sh;
+    if (MC && cslot >= 0 && cslot < A->c_cap) {
+      // BP+OSD candidate: syndrome (original check order), sampled error, shot
+      if (!conv) {
+        uint8_t* cs = A->c_synd[q] + cslot * (long long)m;
+        int qq = 0;
+        for (int i = tidl; i < m; i += TB, ++qq) cs[S.rperm ? S.rperm[i] : i] = (uint8_t)((sb >> qq) & 1u);
+        uint8_t* ce = A->c_err[q] + cslot * (long long)n;
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+          const int j = S.perm[k * TB + tidl];
+          if (j >= 0) ce[j] = (uint8_t)((eb >> k) & 1u);
+        }
+      }
+      if (tid == 0) A->c_shot[q][cslot] = conv ? -1 : sl;
+    }
     if (MC) {
       // residual r = e ^ x and its logical syndrome L r (src/Simulators.py:135-160)
       const uint32_t r = eb ^ xb;

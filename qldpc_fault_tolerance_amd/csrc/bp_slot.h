@@ -66,6 +66,15 @@ struct SMcArgs {
   uint8_t* corr;
   int* iters;
   unsigned int* work;  // engine 3: chunk queue head (zeroed per launch), NULL = static chunk striding
+  // BP+OSD capture (engine 3, qldpc_mc_set_osd): every decode that reaches max_iter claims a slot
+  // of its sector q and leaves its last-iteration posteriors, syndrome, sampled error and shot
+  // index there; c_n == NULL disables it
+  unsigned int* c_n;      // [2] slots claimed per sector (zeroed per launch)
+  double* c_post[2];      // [cap][n]
+  uint8_t* c_synd[2];     // [cap][m]
+  uint8_t* c_err[2];      // [cap][n]
+  long long* c_shot[2];   // [cap] launch-relative shot, -1 = converged at max_iter (no OSD)
+  long long c_cap;
 };
 
 struct SDecArgs {

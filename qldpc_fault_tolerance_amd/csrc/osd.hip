@@ -613,7 +613,76 @@ struct qldpc_osd_gpu {
   qldpc_rt::DevBuf rp, ci, ws, iws;
 };
 
+namespace {
+
+// BP+OSD failure re-check of the fused shot loop's candidates (qldpc_mc_set_osd): per
+// candidate, the residual r = e ^ x_osd against H (src/Simulators.py:139-160: a syndrome
+// mismatch counts as a failure) and the logical operators (column masks, as the MC kernel uses);
+// a sector verdict the OSD turned into a success clears that sector's bit of the shot's fail
+// flags and takes the shot out of the sector / total failure counters.
+__global__ void __launch_bounds__(256) osd_recheck_kernel(const int32_t* rp, const int32_t* ci, int m, int n,
+                                                          const unsigned long long* lmask, int kw, const uint8_t* err,
+                                                          const uint8_t* outw, const long long* shot, long long ncand,
+                                                          int q, int logical_mode, uint8_t* fail,
+                                                          unsigned long long* counters) {
+  __shared__ uint32_t lsyn[8];
+  __shared__ int hbad;
+  const int tid = threadIdx.x;
+  for (long long b = blockIdx.x; b < ncand; b += gridDim.x) {
+    const long long s = shot[b];
+    if (s < 0) continue;  // converged at max_iter: the BP verdict stands (uniform)
+    if (tid < 8) lsyn[tid] = 0;
+    if (tid == 0) hbad = 0;
+    __syncthreads();
+    const uint8_t* e = err + b * (long long)n;
+    const uint8_t* x = outw + b * (long long)n;
+    for (int j = tid; j < n; j += blockDim.x)
+      if ((e[j] ^ x[j]) & 1u)
+        for (int w = 0; w < kw; ++w) {
+          const unsigned long long v = lmask[(long long)j * kw + w];
+          if ((uint32_t)v) atomicXor(&lsyn[2 * w], (uint32_t)v);
+          if ((uint32_t)(v >> 32)) atomicXor(&lsyn[2 * w + 1], (uint32_t)(v >> 32));
+        }
+    for (int i = tid; i < m; i += blockDim.x) {
+      uint32_t par = 0;
+      for (int k = rp[i]; k < rp[i + 1]; ++k) par ^= (uint32_t)(e[ci[k]] ^ x[ci[k]]);
+      if (par & 1u) hbad = 1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t any = (uint32_t)hbad;
+      for (int w = 0; w < 8; ++w) any |= lsyn[w];
+      if (!any) {
+        const uint32_t old = fail[s], nw = old & ~(1u << q);
+        fail[s] = (uint8_t)nw;
+        atomicAdd(&counters[8 + q], ~0ull);  // sector failures - 1
+        auto tot = [&](uint32_t f) { return logical_mode == 0 ? (f & 1u) : logical_mode == 1 ? (f >> 1) & 1u : (f != 0); };
+        if (tot(old) && !tot(nw)) atomicAdd(&counters[1], ~0ull);  // failures - 1
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
 namespace qldpc_rt {
+// BP+OSD stage of the fused shot loop for one sector: GPU OSD on the ncand captured
+// candidates, then the failure re-check (osd_recheck_kernel).
+int osd_gpu_bposd_stage(qldpc_osd_gpu* osd, const uint8_t* synd, const double* post, const uint8_t* err,
+                        const long long* shot, uint8_t* outw, long long ncand, const unsigned long long* lmask, int kw,
+                        int q, int logical_mode, uint8_t* fail, unsigned long long* counters, hipStream_t stream) {
+  if (ncand <= 0) return 0;
+  int rc = qldpc_osd_gpu_decode(osd, synd, post, nullptr, nullptr, nullptr, outw, ncand, stream);
+  if (rc) return rc;
+  const int grid = (int)std::min<long long>(ncand, 4096);
+  hipLaunchKernelGGL(osd_recheck_kernel, dim3(grid), dim3(256), 0, stream, static_cast<const int32_t*>(osd->rp.p),
+                     static_cast<const int32_t*>(osd->ci.p), osd->host.m, osd->host.n, lmask, kw, err, outw, shot,
+                     ncand, q, logical_mode, fail, counters);
+  QLDPC_HIP(hipGetLastError());
+  return 0;
+}
+
 // true when the GPU OSD handle was built on exactly this graph (shape and edges)
 bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g) {
   return o && g && o->host.m == g->m && o->host.n == g->n && o->host.col_rows == g->col_rows;

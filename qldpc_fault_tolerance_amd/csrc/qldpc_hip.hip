@@ -1069,8 +1069,28 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   return 0;
 }
 
+int qldpc_mc_set_osd(qldpc_mc* mc, qldpc_osd_gpu* osd_x, qldpc_osd_gpu* osd_z) {
+  if (!mc) return set_err(QLDPC_EINVAL, "NULL mc");
+  qldpc_osd_gpu* o[2] = {osd_x, osd_z};
+  for (int q = 0; q < 2; ++q) {
+    if (!o[q]) continue;
+    if (mc->staged || mc->engine != 3)
+      return set_err(QLDPC_ENOTSUP, "BP+OSD shot loop needs the fused engine-3 MC kernel");
+    if (!mc->dec[q] || !osd_gpu_matches(o[q], mc->dec[q]->g))
+      return set_err(QLDPC_EINVAL, q == 0 ? "X-sector OSD handle was built on a different graph than dec_x"
+                                          : "Z-sector OSD handle was built on a different graph than dec_z");
+  }
+  mc->osd[0] = osd_x;
+  mc->osd[1] = osd_z;
+  return 0;
+}
+
 int qldpc_mc_destroy(qldpc_mc* mc) {
   if (!mc) return 0;
+  for (int q = 0; q < 2; ++q)
+    for (DevBuf* d : {&mc->c_post[q], &mc->c_synd[q], &mc->c_err[q], &mc->c_shot[q], &mc->c_outw[q]}) d->release();
+  mc->c_n.release();
+  mc->c_fail.release();
   mc->lmask[0].release();
   mc->lmask[1].release();
   mc->counters.release();
@@ -1162,8 +1182,55 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.fail = d_fail; a.err = d_err; a.corr = d_corr; a.iters = d_iters;
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
+    // BP+OSD: capture buffers sized for every decode of the launch
+    const bool bposd = (need[0] && mc->osd[0]) || (need[1] && mc->osd[1]);
+    hipStream_t st = (hipStream_t)stream;
+    if (bposd) {
+      if (mc->c_cap < shot_count) {
+        for (int q = 0; q < 2; ++q) {
+          for (DevBuf* d : {&mc->c_post[q], &mc->c_synd[q], &mc->c_err[q], &mc->c_shot[q], &mc->c_outw[q]}) d->release();
+          if (!mc->dec[q] || !mc->osd[q]) continue;
+          const int n = mc->dec[q]->g->n, m = mc->dec[q]->g->m;
+          int rc;
+          if ((rc = mc->c_post[q].alloc((size_t)shot_count * n * 8)) || (rc = mc->c_synd[q].alloc((size_t)shot_count * m)) ||
+              (rc = mc->c_err[q].alloc((size_t)shot_count * n)) || (rc = mc->c_shot[q].alloc((size_t)shot_count * 8)) ||
+              (rc = mc->c_outw[q].alloc((size_t)shot_count * n)))
+            return rc;
+        }
+        mc->c_fail.release();
+        int rc;
+        if ((rc = mc->c_fail.alloc((size_t)shot_count)) || (!mc->c_n.p && (rc = mc->c_n.alloc(16)))) return rc;
+        mc->c_cap = shot_count;
+      }
+      QLDPC_HIP(hipMemsetAsync(mc->c_n.p, 0, 16, st));
+      a.c_n = static_cast<unsigned int*>(mc->c_n.p);
+      a.c_cap = shot_count;
+      for (int q = 0; q < 2; ++q) {
+        const bool on = need[q] && mc->osd[q];
+        a.c_post[q] = on ? static_cast<double*>(mc->c_post[q].p) : nullptr;
+        a.c_synd[q] = on ? static_cast<uint8_t*>(mc->c_synd[q].p) : nullptr;
+        a.c_err[q] = on ? static_cast<uint8_t*>(mc->c_err[q].p) : nullptr;
+        a.c_shot[q] = on ? static_cast<long long*>(mc->c_shot[q].p) : nullptr;
+      }
+      if (!a.fail) a.fail = static_cast<uint8_t*>(mc->c_fail.p);  // per-shot verdicts the OSD stage revises
+    }
     SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch);
-    QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, (hipStream_t)stream, a));
+    QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, st, a));
+    if (bposd) {
+      unsigned int nc[4] = {0, 0, 0, 0};
+      QLDPC_HIP(hipMemcpyAsync(nc, mc->c_n.p, 16, hipMemcpyDeviceToHost, st));
+      QLDPC_HIP(hipStreamSynchronize(st));
+      for (int q = 0; q < 2; ++q) {
+        if (!(need[q] && mc->osd[q]) || nc[q] == 0) continue;
+        const long long ncand = std::min<long long>(nc[q], a.c_cap);
+        int rc = osd_gpu_bposd_stage(mc->osd[q], static_cast<const uint8_t*>(mc->c_synd[q].p),
+                                     static_cast<const double*>(mc->c_post[q].p), static_cast<const uint8_t*>(mc->c_err[q].p),
+                                     static_cast<const long long*>(mc->c_shot[q].p), static_cast<uint8_t*>(mc->c_outw[q].p),
+                                     ncand, static_cast<const unsigned long long*>(mc->lmask[q].p), mc->kw[q], q,
+                                     logical_mode, a.fail, static_cast<unsigned long long*>(d_counters), st);
+        if (rc) return rc;
+      }
+    }
   }
   return 0;
 }

@@ -93,6 +93,10 @@ struct qldpc_mc {
   // staged pipeline (staged.hip): product-sum decoders, or QLDPC_MC_STAGED=1
   bool staged = false;
   long long sbatch = 0;
+  // BP+OSD (qldpc_mc_set_osd): GPU OSD per sector on the decodes that reached max_iter
+  qldpc_osd_gpu* osd[2] = {nullptr, nullptr};
+  long long c_cap = 0;
+  qldpc_rt::DevBuf c_post[2], c_synd[2], c_err[2], c_shot[2], c_outw[2], c_n, c_fail;
   int sm[2] = {0, 0}, sk[2] = {0, 0};
   qldpc_rt::DevBuf s_rp[2], s_ci[2], s_cur[2], s_failw[2], s_D, s_det, s_corr, s_iters, s_conv;
 };
@@ -108,6 +112,10 @@ int ps_decode_launch(const qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int
 
 // GPU OSD handle built on this graph? (osd.hip; qldpc_phenl_set_final_osd checks it)
 bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g);
+// BP+OSD stage of the fused shot loop, one sector (osd.hip)
+int osd_gpu_bposd_stage(qldpc_osd_gpu* osd, const uint8_t* synd, const double* post, const uint8_t* err,
+                        const long long* shot, uint8_t* outw, long long ncand, const unsigned long long* lmask, int kw,
+                        int q, int logical_mode, uint8_t* fail, unsigned long long* counters, hipStream_t stream);
 
 // engine 6 (bp_hbm.hip)
 int hbm_prepare(qldpc_bp* bp);

@@ -378,6 +378,13 @@ class DeviceMC:
             "qldpc_mc_create")
         self.handle = h
 
+    def set_osd(self, osd_x: "DeviceOSD | None", osd_z: "DeviceOSD | None"):
+        """BP+OSD in the fused loop (``qldpc_mc_set_osd``): decodes that reach max_iter go through the
+        GPU OSD stage and their failures are re-checked on the device."""
+        self._osd = (osd_x, osd_z)  # keep the handles alive
+        _native.check(_native.lib().qldpc_mc_set_osd(self.handle, osd_x.handle if osd_x is not None else None,
+                                                     osd_z.handle if osd_z is not None else None), "qldpc_mc_set_osd")
+
     def new_counters(self):
         torch = _torch()
         return torch.zeros(_native.COUNTER_WORDS, dtype=torch.int64, device=torch.device("cuda", self.device))

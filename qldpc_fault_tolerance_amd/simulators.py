@@ -209,22 +209,75 @@ class CodeSimulator_DataError:
         need_z = self.eval_logical_type != "X"
         return (not need_x or _is_bposd(self.decoder_x)) and (not need_z or _is_bposd(self.decoder_z))
 
-    def bposd_counts(self, num_run: int, batch: int = 16384, keep_shots: bool = False):
+    def bposd_counts(self, num_run: int, batch: int = 1 << 18, keep_shots: bool = False):
         """``num_run`` shots with BPOSD_Decoder sectors (the notebooks' decoder,
         src/Decoders.py:26-41) -> (failures, shots, osd_decodes), all-reduced.
 
-        Per batch, the fused GPU shot loop samples the Philox errors, forms the
-        syndromes and runs BP with the BPOSD decoders' own (soft-capable) BP,
-        handing back per-shot errors and BP corrections.  Shots whose BP
-        correction leaves a syndrome mismatch (BP did not converge) are
-        re-decoded with BP+OSD (GPU soft BP, bit-identical to the first BP, then
-        the native OSD stage) and their failure re-checked; converged shots keep
-        the fused verdict, exactly as ``bposd_decoder`` returns the BP decoding
-        when BP converges.  ``keep_shots`` stores ``last_shots`` =
-        (errors [S, n] bit0 x / bit1 z, sector failures [S, 2]) of the run.
+        Device-resident when both sectors' OSD runs on the GPU (uniform priors, every reference
+        call site): per batch ONE fused launch samples, decodes with engine-3 BP built on the
+        BPOSD decoders' own graphs and parameters, captures every decode that reaches max_iter
+        without converging (its posteriors, syndrome and error), runs the GPU OSD stage on those
+        and re-checks their residuals, all on the device (``qldpc_mc_set_osd``); converged decodes
+        keep the BP verdict, exactly as ``bposd_decoder`` returns the BP decoding when BP
+        converges.  Otherwise the host-assisted path below.  ``keep_shots`` stores ``last_shots``
+        = (errors [S, n] bit0 x / bit1 z, sector failures [S, 2]).
         """
         if not self._bposd_ready():
             raise TypeError("bposd_counts needs BPOSD_Decoder instances for the sectors eval_logical_type uses")
+        need_x = self.eval_logical_type != "Z"
+        need_z = self.eval_logical_type != "X"
+        decs = [d for d, need in ((self.decoder_x, need_x), (self.decoder_z, need_z)) if need]
+        if all(getattr(d, "gpu_osd", None) is not None for d in decs):
+            return self._bposd_counts_device(num_run, batch, keep_shots, need_x, need_z)
+        return self._bposd_counts_host(num_run, min(int(batch), 16384), keep_shots)
+
+    def _bposd_counts_device(self, num_run, batch, keep_shots, need_x, need_z):
+        from .engine import DeviceBP, DeviceMC, MCResult, _torch
+
+        torch = _torch()
+        if self.seed is None:
+            self.seed = random.getrandbits(64)
+        if getattr(self, "_bposd_dev", None) is None:
+            def fast(dec, vpl=0):
+                b = dec.decoder  # the soft (engine-1) BP: same graph, priors, max_iter, alpha, precision
+                return DeviceBP(None, b.channel_probs, max_iter=b.max_iter, bp_method="minimum_sum",
+                                ms_scaling_factor=b.ms_scaling_factor, precision=b.precision, graph=b.graph,
+                                vars_per_thread=vpl)
+
+            bx = fast(self.decoder_x) if need_x else None
+            # one fused kernel serves both sectors: the Z sector takes the X sector's geometry
+            bz = fast(self.decoder_z, bx.geometry()["vars_per_thread"] if bx is not None else 0) if need_z else None
+            mc = DeviceMC(self.code, bx, bz)
+            mc.set_osd(self.decoder_x.gpu_osd if need_x else None, self.decoder_z.gpu_osd if need_z else None)
+            self._bposd_dev = mc
+        mc = self._bposd_dev
+        rank, ws = parallel.world()
+        b, c = parallel.shard_range(num_run, rank, ws, begin=self._shot_offset)
+        self._shot_offset += int(num_run)
+        px, py, pz = self.channel_probs
+        dev = torch.device("cuda", mc.device)
+        cnt = mc.new_counters()
+        kept_e, kept_f = [], []
+        for s0 in range(b, b + c, int(batch)):
+            S = min(int(batch), b + c - s0)
+            f_d = e_d = None
+            if keep_shots:
+                f_d = torch.zeros(S, dtype=torch.uint8, device=dev)
+                e_d = torch.zeros((S, self.N), dtype=torch.uint8, device=dev)
+            mc.launch(px, py, pz, self.seed, s0, S, self.eval_logical_type, cnt, None, f_d, e_d)
+            if keep_shots:
+                f = f_d.cpu().numpy()
+                kept_e.append(e_d.cpu().numpy())
+                kept_f.append(np.stack([(f & 1) != 0, (f & 2) != 0], axis=1))
+        if keep_shots:
+            self.last_shots = (np.concatenate(kept_e) if kept_e else None, np.concatenate(kept_f) if kept_f else None)
+        parallel.allreduce_counters(cnt)
+        res = MCResult.from_words(cnt.cpu().numpy())
+        self.last_result = res
+        return res.failures, res.shots, int(sum(res.sector_nonconv))
+
+    def _bposd_counts_host(self, num_run: int, batch: int = 16384, keep_shots: bool = False):
+        """Host-assisted BP+OSD loop (non-uniform priors: the OSD half runs on the host stage)."""
         from .engine import DeviceMC, _torch
 
         torch = _torch()
