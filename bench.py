@@ -107,6 +107,10 @@ def kernel_name(dec):
             and nch in (3, 4) and os.environ.get("QLDPC_F64W", "1") != "0":
         # fp64 family for <= 256-thread workgroups (engine id 103, launch bounds 256, rows of nch chunks)
         return f"qldpc::rmc_kernel<double, 4, {g['vars_per_thread']}, 103, {g['degree3_slots']}, 256, {nch}>"
+    if g["engine"] == 3 and dec.precision == 32 and dmax == 4 and 5 <= g["vars_per_thread"] <= 8 and nch == 2 \
+            and os.environ.get("QLDPC_F32W", "1") != "0":
+        # fp32 family with the compile-time 2-chunk check phase
+        return f"qldpc::rmc_kernel<float, 4, {g['vars_per_thread']}, 3, {g['degree3_slots']}, 1024, 2>"
     if g["engine"] >= 3:
         return f"qldpc::rmc_kernel<{t}, {dmax}, {g['vars_per_thread']}, {g['engine']}, {g['degree3_slots']}>"
     return f"qldpc::smc_kernel<{t}, {dmax}, 1> (engine {g['engine']})"

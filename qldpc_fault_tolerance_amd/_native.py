@@ -11,7 +11,7 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libqldpc_hip.so")
+LIB_PATH = os.environ.get("QLDPC_LIB") or os.path.join(PKG_DIR, "libqldpc_hip.so")
 HIST_BINS = 1025
 
 # Every symbol include/qldpc_hip.h declares (tests check the .so exports them).

@@ -40,21 +40,25 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
 
-def build_native(force: bool = False, verbose: bool = True) -> str:
+def build_native(force: bool = False, verbose: bool = True, out: str | None = None,
+                 defines: tuple = ()) -> str:
+    """Build the engine; ``out``/``defines`` build a side variant for A/B timing
+    (tools/build_variant.py; loaded through ``QLDPC_LIB``)."""
+    OUT = out or globals()["OUT"]
     srcs = sources()
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     deps.append(os.path.join(REPO, "include", "qldpc_hip.h"))
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     hipcc = _hipcc()
-    objdir = os.path.join(PKG_DIR, "build")
+    objdir = os.path.join(PKG_DIR, "build" if out is None else "build_" + os.path.basename(OUT).replace(".so", ""))
     os.makedirs(objdir, exist_ok=True)
     procs = []
     objs = []
     for s in srcs:
         o = os.path.join(objdir, os.path.basename(s).replace(".hip", ".o"))
         objs.append(o)
-        cmd = [hipcc, *HIPCC_FLAGS, "-c", s, "-o", o]
+        cmd = [hipcc, *HIPCC_FLAGS, *("-D" + d for d in defines), "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append(subprocess.Popen(cmd))

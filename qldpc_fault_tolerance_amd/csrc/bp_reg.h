@@ -31,6 +31,16 @@
 // write a sink.  Image: [V: zero chunk + m rows][F (m+1): bit0 (H x)_i, bit1
 // syndrome, bits 16.. row degree][sink 16][lred 8][flags 2].
 #pragma once
+
+#ifndef QLDPC_TID_LAUNDER
+#define QLDPC_TID_LAUNDER 1
+#endif
+// Diagnostic build only (tools/build_variant.py ... QLDPC_STAMPS=1): s_memtime stamps at the
+// phase boundaries of the fused MC pass, summed per wave into SMcArgs::stamps.  Never on in
+// the shipped library; its run times are not quoted (the stamps' waits forbid overlaps).
+#ifndef QLDPC_STAMPS
+#define QLDPC_STAMPS 0
+#endif
 #include "bp_slot.h"
 
 namespace qldpc {
@@ -48,6 +58,17 @@ template <typename T, int ENG>
 constexpr int lb_waves(int LB) {
   // engine 4 fp64 images (no CS array) fit 3 workgroups per CU: <= 168 VGPRs
   return LB <= 256 ? (sizeof(T) == 8 ? (eng_base(ENG) == 4 ? 3 : 2) : 4) : 1;
+}
+__device__ inline unsigned long long qstamp() {
+#if QLDPC_STAMPS
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+#else
+  return 0;
+#endif
 }
 template <int ENG>
 __device__ inline uint32_t ea_cs(uint32_t ea) { return (ea & 0xFFFFu) << eng_sh(ENG); }
@@ -106,6 +127,22 @@ __device__ inline typename FT<T>::U canon2(T v) {
   }
 }
 
+// Engine 3 keeps its messages NEGATED ("w domain"): w = -v for every prior, v2c and c2v,
+// except that a zero prior is +0.  Then every w is either exactly -v (v != 0) or +0 (v
+// == 0: an exact cancellation rounds to +0, and a sum is -0 only when all its leaves are
+// -0, which a +0-or-nonzero prior rules out), so the sign bit of w is exactly NOT the
+// canonical sign (v <= 0) the min-sum parity needs: the v2c leave-one-out sums are stored
+// as they come out of the adds (no canon2 per edge), the decision is w >= 0, and the
+// check phase flips its parity by the row degree (F bit 2, folded into the syndrome bit it
+// keeps per row), which turns the xor of the w signs back into the xor of the canonical
+// ones.  -w is the c2v product with the same sign rule, so the c2v arithmetic is unchanged.
+template <typename T>
+__device__ inline T w_prior(T l) {
+  using U = typename FT<T>::U;
+  const U b = FT<T>::bits(-l);
+  return FT<T>::val(b == FT<T>::kSign ? (U)0 : b);  // -(+0) = -0 -> +0
+}
+
 // x is +0 or -0 (v_cmp_class_*: class bits 5 = -0, 6 = +0)
 __device__ inline bool is_zero(float x) { return __builtin_amdgcn_classf(x, 0x60); }
 __device__ inline bool is_zero(double x) { return __builtin_amdgcn_class(x, 0x60); }
@@ -143,7 +180,8 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
       else
         R.ea[k][t] = ((echk(e) * (uint32_t)(2 * sizeof(T))) >> eng_sh(ENG)) | ((va >> eng_sh(ENG)) << 16);
     }
-    R.L[k] = (S.perm[k * TB + tid] >= 0) ? llr[k * TB + tid] : (T)1;
+    const T l = (S.perm[k * TB + tid] >= 0) ? llr[k * TB + tid] : (T)1;
+    R.L[k] = eng_base(ENG) == 3 ? w_prior<T>(l) : l;  // engine 3: w domain
   }
 }
 
@@ -246,17 +284,17 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     f[t] = acc;
     acc = acc + c[t];
   }
-  const bool x = acc <= (T)0;
+  const bool x = acc >= (T)0;  // w domain: v <= 0
   if (post) {  // BP+OSD capture (last iteration): ldpc's log_prob_ratios, the OSD sort key
     const int j = *perm;
-    if (j >= 0) post[j] = (double)acc;
+    if (j >= 0) post[j] = -(double)acc;  // (a zero's sign may differ: the OSD sort ties +-0)
   }
   T b = c[ND - 1];
   U nv[ND];
-  nv[ND - 1] = canon2<T>(f[ND - 1]);
+  nv[ND - 1] = FT<T>::bits(f[ND - 1]);  // w domain: stored as computed (no canon2)
 #pragma unroll
   for (int t = ND - 2; t >= 0; --t) {
-    nv[t] = canon2<T>(f[t] + b);
+    nv[t] = FT<T>::bits(f[t] + b);
     if (t > 0) b = b + c[t];
   }
 #pragma unroll
@@ -329,9 +367,11 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
     const uint32_t f = F;
     uint32_t s;
     if (FIRST) {
-      s = (f >> 1) & 1u;
+      // w domain: the kept bit is syndrome ^ row-degree parity (F bit 2), and F bit 0 =
+      // (H x) ^ that parity starts at the parity, so mism below compares like for like
+      s = ((f >> 1) ^ (f >> 2)) & 1u;
       sbits |= s << q;
-      F = 0;  // H x starts at 0; the variable phases keep it current
+      F = (f & 4u) | ((f >> 2) & 1u);  // H x starts at 0; the variable phases keep it current
     } else {
       s = (sbits >> q) & 1u;
       mism |= (int)((f ^ s) & 1u);
@@ -421,9 +461,9 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
     }
     uint32_t s;
     if (FIRST) {
-      s = (fcur >> 1) & 1u;
+      s = ((fcur >> 1) ^ (fcur >> 2)) & 1u;  // as r_check: syndrome ^ row-degree parity
       sbits |= s << q;
-      lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1)) = 0;  // H x starts at 0; the variable phases keep it current
+      lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1)) = (fcur & 4u) | ((fcur >> 2) & 1u);
     } else {
       s = (sbits >> q) & 1u;
       mism |= (int)((fcur ^ s) & 1u);
@@ -607,7 +647,10 @@ __device__ inline void r_fill(const SSector& S, unsigned char* smem, const RLayo
   // engine 4: the first chunk is the zero chunk missing edges read
   for (int i = tid; i < vslots / V16<T>::N; i += TB) V4[i] = (eng_base(ENG) == 4 && i == 0) ? V16<T>::splat((T)0) : s;
   uint32_t* F = reinterpret_cast<uint32_t*>(smem + Ly.f);
-  for (int i = tid; i <= mmax; i += TB) F[i] = (eng_base(ENG) == 4 && i >= 1 && i <= S.m) ? ((uint32_t)S.rdeg[i - 1] << 16) : 0u;
+  // engine 4: row degree in the high half; engine 3: row-degree parity in bit 2 (w domain)
+  for (int i = tid; i <= mmax; i += TB)
+    F[i] = (i >= 1 && i <= S.m) ? (eng_base(ENG) == 4 ? ((uint32_t)S.rdeg[i - 1] << 16) : (((uint32_t)S.rdeg[i - 1] & 1u) << 2))
+                                : 0u;
   uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);
   if (tid < 10) lred[tid] = 0;  // lred[0..7], flags[0..1]
   if (eng_base(ENG) == 3 && tid == 0) {
@@ -637,9 +680,15 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   using U = typename FT<T>::U;
   constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
   const int m = S.m, n = S.n, nch = S.nch;
+  // Re-derive tid-based table addresses in every pass: without the opaque copy the
+  // compiler hoists ~20 64-bit addresses out of the chunk loop and spills them.
+  int tidp = tid;
+#if QLDPC_TID_LAUNDER
+  asm volatile("" : "+v"(tidp));
+#endif
   RState<T, DMAX, VPL, ENG> R;
-  r_load<T, DMAX, VPL, ENG>(S, R, Ly, tid, TB);
-  r_fill<T, ENG>(S, smem, Ly, vslots, mmax, tid, TB);
+  r_load<T, DMAX, VPL, ENG>(S, R, Ly, tidp, TB);
+  r_fill<T, ENG>(S, smem, Ly, vslots, mmax, tidp, TB);
   FMap M;
   M.fbase = eng_base(ENG) == 4 ? Ly.f + 4u : Ly.f;
   M.rstart = Ly.v + 16u;
@@ -654,6 +703,10 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   __syncthreads();
 
   int pshot = -1, pit = 0, pconv = 0;
+  // QLDPC_STAMPS: [0] variable phase, [1] its barrier, [2] check phase, [3] flags + barrier,
+  // [4] shot setup (priors, sampling, first check), [5] epilogue, [6] iterations, [7] shots
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_a = qstamp();
   for (int sh = 0; sh <= cn; ++sh) {
     const bool have = sh < cn;
     uint32_t eb = 0, sb = 0;
@@ -664,7 +717,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     if (have) {
 #pragma unroll
       for (int k = 0; k < VPL; ++k) {
-        const U cl = canon2<T>(R.L[k]);
+        const U cl = FT<T>::bits(R.L[k]);  // w domain: the prior as is
 #pragma unroll
         for (int t = 0; t < DMAX; ++t) {
           lds_at<U>(smem, ea_v<ENG>(R.ea[k][t])) = cl;
@@ -701,7 +754,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         for (int i = tidl; i < m; i += TB) {  // i = check label (engine 3: S.rperm maps it to the check)
           uint32_t& F = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
           const int oi = S.rperm ? S.rperm[i] : i;
-          F = (eng_base(ENG) == 4 ? (F & 0xFFFF0000u) : 0u) | ((uint32_t)(srow[oi] & 1u) << 1);
+          F = (eng_base(ENG) == 4 ? (F & 0xFFFF0000u) : (F & 4u)) | ((uint32_t)(srow[oi] & 1u) << 1);
         }
       }
     }
@@ -740,6 +793,12 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       r_check<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     __syncthreads();
     if (tid < 10) lred[tid] = 0;  // lred read above (before the barrier); flags[0..1] start clear
+    if (QLDPC_STAMPS) {
+      const unsigned long long t = qstamp();
+      st_acc[4] += t - st_a;
+      st_acc[7] += 1;
+      st_a = t;
+    }
     // ---------------------------------------------------------- iterations
     int it = 1;
     bool conv = false;
@@ -766,16 +825,36 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
         xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
+        unsigned long long t1 = 0;
+        if (QLDPC_STAMPS) {
+          t1 = qstamp();
+          st_acc[0] += t1 - st_a;
+        }
         __syncthreads();
+        if (QLDPC_STAMPS) {
+          st_a = qstamp();
+          st_acc[1] += st_a - t1;
+        }
         // check state for iteration it + 1 (float: pre-scaled by its alpha)
         const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
         if constexpr (NCH > 0)
           mism = r_check_c<T, false, NCH>(smem, Ly, m, tid, TB, sb);
         else
           mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha_next);
+        if (QLDPC_STAMPS) {
+          const unsigned long long t = qstamp();
+          st_acc[2] += t - st_a;
+          st_a = t;
+        }
       }
       if (__any(mism) && (tid & 63) == 0) flags[it & 1] = 1u;
       __syncthreads();
+      if (QLDPC_STAMPS) {
+        const unsigned long long t = qstamp();
+        st_acc[3] += t - st_a;
+        st_acc[6] += 1;
+        st_a = t;
+      }
       const int any = uni((int)flags[it & 1]);
       if (tid == 0) flags[(it & 1) ^ 1] = 0;  // read by everyone before this barrier
       conv = any == 0;
@@ -788,7 +867,9 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       if (!conv) {
         uint8_t* cs = A->c_synd[q] + cslot * (long long)m;
         int qq = 0;
-        for (int i = tidl; i < m; i += TB, ++qq) cs[S.rperm ? S.rperm[i] : i] = (uint8_t)((sb >> qq) & 1u);
+        for (int i = tidl; i < m; i += TB, ++qq)  // sb holds syndrome ^ row-degree parity (F bit 2)
+          cs[S.rperm ? S.rperm[i] : i] =
+              (uint8_t)(((sb >> qq) ^ (lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1)) >> 2)) & 1u);
         uint8_t* ce = A->c_err[q] + cslot * (long long)n;
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
@@ -835,6 +916,15 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     pshot = sh;
     pit = conv ? it : S.max_iter;
     pconv = conv ? 1 : 0;
+    if (QLDPC_STAMPS) {
+      const unsigned long long t = qstamp();
+      st_acc[5] += t - st_a;
+      st_a = t;
+    }
+  }
+  if (QLDPC_STAMPS && MC && A->stamps && (tid & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(&A->stamps[k], st_acc[k]);
   }
   __syncthreads();  // image reused by the next pass
 }

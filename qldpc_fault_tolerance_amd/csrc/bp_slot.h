@@ -43,7 +43,7 @@ struct SSector {
   const uint32_t* edges;            // [VPL][DMAX][TB]
   const void* llr;                  // T [VPL][TB]
   const unsigned long long* lmask;  // [n][kw] logical-row masks per column (MC only)
-  const uint8_t* rdeg;              // [m] row degrees (engine 4 only)
+  const uint8_t* rdeg;              // [m] row degrees by check label (engines 3, 4)
   const int32_t* perm;              // [VPL][TB] variable of each slot, -1 = padding (engines 3/4)
   const int32_t* rperm;             // [m] original check of each check label (engine 3), NULL = identity
   int m, n, kw, max_iter, nch, vpl; // nch = 16-byte chunks per row; vpl = variables per thread
@@ -75,6 +75,7 @@ struct SMcArgs {
   uint8_t* c_err[2];      // [cap][n]
   long long* c_shot[2];   // [cap] launch-relative shot, -1 = converged at max_iter (no OSD)
   long long c_cap;
+  unsigned long long* stamps;  // diagnostic builds (QLDPC_STAMPS): per-segment cycle sums, else NULL
 };
 
 struct SDecArgs {

@@ -73,10 +73,28 @@ bool use_f64w(int engine, int precision, int dmax, int tb, int vpl, int ea_shift
          (nch == 3 || nch == 4) && env_int("QLDPC_F64W", 1) != 0;
 }
 
+// fp32 engine-3 kernels with the compile-time 2-chunk check phase (rows of <= 8 edges);
+// QLDPC_F32W=0 falls back to the runtime-width check loop.
+bool use_f32w(int engine, int precision, int dmax, int tb, int vpl, int ea_shift, int nch) {
+  (void)tb;
+  return engine == 3 && precision == 32 && dmax == 4 && ea_shift == 0 && vpl >= 5 && vpl <= 8 && nch == 2 &&
+         env_int("QLDPC_F32W", 1) != 0;
+}
+
+#if QLDPC_STAMPS
+// diagnostic build: phase-cycle sums of the fused MC kernels (bp_reg.h, QLDPC_STAMPS)
+unsigned long long* debug_stamps_buffer() {
+  static unsigned long long* buf = nullptr;
+  if (!buf && hipMalloc(&buf, 8 * sizeof(unsigned long long)) == hipSuccess) (void)hipMemset(buf, 0, 64);
+  return buf;
+}
+#endif
+
 // Slot-family kernels of an engine (2, 3 or 4).
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
                       int nch = 0) {
   if (use_f64w(engine, precision, dmax, tb, vpl, ea_shift, nch)) return get_rvariant_f64_w(vpl, d3k, nch);
+  if (use_f32w(engine, precision, dmax, tb, vpl, ea_shift, nch)) return get_rvariant_f32_w(vpl, d3k);
   if (engine == 4 && precision == 64 && tb <= 256 && vpl >= 4) return get_r4variant_f64_w(vpl);
   if (engine == 3 && ea_shift == 2)
     return (precision == 32 && dmax == 4) ? get_rvariant_f32_big(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
@@ -205,6 +223,15 @@ int device_cus(int dev, int& cus) {
 
 // ================================================================== C ABI
 extern "C" {
+
+#if QLDPC_STAMPS
+// diagnostic builds only (not in include/qldpc_hip.h): read and clear the phase-cycle sums
+int qldpc_debug_stamps(unsigned long long* out) {
+  unsigned long long* b = debug_stamps_buffer();
+  if (!b || hipDeviceSynchronize() != hipSuccess || hipMemcpy(out, b, 64, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return hipMemset(b, 0, 64) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int qldpc_abi_version(void) { return QLDPC_ABI_VERSION; }
 
@@ -781,6 +808,14 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     }
     build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab);
     kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch).dec_k;
+    if (bp->engine >= 3) {
+      // row degrees by check label: engine 4 keeps them in F, engine 3 their parity (bp_reg.h, w domain)
+      std::vector<uint8_t> deg(std::max(1, g->m));
+      for (int i = 0; i < g->m; ++i) deg[lab.empty() ? i : lab[i]] = (uint8_t)(g->row_ptr[i + 1] - g->row_ptr[i]);
+      if ((rc = bp->rdeg.alloc(deg.size()))) return fail(rc);
+      if (hipMemcpy(bp->rdeg.p, deg.data(), deg.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(set_err(QLDPC_EHIP, "upload row degrees"));
+    }
   }
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
   if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)bp->VPL * bp->TB * tsize))) return fail(rc);
@@ -791,13 +826,6 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     if ((rc = bp->perm.alloc(bp->slot_var.size() * 4))) return fail(rc);
     if (hipMemcpy(bp->perm.p, bp->slot_var.data(), bp->slot_var.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       return fail(set_err(QLDPC_EHIP, "upload slot map"));
-  }
-  if (bp->engine == 4) {
-    std::vector<uint8_t> deg(std::max(1, g->m));
-    for (int i = 0; i < g->m; ++i) deg[i] = (uint8_t)(g->row_ptr[i + 1] - g->row_ptr[i]);
-    if ((rc = bp->rdeg.alloc(deg.size()))) return fail(rc);
-    if (hipMemcpy(bp->rdeg.p, deg.data(), deg.size(), hipMemcpyHostToDevice) != hipSuccess)
-      return fail(set_err(QLDPC_EHIP, "upload row degrees"));
   }
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, bp->TB, bp->lds_bytes) != hipSuccess) nb = 1;
@@ -1180,6 +1208,9 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.uniforms = d_uniforms;
     a.counters = static_cast<unsigned long long*>(d_counters);
     a.fail = d_fail; a.err = d_err; a.corr = d_corr; a.iters = d_iters;
+#if QLDPC_STAMPS
+    a.stamps = debug_stamps_buffer();
+#endif
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
     // BP+OSD: capture buffers sized for every decode of the launch

@@ -62,7 +62,7 @@ struct qldpc_bp {
   int lds_bytes = 0, blocks_per_cu = 0, cus = 0;
   std::vector<double> probs;
   qldpc_rt::DevBuf vchk, llr;  // engine 1: packed u16 check ids; engines 2-4: edge words (check | slot<<16)
-  qldpc_rt::DevBuf rdeg;       // engine 4: u8 row degrees
+  qldpc_rt::DevBuf rdeg;       // engines 3/4: u8 row degrees (by check label)
   qldpc_rt::DevBuf work;       // engine 3 decode_batch: chunk-queue head
   // engines 3/4: variable of each (k, t) slot (-1 = padding).  Engine 3 sorts
   // degree <= 3 variables first so that slots k < d3k skip the 4th edge slot.
