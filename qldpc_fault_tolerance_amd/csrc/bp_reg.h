@@ -106,6 +106,51 @@ template <typename T>
 __device__ inline T& lds_at(unsigned char* smem, uint32_t off) {
   return *reinterpret_cast<T*>(smem + off);
 }
+// LDS access by absolute address (no add of the dynamic-LDS base per access)
+template <typename X>
+using LdsPtr = __attribute__((address_space(3))) X*;
+__device__ inline uint32_t lds_base(unsigned char* smem) {
+  return (uint32_t)(uintptr_t)(LdsPtr<unsigned char>)smem;
+}
+// load / store of an LDS word at `a`: absolute address (ABS) or offset from smem
+// (through a same-size clang vector: the message structs have no address-space copy)
+template <int B>
+struct LdsWord;
+template <>
+struct LdsWord<4> {
+  typedef uint32_t type;
+};
+template <>
+struct LdsWord<8> {
+  typedef uint32_t type __attribute__((ext_vector_type(2)));
+};
+template <>
+struct LdsWord<16> {
+  typedef uint32_t type __attribute__((ext_vector_type(4)));
+};
+template <typename X, bool ABS>
+__device__ inline X lds_ld(unsigned char* smem, uint32_t a) {
+  if constexpr (ABS) {
+    using W = typename LdsWord<sizeof(X)>::type;
+    const W w = *(LdsPtr<const W>)(uintptr_t)a;
+    X x;
+    __builtin_memcpy(&x, &w, sizeof(X));
+    return x;
+  } else {
+    return lds_at<X>(smem, a);
+  }
+}
+template <typename X, bool ABS>
+__device__ inline void lds_st(unsigned char* smem, uint32_t a, X v) {
+  if constexpr (ABS) {
+    using W = typename LdsWord<sizeof(X)>::type;
+    W w;
+    __builtin_memcpy(&w, &v, sizeof(X));
+    *(LdsPtr<W>)(uintptr_t)a = w;
+  } else {
+    lds_at<X>(smem, a) = v;
+  }
+}
 
 // canonical bits: |v| with the sign bit := (v <= 0).  Only +0 differs from the
 // raw bits (-0 and negatives already carry the sign bit; NaN never occurs).
@@ -161,13 +206,34 @@ template <typename T, int DMAX, int VPL, int ENG = 3>
 struct RState {
   using U = typename FT<T>::U;
   static constexpr bool kKeepV = eng_base(ENG) == 3 && (sizeof(T) == 4 || eng_kv64(ENG));  // own v2c in VGPRs
+  // the fp64 <= 256-thread family (256-VGPR budget) keeps the two addresses of an edge
+  // unpacked and absolute (ea = CS address, ev = V slot address): no unpack / base add
+  // per access, 2 VALU per edge and iteration fewer
+  static constexpr bool kSplit = eng_kv64(ENG) && sizeof(T) == 8;
   uint32_t ea[VPL][DMAX];
+  uint32_t ev[kSplit ? VPL : 1][kSplit ? DMAX : 1];
   T L[VPL];
   U ov[kKeepV ? VPL : 1][kKeepV ? DMAX : 1];
 };
+// CS / V slot address of edge (k, t): absolute when split, else offsets from smem
+template <typename T, int DMAX, int VPL, int ENG>
+__device__ inline uint32_t r_csa(const RState<T, DMAX, VPL, ENG>& R, int k, int t) {
+  if constexpr (RState<T, DMAX, VPL, ENG>::kSplit)
+    return R.ea[k][t];
+  else
+    return ea_cs<ENG>(R.ea[k][t]);
+}
+template <typename T, int DMAX, int VPL, int ENG>
+__device__ inline uint32_t r_va(const RState<T, DMAX, VPL, ENG>& R, int k, int t) {
+  if constexpr (RState<T, DMAX, VPL, ENG>::kSplit)
+    return R.ev[k][t];
+  else
+    return ea_v<ENG>(R.ea[k][t]);
+}
 
 template <typename T, int DMAX, int VPL, int ENG>
-__device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, const RLayout& Ly, int tid, int TB) {
+__device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, const RLayout& Ly, int tid, int TB,
+                              uint32_t sbase) {
   const T* llr = static_cast<const T*>(S.llr);
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
@@ -175,10 +241,14 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
     for (int t = 0; t < DMAX; ++t) {
       const uint32_t e = S.edges[(k * DMAX + t) * TB + tid];
       const uint32_t va = Ly.v + eslot(e) * (uint32_t)sizeof(T);
-      if (eng_base(ENG) == 4)
+      if (eng_base(ENG) == 4) {
         R.ea[k][t] = e == kNoEdgeS ? (Ly.v | (Ly.sink << 16)) : (va | (va << 16));
-      else
+      } else if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) {
+        R.ea[k][t] = sbase + echk(e) * (uint32_t)(2 * sizeof(T));
+        R.ev[k][t] = sbase + va;
+      } else {
         R.ea[k][t] = ((echk(e) * (uint32_t)(2 * sizeof(T))) >> eng_sh(ENG)) | ((va >> eng_sh(ENG)) << 16);
+      }
     }
     const T l = (S.perm[k * TB + tid] >= 0) ? llr[k * TB + tid] : (T)1;
     R.L[k] = eng_base(ENG) == 3 ? w_prior<T>(l) : l;  // engine 3: w domain
@@ -198,6 +268,12 @@ __device__ inline uint32_t f_addr(uint32_t ea, const FMap& M) {
   if (eng_base(ENG) == 4) return M.fbase + 4u * (uint32_t)((int)((ea & 0xFFFFu) - M.rstart) >> M.rsh);
   return (ea_cs<ENG>(ea) >> (sizeof(T) == 4 ? 1 : 2)) + M.fbase;
 }
+// F word offset of edge (k, t) (engine 3); split addresses are absolute: fbase is then
+// Ly.f - (LDS base >> 2)
+template <typename T, int DMAX, int VPL, int ENG>
+__device__ inline uint32_t r_fa(const RState<T, DMAX, VPL, ENG>& R, int k, int t, uint32_t fbase) {
+  return (r_csa(R, k, t) >> (sizeof(T) == 4 ? 1 : 2)) + fbase;
+}
 
 // Opaque redefinition of the edge words (no instruction): without it the
 // compiler hoists their derived CS / V / F addresses out of the iteration and
@@ -207,7 +283,10 @@ __device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
 #pragma unroll
   for (int k = 0; k < VPL; ++k)
 #pragma unroll
-    for (int t = 0; t < DMAX; ++t) asm volatile("" : "+v"(R.ea[k][t]));
+    for (int t = 0; t < DMAX; ++t) {
+      asm volatile("" : "+v"(R.ea[k][t]));
+      if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) asm volatile("" : "+v"(R.ev[k][t]));
+    }
 }
 
 // Variable phase (one flooding iteration's column pass).  Returns decision bits.
@@ -220,10 +299,11 @@ __device__ inline void r_gather(unsigned char* smem, const RState<T, DMAX, VPL, 
                                 typename CSEntry<T>::type (&pn)[DMAX],
                                 typename FT<T>::U (&on)[DMAX]) {
   constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
+  constexpr bool SP = RState<T, DMAX, VPL, ENG>::kSplit;
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
-    pn[t] = lds_at<typename CSEntry<T>::type>(smem, ea_cs<ENG>(R.ea[k][t]));
-    if (!KV) on[t] = FT<T>::bits(lds_at<T>(smem, ea_v<ENG>(R.ea[k][t])));
+    pn[t] = lds_ld<typename CSEntry<T>::type, SP>(smem, r_csa(R, k, t));
+    if (!KV) on[t] = FT<T>::bits(lds_ld<T, SP>(smem, r_va(R, k, t)));
   }
 }
 
@@ -299,13 +379,12 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   }
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
-    lds_at<U>(smem, ea_v<ENG>(R.ea[k][t])) = nv[t];
+    lds_st<U, RState<T, DMAX, VPL, ENG>::kSplit>(smem, r_va(R, k, t), nv[t]);
     if (KV) R.ov[KV ? k : 0][KV ? t : 0] = nv[t];
   }
   if (x != xprev) {
 #pragma unroll
-    for (int t = 0; t < ND; ++t)
-      atomicXor(&lds_at<uint32_t>(smem, (ea_cs<ENG>(R.ea[k][t]) >> (sizeof(T) == 4 ? 1 : 2)) + fdelta), 1u);
+    for (int t = 0; t < ND; ++t) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), 1u);
   }
   return x;
 }
@@ -687,13 +766,16 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   asm volatile("" : "+v"(tidp));
 #endif
   RState<T, DMAX, VPL, ENG> R;
-  r_load<T, DMAX, VPL, ENG>(S, R, Ly, tidp, TB);
+  constexpr bool SP = RState<T, DMAX, VPL, ENG>::kSplit;
+  const uint32_t sbase = lds_base(smem);
+  r_load<T, DMAX, VPL, ENG>(S, R, Ly, tidp, TB, sbase);
   r_fill<T, ENG>(S, smem, Ly, vslots, mmax, tidp, TB);
   FMap M;
   M.fbase = eng_base(ENG) == 4 ? Ly.f + 4u : Ly.f;
   M.rstart = Ly.v + 16u;
   M.rsh = 4 + __builtin_ctz((unsigned)nch);
-  const uint32_t fdelta = Ly.f;
+  if (SP) M.fbase = Ly.f - (sbase >> 2);  // split: absolute CS addresses (16-byte aligned base)
+  const uint32_t fdelta = eng_base(ENG) == 4 ? Ly.f : M.fbase;
   // waves whose lanes all hold padding variables skip the last variable (engine 4)
   const bool last_live = uni((VPL - 1) * TB + (tid & ~63) < n ? 1 : 0) != 0;
   uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);
@@ -704,8 +786,9 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
 
   int pshot = -1, pit = 0, pconv = 0;
   // QLDPC_STAMPS: [0] variable phase, [1] its barrier, [2] check phase, [3] flags + barrier,
-  // [4] shot setup (priors, sampling, first check), [5] epilogue, [6] iterations, [7] shots
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // [4] shot setup (priors, sampling), [5] epilogue, [6] iterations, [7] shots,
+  // [8] setup barrier + previous decode's bookkeeping, [9] first check pass + barrier
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_a = qstamp();
   for (int sh = 0; sh <= cn; ++sh) {
     const bool have = sh < cn;
@@ -720,7 +803,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         const U cl = FT<T>::bits(R.L[k]);  // w domain: the prior as is
 #pragma unroll
         for (int t = 0; t < DMAX; ++t) {
-          lds_at<U>(smem, ea_v<ENG>(R.ea[k][t])) = cl;
+          lds_st<U, SP>(smem, r_va(R, k, t), cl);
           if (KV) R.ov[KV ? k : 0][KV ? t : 0] = cl;
         }
       }
@@ -728,9 +811,14 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         // sample this shot's Pauli error (src/Simulators.py:99-113); stage s = H e in F bit1
         const long long sl = c0 + sh;
         const unsigned long long gshot = A->shot_begin + (unsigned long long)sl;
+        // the slot map first, in one batch: inside the loop its loads would queue behind the
+        // err stores (u8, may alias) and wait out one memory latency per variable
+        int jv[VPL];
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) jv[k] = S.perm[k * TB + tidl];
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
-          const int j = S.perm[k * TB + tidl];
+          const int j = jv[k];
           if (j >= 0) {
             uint32_t cls;
             if (A->uniforms) {
@@ -745,7 +833,8 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
             if (A->err && q == A->sec_id0) A->err[sl * (long long)n + j] = (uint8_t)cls;
             if (e) {
 #pragma unroll
-              for (int t = 0; t < DMAX; ++t) atomicXor(&lds_at<uint32_t>(smem, f_addr<T, ENG>(R.ea[k][t], M)), 2u);
+              for (int t = 0; t < DMAX; ++t)
+                atomicXor(&lds_at<uint32_t>(smem, eng_base(ENG) == 4 ? f_addr<T, ENG>(R.ea[k][t], M) : r_fa(R, k, t, M.fbase)), 2u);
             }
           }
         }
@@ -757,6 +846,11 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
           F = (eng_base(ENG) == 4 ? (F & 0xFFFF0000u) : (F & 4u)) | ((uint32_t)(srow[oi] & 1u) << 1);
         }
       }
+    }
+    if (QLDPC_STAMPS) {
+      const unsigned long long t = qstamp();
+      st_acc[4] += t - st_a;
+      st_a = t;
     }
     __syncthreads();
     // ---------------------------------------------------------- finish the previous decode
@@ -784,6 +878,11 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       }
     }
     if (!have) break;
+    if (QLDPC_STAMPS) {
+      const unsigned long long t = qstamp();
+      st_acc[8] += t - st_a;
+      st_a = t;
+    }
     // ---------------------------------------------------------- first check pass (CS / c2v from priors)
     if constexpr (eng_base(ENG) == 4)
       c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
@@ -795,7 +894,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     if (tid < 10) lred[tid] = 0;  // lred read above (before the barrier); flags[0..1] start clear
     if (QLDPC_STAMPS) {
       const unsigned long long t = qstamp();
-      st_acc[4] += t - st_a;
+      st_acc[9] += t - st_a;
       st_acc[7] += 1;
       st_a = t;
     }
@@ -880,23 +979,34 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       if (tid == 0) A->c_shot[q][cslot] = conv ? -1 : sl;
     }
     if (MC) {
-      // residual r = e ^ x and its logical syndrome L r (src/Simulators.py:135-160)
+      // residual r = e ^ x and its logical syndrome L r (src/Simulators.py:135-160): the
+      // wave's rows of L r are gathered in batches (slot map, then masks), xor-reduced
+      // across the wave, and lane 0 folds them into lred (one LDS atomic per word and wave)
       const uint32_t r = eb ^ xb;
-      if (r) {
-        unsigned long long acc[4] = {0, 0, 0, 0};
+      if (__any(r != 0)) {
+        int jv[VPL];
 #pragma unroll
-        for (int k = 0; k < VPL; ++k) {
-          if ((r >> k) & 1u) {
-            const int j = S.perm[k * TB + tidl];
-#pragma unroll
-            for (int w = 0; w < 4; ++w)
-              if (w < S.kw) acc[w] ^= S.lmask[(long long)j * S.kw + w];
-          }
-        }
+        for (int k = 0; k < VPL; ++k) jv[k] = ((r >> k) & 1u) ? S.perm[k * TB + tidl] : -1;
+        const int kw = S.kw;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          if ((uint32_t)acc[w]) atomicXor(&lred[2 * w], (uint32_t)acc[w]);
-          if ((uint32_t)(acc[w] >> 32)) atomicXor(&lred[2 * w + 1], (uint32_t)(acc[w] >> 32));
+          if (w >= kw) break;  // uniform
+          unsigned long long lm[VPL];
+#pragma unroll
+          for (int k = 0; k < VPL; ++k) lm[k] = jv[k] >= 0 ? S.lmask[(long long)jv[k] * kw + w] : 0ull;
+          unsigned long long a = 0;
+#pragma unroll
+          for (int k = 0; k < VPL; ++k) a ^= lm[k];
+          uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            lo ^= (uint32_t)__shfl_xor((int)lo, o);
+            hi ^= (uint32_t)__shfl_xor((int)hi, o);
+          }
+          if ((tid & 63) == 0) {
+            if (lo) atomicXor(&lred[2 * w], lo);
+            if (hi) atomicXor(&lred[2 * w + 1], hi);
+          }
         }
       }
       if (A->corr) {
@@ -924,7 +1034,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   }
   if (QLDPC_STAMPS && MC && A->stamps && (tid & 63) == 0) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) atomicAdd(&A->stamps[k], st_acc[k]);
+    for (int k = 0; k < 10; ++k) atomicAdd(&A->stamps[k], st_acc[k]);
   }
   __syncthreads();  // image reused by the next pass
 }

@@ -85,7 +85,7 @@ bool use_f32w(int engine, int precision, int dmax, int tb, int vpl, int ea_shift
 // diagnostic build: phase-cycle sums of the fused MC kernels (bp_reg.h, QLDPC_STAMPS)
 unsigned long long* debug_stamps_buffer() {
   static unsigned long long* buf = nullptr;
-  if (!buf && hipMalloc(&buf, 8 * sizeof(unsigned long long)) == hipSuccess) (void)hipMemset(buf, 0, 64);
+  if (!buf && hipMalloc(&buf, 10 * sizeof(unsigned long long)) == hipSuccess) (void)hipMemset(buf, 0, 80);
   return buf;
 }
 #endif
@@ -228,8 +228,8 @@ extern "C" {
 // diagnostic builds only (not in include/qldpc_hip.h): read and clear the phase-cycle sums
 int qldpc_debug_stamps(unsigned long long* out) {
   unsigned long long* b = debug_stamps_buffer();
-  if (!b || hipDeviceSynchronize() != hipSuccess || hipMemcpy(out, b, 64, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return hipMemset(b, 0, 64) == hipSuccess ? 0 : -1;
+  if (!b || hipDeviceSynchronize() != hipSuccess || hipMemcpy(out, b, 80, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return hipMemset(b, 0, 80) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -39,6 +39,29 @@ def test_decode_batch_matches_oracle(gpu, oracle, precision, name, ratio):
         assert np.array_equal(corr, ocorr.astype(np.int64)), (name, p)
 
 
+@pytest.mark.parametrize("precision", [64, 32])
+def test_decode_zero_priors_matches_oracle(gpu, oracle, precision):
+    """Channel probabilities of exactly 0.5 (zero prior LLRs, zero messages): the engine-3
+    negated message domain maps them to +0 (bp_reg.h w_prior); decisions must still match."""
+    from qldpc_fault_tolerance_amd.engine import DeviceBP
+
+    code = codes.get_code("hgp_34_n225")
+    H = code.hz
+    n = code.N
+    rng = np.random.default_rng(11)
+    for frac in (0.1, 1.0):
+        probs = np.full(n, 0.05)
+        probs[rng.random(n) < frac] = 0.5
+        synd = _sample_synd(H, 0.05, 200, seed=int(frac * 10) + precision)
+        synd[:5] = 0  # all-zero syndromes: messages that stay exactly zero
+        dec = DeviceBP(H, probs, max_iter=25, ms_scaling_factor=0.625, precision=precision)
+        corr, iters, conv = dec.decode_batch(synd)
+        ocorr, oiters, oconv = oracle.bp_decode_batch(H, probs, 25, "minimum_sum", 0.625, synd, precision)
+        assert np.array_equal(iters, oiters), frac
+        assert np.array_equal(conv, oconv), frac
+        assert np.array_equal(corr, ocorr.astype(np.int64)), frac
+
+
 def test_decode_adaptive_alpha_matches_oracle(gpu, oracle):
     from qldpc_fault_tolerance_amd.engine import DeviceBP
 

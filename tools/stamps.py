@@ -18,13 +18,16 @@ runpy.run_path(sys.argv[0], run_name="__main__")
 from qldpc_fault_tolerance_amd import _native  # noqa: E402
 
 lib = ctypes.CDLL(_native.LIB_PATH)
-out = (ctypes.c_ulonglong * 8)()
+out = (ctypes.c_ulonglong * 10)()
 assert lib.qldpc_debug_stamps(out) == 0
 v = list(out)
-names = ["var", "var_barrier", "check", "flag_barrier", "setup", "epilogue"]
-tot = sum(v[:6])
+names = ["var", "var_barrier", "check", "flag_barrier", "setup_sample", "epilogue", "", "", "setup_prev_bar",
+         "first_check"]
+tot = sum(v[:6]) + v[8] + v[9]
 its, shots = v[6], v[7]
 print(f"wave-iterations {its}  wave-shots {shots}  iters/shot {its / max(1, shots):.1f}")
 for k, nm in enumerate(names):
+    if not nm:
+        continue
     per = v[k] / max(1, its if k < 4 else shots)
     print(f"{nm:14s} {100 * v[k] / tot:6.2f}%  {per:9.1f} clk per {'iteration' if k < 4 else 'shot'}")
