@@ -519,13 +519,23 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
   int mism = 0;
   int q = 0;
   const uint32_t rstride = (uint32_t)NCH * 16u;
+  // Bank rotation: the 16 lanes of a ds_read_b128 lane group read rows whose 16-byte chunk c
+  // would fall on only 256 / rstride bank groups (rows of 2^k chunks: a 16 / (256 / rstride)-
+  // way conflict).  Each lane reads its row's chunks rotated by (lane / rows-per-256-B):
+  // conflict-free, and the row's min / second min / parity do not depend on the order.
+  constexpr int kRows256 = 256 / (16 * NCH) > 0 ? 256 / (16 * NCH) : 1;
+  constexpr bool kRot = NCH == 2 || NCH == 4 || NCH == 8;
+  const uint32_t rot = kRot ? ((uint32_t)(tid / kRows256) & (uint32_t)(NCH - 1)) : 0u;
+  uint32_t coff[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) coff[c] = kRot ? (((uint32_t)c + rot) & (uint32_t)(NCH - 1)) * 16u : (uint32_t)c * 16u;
   VT cur[NCH];
   uint32_t fcur = 0;
   int i = tid;
   if (i < m) {
-    const VT* row = reinterpret_cast<const VT*>(smem + Ly.v + 16 + (uint32_t)i * rstride);
+    const unsigned char* row = smem + Ly.v + 16 + (uint32_t)i * rstride;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) cur[c] = row[c];
+    for (int c = 0; c < NCH; ++c) cur[c] = *reinterpret_cast<const VT*>(row + coff[c]);
     fcur = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
   }
   for (; i < m; i += TB, ++q) {
@@ -533,9 +543,9 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
     uint32_t fnxt = 0;
     const int i2 = i + TB;
     if (i2 < m) {
-      const VT* row = reinterpret_cast<const VT*>(smem + Ly.v + 16 + (uint32_t)i2 * rstride);
+      const unsigned char* row = smem + Ly.v + 16 + (uint32_t)i2 * rstride;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) nxt[c] = row[c];
+      for (int c = 0; c < NCH; ++c) nxt[c] = *reinterpret_cast<const VT*>(row + coff[c]);
       fnxt = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i2 + 1));
     }
     uint32_t s;
