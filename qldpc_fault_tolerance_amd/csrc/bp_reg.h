@@ -440,6 +440,9 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
   constexpr U kS = FT<T>::kSign;
   int mism = 0;
   int q = 0;
+  // chunk rotation against ds_read_b128 bank conflicts (as r_check_c; power-of-two widths)
+  const int rmask = (nch & (nch - 1)) == 0 ? nch - 1 : 0;
+  const int rot = rmask ? (tid / (nch < 16 ? 16 / nch : 1)) & rmask : 0;
   for (int i = tid; i < m; i += TB, ++q) {
     const VT* row = reinterpret_cast<const VT*>(smem + Ly.v + 16 + (uint32_t)i * (uint32_t)nch * 16u);
     uint32_t& F = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
@@ -464,7 +467,7 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
       // with the masking folded into the instructions
       float f1 = FT<T>::val(m1), f2 = FT<T>::val(m2);
       for (int c = 0; c < nch; ++c) {
-        const VT v = row[c];
+        const VT v = row[(c + rot) & (rmask | (rmask ? 0 : 0x7fffffff))];
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
           const float x = V16<T>::get(v, k);
@@ -482,7 +485,7 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
       m2 = FT<T>::bits(f2);
     } else {
       for (int c = 0; c < nch; ++c) {
-        const VT v = row[c];
+        const VT v = row[(c + rot) & (rmask | (rmask ? 0 : 0x7fffffff))];
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
           const U xb = FT<T>::bits(V16<T>::get(v, k));
