@@ -57,7 +57,8 @@ constexpr bool eng_kv64(int E) { return (E / 100) % 10 != 0; }
 template <typename T, int ENG>
 constexpr int lb_waves(int LB) {
   // engine 4 fp64 images (no CS array) fit 3 workgroups per CU: <= 168 VGPRs
-  return LB <= 256 ? (sizeof(T) == 8 ? (eng_base(ENG) == 4 ? 3 : 2) : 4) : 1;
+  // (the fp64 512-thread family: 2 workgroups of 8 waves per CU, 128 VGPRs)
+  return LB <= 256 ? (sizeof(T) == 8 ? (eng_base(ENG) == 4 ? 3 : 2) : 4) : (LB <= 512 && eng_kv64(ENG)) ? 4 : 1;
 }
 __device__ inline unsigned long long qstamp() {
 #if QLDPC_STAMPS
@@ -209,7 +210,7 @@ struct RState {
   // the fp64 <= 256-thread family (256-VGPR budget) keeps the two addresses of an edge
   // unpacked and absolute (ea = CS address, ev = V slot address): no unpack / base add
   // per access, 2 VALU per edge and iteration fewer
-  static constexpr bool kSplit = eng_kv64(ENG) && sizeof(T) == 8;
+  static constexpr bool kSplit = (ENG / 100) % 10 == 1 && sizeof(T) == 8;  // engine id 103 (not 303)
   uint32_t ea[VPL][DMAX];
   uint32_t ev[kSplit ? VPL : 1][kSplit ? DMAX : 1];
   T L[VPL];

@@ -90,10 +90,17 @@ unsigned long long* debug_stamps_buffer() {
 }
 #endif
 
+// fp64 engine-3 kernels for 257-512-thread workgroups (engine id 303, VPL 3-4); opt-in QLDPC_F64X=1
+bool use_f64x(int engine, int precision, int dmax, int tb, int vpl, int ea_shift) {
+  return engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && tb > 256 && tb <= 512 && vpl >= 3 &&
+         vpl <= 4 && env_int("QLDPC_F64X", 0) != 0;
+}
+
 // Slot-family kernels of an engine (2, 3 or 4).
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
                       int nch = 0) {
   if (use_f64w(engine, precision, dmax, tb, vpl, ea_shift, nch)) return get_rvariant_f64_w(vpl, d3k, nch);
+  if (use_f64x(engine, precision, dmax, tb, vpl, ea_shift)) return get_rvariant_f64_x(vpl, d3k);
   if (use_f32w(engine, precision, dmax, tb, vpl, ea_shift, nch)) return get_rvariant_f32_w(vpl, d3k);
   if (engine == 4 && precision == 64 && tb <= 256 && vpl >= 4) return get_r4variant_f64_w(vpl);
   if (engine == 3 && ea_shift == 2)
@@ -794,7 +801,9 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
                              ? (int)(r_layout(3, vslots2, g->m, tsize).v / 4)
                              : -1;
     // fp64 engine-3 kernels are built with D3K = 0 only, except the <= 256-thread family
-    if (precision != 32 && !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch)) bp->d3k = 0;
+    if (precision != 32 && !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch) &&
+        !use_f64x(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift))
+      bp->d3k = 0;
     std::vector<int> lab;
     // fp64 (measured +3 % with the bank-aware fp64 v2c placement); fp32 gathers of the
     // structured codes are already near conflict-free (QLDPC_LABEL=1 forces it on)

@@ -771,9 +771,13 @@ class CodeFamily_SpaceTime:
     as the reference (``:1189-1216``; p_data = eval_p, q = eval_p, Pauli
     ``[eval_p/2]*3``) and runs :class:`CodeSimulator_Phenon_SpaceTime` (the
     reference names an undefined ``CodeSimulator_SpaceTime`` there, quirk Q5).
-    Returns ``(eval_wer_list, eval_p_list_per_code)``; the reference leaves the
-    second value undefined for 'phenl' and this returns the p grid per code.
-    ``'circuit'`` needs stim (absent) and raises.
+    Return shapes (``:1165-1296``): ``'data'`` — ``(eval_wer_list, eval_p_list)``, one ``np.array``
+    of WERs per code and the p list exactly as passed, as the reference.  ``'phenl'`` — the
+    reference appends one scalar per (code, p) to a flat list and then fails at its ``return`` on
+    the unbound ``eval_p_adapt_list`` (UnboundLocalError); here it returns the same values
+    nested like ``'data'`` (``eval_wer_list[c][i]`` = code c at ``eval_p_list[i]``, i.e. the
+    reference's flat list reshaped to ``[len(code_list), len(eval_p_list)]`` as its commented-out
+    ``np.reshape`` does) and one p array per code.  ``'circuit'`` needs stim (absent) and raises.
     """
 
     def __init__(self, code_list: list, decoder1_class, decoder2_class):
@@ -817,6 +821,8 @@ class CodeFamily_SpaceTime:
                     per_code.append(sim.WordErrorRate(num_cycles=num_cycles, num_samples=num_samples)[0])
             eval_wer_list.append(np.array(per_code))
             eval_p_adapt_list.append(np.array(eval_p_list))
+        if noise_model == "data":
+            return eval_wer_list, eval_p_list  # :1166 eval_p_adapt_list = eval_p_list
         return eval_wer_list, eval_p_adapt_list
 
     def EvalThreshold(self, noise_model: str, eval_logical_type: str, eval_method: str, est_threshold: float,

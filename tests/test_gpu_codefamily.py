@@ -72,7 +72,8 @@ def test_codefamily_spacetime_evalwer(gpu, oracle):
         want.append(simulators.word_error_rate_per_cycle(r["failures"], S, code.K, 7))
     assert len(wl) == 1 and wl[0].tolist() == want and pl[0].tolist() == p_list
     random.seed(10)
-    wl, _ = fam.EvalWER("data", "X", [0.05], S, if_plot=False)
+    wl, pl = fam.EvalWER("data", "X", [0.05], S, if_plot=False)
+    assert pl == [0.05]  # the p list as passed (src/Simulators_SpaceTime.py:1166)
     random.seed(10)
     seed = random.getrandbits(64)
     r = oracle.mc_run(code, 0.025, 0.025, 0.025, seed=seed, shot_begin=0, shot_count=S, logical_mode="X",
