@@ -528,7 +528,7 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
   // way conflict).  Each lane reads its row's chunks rotated by (lane / rows-per-256-B):
   // conflict-free, and the row's min / second min / parity do not depend on the order.
   constexpr int kRows256 = 256 / (16 * NCH) > 0 ? 256 / (16 * NCH) : 1;
-  constexpr bool kRot = NCH == 2 || NCH == 4 || NCH == 8;
+  constexpr bool kRot = (NCH == 4 || NCH == 8) && sizeof(T) == 8;  // fp32 2-chunk rows: 2-way only, not worth its VGPRs
   const uint32_t rot = kRot ? ((uint32_t)(tid / kRows256) & (uint32_t)(NCH - 1)) : 0u;
   uint32_t coff[NCH];
 #pragma unroll
@@ -747,10 +747,13 @@ __device__ inline void r_fill(const SSector& S, unsigned char* smem, const RLayo
   uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);
   if (tid < 10) lred[tid] = 0;  // lred[0..7], flags[0..1]
   if (eng_base(ENG) == 3 && tid == 0) {
+    // missing-edge dummy: c2v = ±0 (an opaque zero: a hoisted zero pair outlives the loops)
+    uint32_t zz = 0;
+    asm volatile("" : "+v"(zz));
     Pair<T> z;
-    z.a = 0;
-    z.b = 0;
-    lds_at<Pair<T>>(smem, 0) = z;  // missing-edge dummy: c2v = ±0
+    z.a = (typename FT<T>::U)zz;
+    z.b = (typename FT<T>::U)zz;
+    lds_at<Pair<T>>(smem, 0) = z;
   }
 }
 
@@ -1064,19 +1067,22 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rmc_kernel(SMcArgs
   uint32_t* fm1 = fm0 + ((fw + 3) & ~3);
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(fm1 + ((fw + 3) & ~3));
   if (tid < kCntHist) cnt[tid] = 0;
-  const long long nchunks = (A.shot_count + CH - 1) / CH;
+  // chunk indices are 32-bit (host-checked) and c0 a 32x32-bit product: no 64-bit copy of the
+  // chunk size stays live across the loops (it was spilled)
+  const int nchunks = (int)((A.shot_count + CH - 1) / CH);
   // chunks come from a queue (A.work): a workgroup that drew short decodes takes more
   // chunks, so the launch does not wait on the unluckiest static share
-  __shared__ long long s_next;
-  long long ch = blockIdx.x;
+  __shared__ int s_next;
+  int ch = blockIdx.x;
   if (A.work) {
-    if (tid == 0) s_next = (long long)atomicAdd(A.work, 1u);
+    if (tid == 0) s_next = (int)atomicAdd(A.work, 1u);
     __syncthreads();
     ch = s_next;
   }
   for (; ch < nchunks;) {
-    const long long c0 = ch * CH;
-    const int cn = (int)(A.shot_count - c0 < CH ? A.shot_count - c0 : CH);
+    const long long c0 = (long long)((unsigned long long)(unsigned)ch * (unsigned)CH);
+    const unsigned long long rem = (unsigned long long)(A.shot_count - c0);  // > 0
+    const int cn = (rem >> 31) ? CH : ((int)rem < CH ? (int)rem : CH);  // no 64-bit compare (VALU on gfx9)
     for (int i = tid; i < fw; i += TB) {
       fm0[i] = 0;
       fm1[i] = 0;
@@ -1099,10 +1105,10 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rmc_kernel(SMcArgs
     if (nf) atomicAdd(&cnt[kCntFail], nf);
     if (tid == 0) {
       cnt[kCntShots] += (unsigned long long)cn;
-      if (A.work) s_next = (long long)atomicAdd(A.work, 1u);
+      if (A.work) s_next = (int)atomicAdd(A.work, 1u);
     }
     __syncthreads();
-    ch = A.work ? s_next : ch + gridDim.x;
+    ch = A.work ? s_next : ch + (int)gridDim.x;
   }
   __syncthreads();
   if (tid < kCntHist && cnt[tid]) atomicAdd(&A.counters[tid], cnt[tid]);

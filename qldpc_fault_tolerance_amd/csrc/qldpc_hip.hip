@@ -1221,6 +1221,7 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     a.stamps = debug_stamps_buffer();
 #endif
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
+    if (nchunks > 0x7fffffffLL) return set_err(QLDPC_EINVAL, "too many shots for one launch (chunk count >= 2^31)");
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
     // BP+OSD: capture buffers sized for every decode of the launch
     const bool bposd = (need[0] && mc->osd[0]) || (need[1] && mc->osd[1]);
