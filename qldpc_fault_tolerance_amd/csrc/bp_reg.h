@@ -189,6 +189,18 @@ __device__ inline T w_prior(T l) {
   return FT<T>::val(b == FT<T>::kSign ? (U)0 : b);  // -(+0) = -0 -> +0
 }
 
+// XOR of a 32-bit value over the 64 lanes of a wave (all lanes active), without the LDS
+// crossbar: quad butterflies and row rotations in DPP give each lane its 16-lane row's xor,
+// then the four row values are read into SGPRs.  The result is wave-uniform.
+__device__ inline uint32_t wave_xor_u32(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 16) ^
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
 // x is +0 or -0 (v_cmp_class_*: class bits 5 = -0, 6 = +0)
 __device__ inline bool is_zero(float x) { return __builtin_amdgcn_classf(x, 0x60); }
 __device__ inline bool is_zero(double x) { return __builtin_amdgcn_class(x, 0x60); }
@@ -1014,12 +1026,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
           unsigned long long a = 0;
 #pragma unroll
           for (int k = 0; k < VPL; ++k) a ^= lm[k];
-          uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
-#pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            lo ^= (uint32_t)__shfl_xor((int)lo, o);
-            hi ^= (uint32_t)__shfl_xor((int)hi, o);
-          }
+          const uint32_t lo = wave_xor_u32((uint32_t)a), hi = wave_xor_u32((uint32_t)(a >> 32));
           if ((tid & 63) == 0) {
             if (lo) atomicXor(&lred[2 * w], lo);
             if (hi) atomicXor(&lred[2 * w + 1], hi);
