@@ -101,12 +101,13 @@ def kernel_name(dec):
     if g["engine"] == 6:  # HBM-resident messages: staged pipeline around the per-lane decode kernel
         return f"(anonymous namespace)::hdec_kernel<{t}> (engine 6, staged shot loop)"
     mc = dec.graph.info()["max_col_deg"]
-    dmax = 4 if mc <= 4 else (mc if g["engine"] == 3 and mc <= 6 and dec.precision == 32 else 8)
+    dmax = 4 if mc <= 4 else (mc if g["engine"] == 3 and (mc <= 6 if dec.precision == 32 else mc == 5) else 8)
     nch = (max(1, dec.graph.info()["max_row_deg"]) * (4 if dec.precision == 32 else 8) + 15) // 16
-    if g["engine"] == 3 and dec.precision == 64 and dmax == 4 and g["threads"] <= 256 and 4 <= g["vars_per_thread"] <= 8 \
-            and nch in (3, 4) and os.environ.get("QLDPC_F64W", "1") != "0":
+    if g["engine"] == 3 and dec.precision == 64 and (dmax == 4 or (dmax == 5 and g["vars_per_thread"] <= 5)) \
+            and g["threads"] <= 256 and 4 <= g["vars_per_thread"] <= 8 and nch in (3, 4) \
+            and os.environ.get("QLDPC_F64W", "1") != "0":
         # fp64 family for <= 256-thread workgroups (engine id 103, launch bounds 256, rows of nch chunks)
-        return f"qldpc::rmc_kernel<double, 4, {g['vars_per_thread']}, 103, {g['degree3_slots']}, 256, {nch}>"
+        return f"qldpc::rmc_kernel<double, {dmax}, {g['vars_per_thread']}, 103, {g['degree3_slots']}, 256, {nch}>"
     if g["engine"] == 3 and dec.precision == 32 and dmax == 4 and 5 <= g["vars_per_thread"] <= 8 and nch == 2 \
             and os.environ.get("QLDPC_F32W", "1") != "0":
         # fp32 family with the compile-time 2-chunk check phase

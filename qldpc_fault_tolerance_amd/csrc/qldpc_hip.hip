@@ -69,8 +69,9 @@ SVariant get_rvariant(int engine, int precision, int vpl, int d3k, int dmax) {
 // fp64 engine-3 kernels built for <= 256-thread workgroups (engine id 103:
 // 256-VGPR budget, own v2c in VGPRs, compile-time D3K); QLDPC_F64W=0 disables.
 bool use_f64w(int engine, int precision, int dmax, int tb, int vpl, int ea_shift, int nch) {
-  return engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && tb <= 256 && vpl >= 4 && vpl <= 8 &&
-         (nch == 3 || nch == 4) && env_int("QLDPC_F64W", 1) != 0;
+  // column degree 5 (kern_r_f64_d5.hip): VPL 4-5 only
+  return engine == 3 && precision == 64 && (dmax == 4 || (dmax == 5 && vpl <= 5)) && ea_shift == 0 && tb <= 256 &&
+         vpl >= 4 && vpl <= 8 && (nch == 3 || nch == 4) && env_int("QLDPC_F64W", 1) != 0;
 }
 
 // fp32 engine-3 kernels with the compile-time 2-chunk check phase (rows of <= 8 edges);
@@ -99,7 +100,8 @@ bool use_f64x(int engine, int precision, int dmax, int tb, int vpl, int ea_shift
 // Slot-family kernels of an engine (2, 3 or 4).
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
                       int nch = 0) {
-  if (use_f64w(engine, precision, dmax, tb, vpl, ea_shift, nch)) return get_rvariant_f64_w(vpl, d3k, nch);
+  if (use_f64w(engine, precision, dmax, tb, vpl, ea_shift, nch))
+    return dmax == 5 ? get_rvariant_f64_w_d5(vpl, d3k, nch) : get_rvariant_f64_w(vpl, d3k, nch);
   if (use_f64x(engine, precision, dmax, tb, vpl, ea_shift)) return get_rvariant_f64_x(vpl, d3k);
   if (use_f32w(engine, precision, dmax, tb, vpl, ea_shift, nch)) return get_rvariant_f32_w(vpl, d3k);
   if (engine == 4 && precision == 64 && tb <= 256 && vpl >= 4) return get_r4variant_f64_w(vpl);
@@ -681,6 +683,8 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
   // engine 3 also takes fp32 graphs with column degree 5-6 (lifted-product codes), exact slot count
   if (bp->engine == 3 && precision == 32 && colmax > 4 && colmax <= 6 && env_int("QLDPC_E3_D56", 1) != 0)
     bp->DMAX = colmax;
+  // fp64: column degree 5 on the <= 256-thread family (checked with the geometry below)
+  if (bp->engine == 3 && precision == 64 && colmax == 5 && env_int("QLDPC_E3_D56", 1) != 0) bp->DMAX = 5;
   bp->probs.assign(channel_probs, channel_probs + g->n);
   auto fail = [&](int code) {
     for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->rperm, &bp->work, &bp->h_rp, &bp->h_rcol,
@@ -743,7 +747,9 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       bp->ea_shift = 2;
     if (bp->engine >= 3 && ((DM != 4 && !(bp->engine == 3 && (DM == 5 || DM == 6))) ||
                             choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL, pref, vmax) ||
-                            !r_fits(bp->engine, vslots, g->m, tsize, bp->ea_shift))) {
+                            !r_fits(bp->engine, vslots, g->m, tsize, bp->ea_shift) ||
+                            (precision == 64 && DM == 5 &&
+                             !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch)))) {
       bp->ea_shift = 0;
       bp->engine = 2;  // graph outside the register engines' envelope
       bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;

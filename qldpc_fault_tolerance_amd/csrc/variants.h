@@ -45,6 +45,7 @@ SVariant get_rvariant_f64(int vpl);
 SVariant get_rvariant_f32_w(int vpl, int d3k);  // kern_r_f32_w.hip: compile-time 2-chunk rows
 SVariant get_rvariant_f64_w(int vpl, int d3k, int nch);  // kern_r_f64_w{3,4}.hip: <= 256 threads, own v2c in VGPRs, D3K
 SVariant get_rvariant_f64_w3(int vpl, int d3k);
+SVariant get_rvariant_f64_w_d5(int vpl, int d3k, int nch);  // kern_r_f64_d5.hip: column degree 5
 SVariant get_rvariant_f64_x(int vpl, int d3k);  // kern_r_f64_x.hip: 257-512 threads, 128 VGPRs (opt-in)
 SVariant get_rvariant_f64_w4(int vpl, int d3k);
 SVariant get_r4variant_f32(int vpl);
