@@ -41,6 +41,9 @@
 #ifndef QLDPC_STAMPS
 #define QLDPC_STAMPS 0
 #endif
+#ifndef QLDPC_FLIP_BRANCHFREE
+#define QLDPC_FLIP_BRANCHFREE 0
+#endif
 #include "bp_slot.h"
 
 namespace qldpc {
@@ -395,10 +398,16 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     lds_st<U, RState<T, DMAX, VPL, ENG>::kSplit>(smem, r_va(R, k, t), nv[t]);
     if (KV) R.ov[KV ? k : 0][KV ? t : 0] = nv[t];
   }
+#if QLDPC_FLIP_BRANCHFREE
+  // diagnostic variant: every edge xors (x != xprev) into its check's F word, no branch
+#pragma unroll
+  for (int t = 0; t < ND; ++t) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), (uint32_t)(x != xprev));
+#else
   if (x != xprev) {
 #pragma unroll
     for (int t = 0; t < ND; ++t) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), 1u);
   }
+#endif
   return x;
 }
 
