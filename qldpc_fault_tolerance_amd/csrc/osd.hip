@@ -341,7 +341,27 @@ int qldpc_osd_decode_batch(const qldpc_osd* osd, const uint8_t* synd, const doub
 // (weight, candidate index) = the first strictly lightest in ldpc's order.
 namespace {
 
-constexpr int kOsdThreads = 256;
+constexpr int kOsdThreads = 256;      // HBM-slice image: memory-latency bound, 3 workgroups per CU
+constexpr int kOsdThreadsLds = 1024;  // LDS-resident image: one workgroup per CU, 16 waves on its rows
+
+#ifndef QLDPC_STAMPS
+#define QLDPC_STAMPS 0
+#endif
+// diagnostic builds (QLDPC_STAMPS): per-step cycle sums of osd_gpu_kernel, wave 0 of each
+// workgroup: [0] sort, [1] H load, [2] Gauss-Jordan, [3] swaps + bit-vectors, [4] candidates,
+// [5] outputs, [6] syndromes, [7] positions visited, [8] of [2]: pivot searches + their barrier
+__device__ unsigned long long g_osd_stamps[10];
+__device__ inline unsigned long long osd_stamp() {
+#if QLDPC_STAMPS
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+#else
+  return 0;
+#endif
+}
 constexpr int kOsdMaxN = 8192;
 
 struct OsdGpuArgs {
@@ -357,9 +377,17 @@ struct OsdGpuArgs {
   int32_t* iws;            // per workgroup: pivrow [rank] | pivpos [rank] | swp [n]
   long long B;
   int m, n, W, RW, rank, method, order, NP;
-  int m_lds;  // 1: the matrix lives in LDS after the sort tables (flat addressing), else in the HBM slice
+  int m_lds;  // 1: the matrix lives in LDS, aliasing the sort tables (copied out first), else in the HBM slice
+  int bits_off;  // LDS byte offset of the used / syndrome bit-vectors
   long long ws_words, iws_ints;
 };
+
+// dst[q*m] ^= src[q*m] for q < W: no aliasing between the two rows, so the loads can run ahead
+// of the stores (in-place xors through one pointer would serialize word by word)
+__device__ inline void row_xor(u64* __restrict__ dst, const u64* __restrict__ src, int W, int m) {
+#pragma unroll 8
+  for (int q = 0; q < W; ++q) dst[(size_t)q * m] ^= src[(size_t)q * m];
+}
 
 __device__ inline u64 ord_key(double x) {
   if (x == 0.0) x = 0.0;  // -0 ties +0, as std::stable_sort's `<` has it
@@ -367,29 +395,43 @@ __device__ inline u64 ord_key(double x) {
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 
-__global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
+template <int LB>
+__global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int m = A.m, n = A.n, W = A.W, RW = A.RW, NP = A.NP, rank = A.rank;
   u64* skey = reinterpret_cast<u64*>(smem);                    // [NP]
   int32_t* sidx = reinterpret_cast<int32_t*>(skey + NP);       // [NP] -> cols (sorted position -> column)
   int32_t* pos = sidx + NP;                                    // [n]  column -> sorted position
-  uint32_t* used = reinterpret_cast<uint32_t*>(pos + n);       // [ceil(m/32)]
+  uint32_t* used = reinterpret_cast<uint32_t*>(smem + A.bits_off);  // [ceil(m/32)]
   uint32_t* sb = used + (m + 31) / 32;                         // [ceil(m/32)] syndrome, reduced
   __shared__ int s_piv[3], s_npiv;  // s_piv triple-buffered by position: reset two columns ahead
   __shared__ u64 s_best;
   u64* Mg = A.ws + (size_t)blockIdx.x * A.ws_words;
   u64* X = Mg + (size_t)W * m;  // X[0] = S0, X[1 + j] = x(h_j)
-  // matrix: LDS when it fits (after the bit-vectors), else the per-workgroup HBM slice
-  u64* M = A.m_lds ? reinterpret_cast<u64*>(smem + (((size_t)NP * 12 + (size_t)n * 4 + (size_t)((m + 31) / 32) * 8 + 15) & ~(size_t)15))
-                   : Mg;
+  // matrix: LDS when it fits (at offset 0, over the sort tables, which are copied to the
+  // workgroup's HBM ints first), else the per-workgroup HBM slice
+  // (compile-time per instantiation, so the accesses are ds_* or global_*, never flat)
+  constexpr bool kMLds = LB == kOsdThreadsLds;
+  u64* M = kMLds ? reinterpret_cast<u64*>(smem) : Mg;
   int32_t* pivrow = A.iws + (size_t)blockIdx.x * A.iws_ints;
   int32_t* pivpos = pivrow + rank;
   int32_t* swp = pivpos + rank;
+  int32_t* gsidx = swp + n;   // [n] LDS mode: sorted position -> column
+  int32_t* gpos = gsidx + n;  // [n] LDS mode: column -> sorted position
+  const int32_t* sidxr = kMLds ? gsidx : sidx;
   const int k = n - rank;
   const int w = A.order < k ? A.order : k;
   const int nh = A.method == 2 ? k : w;
 
+  unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t0 = osd_stamp(), t1;
+#define OSD_ST(k)              \
+  if (QLDPC_STAMPS) {          \
+    t1 = osd_stamp();          \
+    st[k] += t1 - t0;          \
+    t0 = t1;                   \
+  }
   for (long long b = blockIdx.x; b < A.B; b += gridDim.x) {
     uint8_t* ow = A.outw + b * (long long)n;
     uint8_t* o0 = A.out0 ? A.out0 + b * (long long)n : nullptr;
@@ -425,7 +467,16 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
         }
         __syncthreads();
       }
-    for (int q = tid; q < n; q += TB) pos[sidx[q]] = q;
+    OSD_ST(0)
+    if (kMLds) {
+      for (int q = tid; q < n; q += TB) {
+        const int c = sidx[q];
+        gsidx[q] = c;
+        gpos[c] = q;
+      }
+    } else {
+      for (int q = tid; q < n; q += TB) pos[sidx[q]] = q;
+    }
     for (int q = tid; q < (m + 31) / 32; q += TB) {
       used[q] = 0;
       uint32_t v = 0;
@@ -437,32 +488,72 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
       s_piv[0] = s_piv[1] = s_piv[2] = 0x7FFFFFFF;
     }
     __syncthreads();
-    // 2. H with permuted columns, word-major; each thread owns whole rows
+    // 2. H with permuted columns, word-major; each thread owns whole rows (LDS mode: the
+    // barrier above ended every read of the sort tables this overwrites)
+    const int32_t* posr = kMLds ? gpos : pos;
     for (int i = tid; i < m; i += TB) {
       for (int q = 0; q < W; ++q) M[(size_t)q * m + i] = 0;
       for (int e = A.rp[i]; e < A.rp[i + 1]; ++e) {
-        const int p = pos[A.ci[e]];
+        const int p = posr[A.ci[e]];
         M[(size_t)(p >> 6) * m + i] ^= 1ull << (p & 63);
       }
     }
     __syncthreads();
+    OSD_ST(1)
     // 3. Gauss-Jordan over positions in order (greedy pivots = ldpc's pivot set).
     // Barriers: one per dependent position, two per pivot.  Slot p%3 of s_piv collects
     // column p's pivot row; thread 0 re-arms slot (p+2)%3 after this column's first
     // barrier (its last reader, column p-1, is past that barrier; its next writer,
     // column p+2, is behind column p+1's barrier).  used / pivrow / s_npiv change
     // between the two barriers of a pivot column, while nobody reads them.
+    // Memory shape: M sits in an HBM (MALL/L2) slice, so every dependent round trip costs
+    // ~1 us.  The search batch-loads column p's word of all the thread's rows at once and
+    // keeps which of them have the bit (M does not change until the elimination); the
+    // elimination loads the pivot row and the target row by blocks of kBW words, all loads of
+    // a block ahead of its stores (in-place xors of one array would otherwise serialize).
+    constexpr int kRowsPT = 2048 / LB;  // rows per thread kept in a mask (m <= 2048)
+    const bool masked = m <= kRowsPT * TB;
     for (int p = 0; p < n; ++p) {
       if (s_npiv >= rank) break;
+      unsigned long long ts0 = 0;
+      if (QLDPC_STAMPS) {
+        ts0 = osd_stamp();
+        st[7] += 1;
+      }
       const u64* Mp = M + (size_t)(p >> 6) * m;
       const u64 bit = 1ull << (p & 63);
       const int slot = p % 3;
-      for (int i = tid; i < m; i += TB)
-        if (!((used[i >> 5] >> (i & 31)) & 1u) && (Mp[i] & bit)) {
-          atomicMin(&s_piv[slot], i);
-          break;
+      uint32_t hasb = 0;  // bit j: row tid + j*TB has column p set (masked mode)
+      int cand = 0x7FFFFFFF;
+      if (masked) {
+        u64 wv[kRowsPT];
+#pragma unroll
+        for (int j = 0; j < kRowsPT; ++j) {
+          const int i = tid + j * TB;
+          wv[j] = i < m ? Mp[i] : 0ull;
         }
+        // the wave's first candidate row by ballot (rows tid + j*TB are consecutive per wave for
+        // each j): one LDS atomic per wave instead of one per candidate lane
+        int wcand = 0x7FFFFFFF;
+#pragma unroll
+        for (int j = 0; j < kRowsPT; ++j) {
+          const int i = tid + j * TB;
+          const bool hb = (wv[j] & bit) != 0;
+          if (hb) hasb |= 1u << j;
+          const unsigned long long bal = __ballot(hb && !((used[i >> 5] >> (i & 31)) & 1u));
+          if (wcand == 0x7FFFFFFF && bal) wcand = (tid & ~63) + j * TB + (__ffsll((long long)bal) - 1);
+        }
+        if ((tid & 63) == 0) cand = wcand;
+      } else {
+        for (int i = tid; i < m; i += TB)
+          if (!((used[i >> 5] >> (i & 31)) & 1u) && (Mp[i] & bit)) {
+            cand = i;
+            break;
+          }
+      }
+      if (cand != 0x7FFFFFFF) atomicMin(&s_piv[slot], cand);
       __syncthreads();
+      if (QLDPC_STAMPS) st[8] += osd_stamp() - ts0;
       const int r = s_piv[slot];
       if (tid == 0) s_piv[(p + 2) % 3] = 0x7FFFFFFF;
       if (r == 0x7FFFFFFF) continue;  // dependent position (uniform)
@@ -473,14 +564,34 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
         pivpos[s_npiv] = p;
         s_npiv = s_npiv + 1;
       }
-      for (int i = tid; i < m; i += TB)
-        if (i != r && (Mp[i] & bit)) {
-          for (int q = 0; q < W; ++q) M[(size_t)q * m + i] ^= M[(size_t)q * m + r];
+      const u64* Mr = M + r;
+      if (masked) {
+        // syndrome bits of the updated rows: one ballot per row slot, two LDS xors per wave
+#pragma unroll 1
+        for (int j = 0; j < kRowsPT; ++j) {
+          const int i = tid + j * TB;
+          const bool upd = ((hasb >> j) & 1u) != 0 && i != r;
+          if (upd) row_xor(M + i, Mr, W, m);
+          if (sr) {
+            const unsigned long long bal = __ballot(upd);
+            const int i0 = (tid & ~63) + j * TB;  // 32-aligned: TB and the wave base are multiples of 64
+            if ((tid & 63) == 0 && bal) {
+              if ((uint32_t)bal) atomicXor(&sb[i0 >> 5], (uint32_t)bal);
+              if ((uint32_t)(bal >> 32)) atomicXor(&sb[(i0 >> 5) + 1], (uint32_t)(bal >> 32));
+            }
+          }
+        }
+      } else {
+        for (int i = tid; i < m; i += TB) {
+          if (i == r || !(Mp[i] & bit)) continue;
+          row_xor(M + i, Mr, W, m);
           if (sr) atomicXor(&sb[i >> 5], 1u << (i & 31));
         }
+      }
       __syncthreads();
     }
     const int r = s_npiv;
+    OSD_ST(2)
     // 4. Neal's column swaps -> non-pivot order Ht (positions swp[r + j])
     for (int q = tid; q < n; q += TB) swp[q] = q;
     __syncthreads();
@@ -511,6 +622,7 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
     }
     if (tid == 0) s_best = ~0ull;
     __syncthreads();
+    OSD_ST(3)
     // 6. candidates: lexicographic min of (weight, index)
     long long L = 1;
     if (A.method == 1 && w > 0) L = 1ll << w;
@@ -553,6 +665,7 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
     }
     if (best != ~0ull) atomicMin(&s_best, best);
     __syncthreads();
+    OSD_ST(4)
     // 7. outputs
     const long long cw = (long long)(s_best & ((1ull << 40) - 1));
     int tw[2];
@@ -588,26 +701,31 @@ __global__ void __launch_bounds__(kOsdThreads) osd_gpu_kernel(OsdGpuArgs A) {
       } else {
         for (int a = 0; a < ntw; ++a) v ^= X[(size_t)(1 + tw[a]) * RW + q];
       }
-      const int col = sidx[pivpos[i]];
+      const int col = sidxr[pivpos[i]];
       ow[col] = (uint8_t)((v >> c) & 1ull);
       if (o0) o0[col] = (uint8_t)s0;
     }
     if (tid == 0) {
       if (A.method == 1) {
-        for (unsigned long long e = ewb; e; e &= e - 1) ow[sidx[swp[r + __ffsll((long long)e) - 1]]] = 1;
+        for (unsigned long long e = ewb; e; e &= e - 1) ow[sidxr[swp[r + __ffsll((long long)e) - 1]]] = 1;
       } else {
-        for (int a = 0; a < ntw; ++a) ow[sidx[swp[r + tw[a]]]] = 1;
+        for (int a = 0; a < ntw; ++a) ow[sidxr[swp[r + tw[a]]]] = 1;
       }
     }
     __syncthreads();
+    OSD_ST(5)
+    if (QLDPC_STAMPS) st[6] += 1;
   }
+#undef OSD_ST
+  if (QLDPC_STAMPS && tid == 0)
+    for (int k2 = 0; k2 < 10; ++k2) atomicAdd(&g_osd_stamps[k2], st[k2]);
 }
 
 }  // namespace
 
 struct qldpc_osd_gpu {
   qldpc_osd host;  // shape, method, order, rank
-  int device = 0, grid = 0, W = 0, RW = 0, NP = 0, nh = 0, m_lds = 0;
+  int device = 0, grid = 0, W = 0, RW = 0, NP = 0, nh = 0, m_lds = 0, bits_off = 0;
   size_t lds = 0;
   long long ws_words = 0, iws_ints = 0;
   qldpc_rt::DevBuf rp, ci, ws, iws;
@@ -717,16 +835,20 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   G->NP = 1;
   while (G->NP < n) G->NP <<= 1;
   G->nh = G->host.method == 2 ? k : w;
-  G->lds = (size_t)G->NP * 12 + (size_t)n * 4 + (size_t)((m + 31) / 32) * 8 + 64;
-  // QLDPC_OSD_LDS=1: the Gauss-Jordan image in LDS too when it fits (<= 144 KiB in all).  Off by
-  // default: measured slower (config-5 final round 244 vs 158 ms) — the image costs residency
-  // (1 workgroup per CU instead of ~6), and the HBM slice stays L2-resident anyway.
-  const size_t mbytes = (size_t)G->W * m * 8;
+  // LDS: sort tables (skey, sidx, pos), then the used / syndrome bit-vectors.  The Gauss-Jordan
+  // image goes to LDS too when it fits over the sort tables (those are copied to HBM ints before
+  // the image is built): every pivot search / row update is then an LDS access instead of a
+  // ~1 us HBM round trip.  QLDPC_OSD_LDS=0 keeps the image in the HBM slice.
+  const size_t lsort = ((size_t)G->NP * 12 + (size_t)n * 4 + 15) & ~(size_t)15;
+  const size_t mbytes = ((size_t)G->W * m * 8 + 15) & ~(size_t)15;
+  const size_t lbits = (size_t)((m + 31) / 32) * 8 + 64;
   const char* lds_env = std::getenv("QLDPC_OSD_LDS");
-  G->m_lds = (lds_env && std::atoi(lds_env) == 1 && ((G->lds + 15) & ~(size_t)15) + mbytes <= 144 * 1024) ? 1 : 0;
-  if (G->m_lds) G->lds = ((G->lds + 15) & ~(size_t)15) + mbytes;
+  const bool want_lds = !lds_env || std::atoi(lds_env) != 0;
+  G->m_lds = (want_lds && std::max(lsort, mbytes) + lbits <= (size_t)160 * 1024 - 256) ? 1 : 0;  // 256: static LDS
+  G->bits_off = (int)(G->m_lds ? std::max(lsort, mbytes) : lsort);
+  G->lds = (size_t)G->bits_off + lbits;
   G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW;
-  G->iws_ints = 2ll * rank + n;
+  G->iws_ints = 2ll * rank + 3ll * n;
   auto fail = [&](int code) {
     G->rp.release(); G->ci.release(); G->ws.release(); G->iws.release();
     delete G;
@@ -737,7 +859,9 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)
     return fail(set_err(QLDPC_EHIP, "device CU count"));
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&osd_gpu_kernel), kOsdThreads,
+  const void* kf = G->m_lds ? reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreadsLds>)
+                            : reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreads>);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf, G->m_lds ? kOsdThreadsLds : kOsdThreads,
                                                    G->lds) != hipSuccess || nb <= 0)
     nb = 1;
   G->grid = cus * nb;
@@ -759,6 +883,16 @@ int qldpc_osd_gpu_destroy(qldpc_osd_gpu* osd) {
   return 0;
 }
 
+#if QLDPC_STAMPS
+// diagnostic builds only: read and clear osd_gpu_kernel's step-cycle sums
+int qldpc_debug_osd_stamps(unsigned long long* out) {
+  unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(out, HIP_SYMBOL(g_osd_stamps), 80) != hipSuccess)
+    return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_osd_stamps), z, 80) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int qldpc_osd_gpu_decode(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double* d_post, const uint8_t* d_conv,
                          const uint8_t* d_bp_corr, uint8_t* d_out0, uint8_t* d_outw, int64_t B, void* stream) {
   if (!osd || (B > 0 && (!d_synd || !d_post || !d_outw))) return set_err(QLDPC_EINVAL, "NULL argument");
@@ -773,10 +907,13 @@ int qldpc_osd_gpu_decode(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double
   a.iws = static_cast<int32_t*>(osd->iws.p);
   a.B = B;
   a.m = osd->host.m; a.n = osd->host.n; a.W = osd->W; a.RW = osd->RW; a.rank = osd->host.rank;
-  a.method = osd->host.method; a.order = osd->host.order; a.NP = osd->NP; a.m_lds = osd->m_lds;
+  a.method = osd->host.method; a.order = osd->host.order; a.NP = osd->NP; a.m_lds = osd->m_lds; a.bits_off = osd->bits_off;
   a.ws_words = osd->ws_words; a.iws_ints = osd->iws_ints;
   const int grid = (int)std::min<long long>(B, osd->grid);
-  hipLaunchKernelGGL(osd_gpu_kernel, dim3(grid), dim3(kOsdThreads), osd->lds, (hipStream_t)stream, a);
+  if (osd->m_lds)
+    hipLaunchKernelGGL(osd_gpu_kernel<kOsdThreadsLds>, dim3(grid), dim3(kOsdThreadsLds), osd->lds, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(osd_gpu_kernel<kOsdThreads>, dim3(grid), dim3(kOsdThreads), osd->lds, (hipStream_t)stream, a);
   QLDPC_HIP(hipGetLastError());
   return 0;
 }
