@@ -55,6 +55,9 @@ namespace qldpc {
 constexpr int eng_base(int E) { return E % 10; }
 constexpr int eng_sh(int E) { return (E / 10) % 10 ? 2 : 0; }
 constexpr bool eng_kv64(int E) { return (E / 100) % 10 != 0; }
+// + 1000 = rows of NCH chunks plus one "tail" slot per row in a separate array (rows one
+// message wider than the chunks: the fp64 space-time graphs, 8 + 1 slots), engine 3 only
+constexpr int eng_tail(int E) { return (E / 1000) % 10; }
 // launch bounds: LB threads per workgroup at most; 256-thread fp64 kernels are
 // built for 2 workgroups per CU (2 waves per SIMD: up to 256 VGPRs, no spills)
 template <typename T, int ENG>
@@ -80,13 +83,15 @@ template <int ENG>
 __device__ inline uint32_t ea_v(uint32_t ea) { return (ea >> 16) << eng_sh(ENG); }
 
 struct RLayout {
-  uint32_t v, f, sink, lred, total;  // byte offsets (engine 3: CS at 0; engine 4: V at 0)
+  uint32_t v, t, f, sink, lred, total;  // byte offsets (engine 3: CS at 0; engine 4: V at 0)
 };
 
-__host__ __device__ inline RLayout r_layout(int eng, int vslots, int mmax, int tsize) {
+// [CS][V][tail: one slot per row label (tail layouts only)][F][sink][lred]
+__host__ __device__ inline RLayout r_layout(int eng, int vslots, int mmax, int tsize, int tail = 0) {
   RLayout L;
   L.v = eng == 4 ? 0u : (uint32_t)a16((size_t)(mmax + 1) * 2 * tsize);
-  L.f = L.v + (uint32_t)a16((size_t)vslots * tsize);
+  L.t = L.v + (uint32_t)a16((size_t)vslots * tsize);
+  L.f = L.t + (tail ? (uint32_t)a16((size_t)mmax * tsize) : 0u);
   L.sink = L.f + (uint32_t)a16((size_t)(mmax + 1) * 4);
   L.lred = L.sink + (eng == 4 ? 16u : 0u);
   L.total = L.lred + 48;
@@ -535,7 +540,7 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
 // non-negative, non-NaN doubles the float order is the bit order and the
 // results are inputs unchanged, i.e. the integer min / second min of |v2c| bits
 // (three instructions per edge instead of three 64-bit compares + six selects).
-template <typename T, bool FIRST, int NCH>
+template <typename T, bool FIRST, int NCH, int TAIL = 0>
 __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, int tid, int TB, uint32_t& sbits) {
   using U = typename FT<T>::U;
   using VT = typename V16<T>::type;
@@ -555,22 +560,26 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
 #pragma unroll
   for (int c = 0; c < NCH; ++c) coff[c] = kRot ? (((uint32_t)c + rot) & (uint32_t)(NCH - 1)) * 16u : (uint32_t)c * 16u;
   VT cur[NCH];
+  T tcur = (T)0;  // TAIL: the row's slot in the tail array (sentinel when the row has no 9th edge)
   uint32_t fcur = 0;
   int i = tid;
   if (i < m) {
     const unsigned char* row = smem + Ly.v + 16 + (uint32_t)i * rstride;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) cur[c] = *reinterpret_cast<const VT*>(row + coff[c]);
+    if (TAIL) tcur = lds_at<T>(smem, Ly.t + (uint32_t)i * (uint32_t)sizeof(T));
     fcur = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
   }
   for (; i < m; i += TB, ++q) {
     VT nxt[NCH];
+    T tnxt = (T)0;
     uint32_t fnxt = 0;
     const int i2 = i + TB;
     if (i2 < m) {
       const unsigned char* row = smem + Ly.v + 16 + (uint32_t)i2 * rstride;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) nxt[c] = *reinterpret_cast<const VT*>(row + coff[c]);
+      if (TAIL) tnxt = lds_at<T>(smem, Ly.t + (uint32_t)i2 * (uint32_t)sizeof(T));
       fnxt = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i2 + 1));
     }
     uint32_t s;
@@ -602,6 +611,14 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
             : "v"(px), "v"((uint32_t)(FT<T>::bits(cur[c].x) >> 32)), "v"((uint32_t)(FT<T>::bits(cur[c].y) >> 32)));
         px = p;
       }
+      if (TAIL) {
+        const double x = (double)tcur;
+        double t;
+        asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x));
+        asm("v_min_f64 %0, %1, %2" : "=v"(f2) : "v"(f2), "v"(t));
+        asm("v_min_f64 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
+        px ^= (uint32_t)(FT<T>::bits(tcur) >> 32);
+      }
       st.a = FT<T>::bits(f1) | ((U)(px & 0x80000000u) << 32);
       st.b = FT<T>::bits(f2);
     } else {
@@ -620,12 +637,19 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
         asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(p23) : "v"(p01), "v"(FT<T>::bits(cur[c].z)), "v"(FT<T>::bits(cur[c].w)));
         px = p23;
       }
+      if (TAIL) {
+        const float x = (float)tcur;
+        f2 = __builtin_amdgcn_fmed3f(f1, f2, __builtin_fabsf(x));
+        asm("v_min_f32 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
+        px ^= (uint32_t)FT<T>::bits(tcur);
+      }
       st.a = FT<T>::bits(f1) | (px & kS);
       st.b = FT<T>::bits(f2);
     }
     lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) cur[c] = nxt[c];
+    tcur = tnxt;
     fcur = fnxt;
   }
   return mism;
@@ -759,7 +783,9 @@ __device__ inline void r_fill(const SSector& S, unsigned char* smem, const RLayo
   VT* V4 = reinterpret_cast<VT*>(smem + Ly.v);
   const VT s = V16<T>::splat(FT<T>::val(FT<T>::kSent));
   // engine 4: the first chunk is the zero chunk missing edges read
-  for (int i = tid; i < vslots / V16<T>::N; i += TB) V4[i] = (eng_base(ENG) == 4 && i == 0) ? V16<T>::splat((T)0) : s;
+  (void)vslots;
+  const int nchunks = (int)((Ly.f - Ly.v) / 16u);  // V rows and (tail layouts) the tail slots
+  for (int i = tid; i < nchunks; i += TB) V4[i] = (eng_base(ENG) == 4 && i == 0) ? V16<T>::splat((T)0) : s;
   uint32_t* F = reinterpret_cast<uint32_t*>(smem + Ly.f);
   // engine 4: row degree in the high half; engine 3: row-degree parity in bit 2 (w domain)
   for (int i = tid; i <= mmax; i += TB)
@@ -925,7 +951,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     if constexpr (eng_base(ENG) == 4)
       c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     else if constexpr (NCH > 0)
-      r_check_c<T, true, NCH>(smem, Ly, m, tid, TB, sb);
+      r_check_c<T, true, NCH, eng_tail(ENG)>(smem, Ly, m, tid, TB, sb);
     else
       r_check<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     __syncthreads();
@@ -975,7 +1001,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         // check state for iteration it + 1 (float: pre-scaled by its alpha)
         const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
         if constexpr (NCH > 0)
-          mism = r_check_c<T, false, NCH>(smem, Ly, m, tid, TB, sb);
+          mism = r_check_c<T, false, NCH, eng_tail(ENG)>(smem, Ly, m, tid, TB, sb);
         else
           mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha_next);
         if (QLDPC_STAMPS) {
@@ -1078,7 +1104,7 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rmc_kernel(SMcArgs
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = A.chunk;
   const int fw = (CH + 31) / 32;
-  const RLayout Ly = r_layout(eng_base(ENG), A.vslots, A.mmax, (int)sizeof(T));
+  const RLayout Ly = r_layout(eng_base(ENG), A.vslots, A.mmax, (int)sizeof(T), eng_tail(ENG));
   uint32_t* fm0 = reinterpret_cast<uint32_t*>(smem + Ly.total);
   uint32_t* fm1 = fm0 + ((fw + 3) & ~3);
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(fm1 + ((fw + 3) & ~3));
@@ -1135,7 +1161,7 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rdec_kernel(SDecAr
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = D.chunk;
-  const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T));
+  const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T), eng_tail(ENG));
   const long long nchunks = (D.B + CH - 1) / CH;
   __shared__ long long s_next;
   long long ch = blockIdx.x;

@@ -99,7 +99,12 @@ bool use_f64x(int engine, int precision, int dmax, int tb, int vpl, int ea_shift
 
 // Slot-family kernels of an engine (2, 3 or 4).
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
-                      int nch = 0) {
+                      int nch = 0, int tail = 0) {
+  // fp64 tail layout (rows of 4 chunks + a tail slot, dword-scaled addresses, 1024 threads)
+  if (tail) {
+    const bool ok = engine == 3 && precision == 64 && dmax == 4 && ea_shift == 2 && nch == 4 && tb > 512;
+    return ok ? get_rvariant_f64_st(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
+  }
   if (use_f64w(engine, precision, dmax, tb, vpl, ea_shift, nch))
     return dmax == 5 ? get_rvariant_f64_w_d5(vpl, d3k, nch) : get_rvariant_f64_w(vpl, d3k, nch);
   if (use_f64x(engine, precision, dmax, tb, vpl, ea_shift)) return get_rvariant_f64_x(vpl, d3k);
@@ -208,8 +213,8 @@ int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL, int pre
 // Engines 3 and 4 address their image with 16-bit byte offsets.
 // Engines 3 and 4 address their image with 16-bit byte offsets; engine 3 with
 // dword-scaled offsets (kernel id 13, ea_shift 2) reaches 256 KiB.
-bool r_fits(int eng, int vslots, int mmax, int tsize, int ea_shift = 0) {
-  const RLayout L = r_layout(eng, vslots, mmax, tsize);
+bool r_fits(int eng, int vslots, int mmax, int tsize, int ea_shift = 0, int tail = 0) {
+  const RLayout L = r_layout(eng, vslots, mmax, tsize, tail);
   return L.lred <= (65536u << ea_shift) && r_lds_bytes((int)L.total, kChunkMax) <= (size_t)kLdsMax;
 }
 
@@ -370,14 +375,17 @@ static int upload_llr(qldpc_bp* bp) {
 // decode path maps syndromes through the inverse permutation (bp->rperm).
 static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
                              const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1,
-                             const std::vector<int>& lab = {}) {
+                             const std::vector<int>& lab = {}, int tail = 0) {
   const int nv = 16 / tsize;  // messages per 16-byte chunk
   const int rw = nch * nv;
+  const int rwt = rw + (tail ? 1 : 0);  // tail layouts: logical slot rw = the row's tail slot
+  const int tail0 = (1 + g->m * nch) * nv;  // first tail slot (right after V, bp_reg.h r_layout)
   const int swz_mask = (nch == 2) ? 1 : (nch == 4) ? 3 : 0;
   const int swz_shift = (nch == 2) ? 3 : 2;
   auto L = [&](int i) { return lab.empty() ? i : lab[i]; };
   auto phys = [&](int i, int ls) {
     const int r = L(i);
+    if (ls == rw) return tail0 + r;
     return nv + r * rw + ((ls / nv) ^ ((r >> swz_shift) & swz_mask)) * nv + ls % nv;
   };
   // logical slot of every edge (CSR order); default = ascending column position
@@ -394,7 +402,7 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
   // slot s on bank pair s mod 16 (MI355X_MICROARCH.md §LDS)
   const int sg = tsize == 4 ? 32 : 16, nb = tsize == 4 ? 32 : 16;
   const int vbase_u = vbase_dw < 0 ? 0 : (tsize == 4 ? vbase_dw : vbase_dw / 2);
-  if (vbase_dw >= 0 && rw <= 32) {
+  if (vbase_dw >= 0 && rwt <= 32) {
     std::vector<uint32_t> used(g->m, 0u);
     for (int k = 0; k < VPL; ++k)
       for (int d = 0; d < DM; ++d)
@@ -405,7 +413,7 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
             if (j < 0 || d >= (int)g->col_rows[j].size()) continue;
             const int i = g->col_rows[j][d];
             int best = -1, bc = 1 << 30;
-            for (int ls = 0; ls < rw; ++ls) {
+            for (int ls = 0; ls < rwt; ++ls) {
               if ((used[i] >> ls) & 1u) continue;
               const int c = cnt[(vbase_u + phys(i, ls)) % nb];
               if (c < bc) {
@@ -745,12 +753,27 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     if (bp->engine == 3 && precision == 32 && DM == 4 && !r_fits(3, vslots, g->m, tsize) &&
         r_fits(3, vslots, g->m, tsize, 2) && env_int("QLDPC_E3_BIG", 1) != 0)
       bp->ea_shift = 2;
+    // fp64 images over 160 KiB whose rows are one message wider than 4 chunks (space-time
+    // graphs: rows of 9): 4-chunk rows + a tail slot per row, dword-scaled addresses
+    if (bp->engine == 3 && precision == 64 && DM == 4 && bp->nch == 5 && g->max_row == 9 &&
+        !r_fits(3, vslots, g->m, tsize, 2) && env_int("QLDPC_E3_TAIL", 1) != 0) {
+      const int vs4 = (1 + g->m * 4) * 2;
+      int tb = 0, vpl = 0;
+      if (r_fits(3, vs4, g->m, tsize, 2, 1) && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb > 512 &&
+          vpl >= 4 && vpl <= 8) {
+        bp->tail = 1;
+        bp->nch = 4;
+        bp->ea_shift = 2;
+      }
+    }
+    const int vslots_e3 = (1 + g->m * bp->nch) * (16 / tsize);
     if (bp->engine >= 3 && ((DM != 4 && !(bp->engine == 3 && (DM == 5 || DM == 6))) ||
                             choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL, pref, vmax) ||
-                            !r_fits(bp->engine, vslots, g->m, tsize, bp->ea_shift) ||
+                            !r_fits(bp->engine, vslots_e3, g->m, tsize, bp->ea_shift, bp->tail) ||
                             (precision == 64 && DM == 5 &&
                              !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch)))) {
       bp->ea_shift = 0;
+      bp->tail = 0;
       bp->engine = 2;  // graph outside the register engines' envelope
       bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
       if (DM == 5 || DM == 6) bp->DMAX = DM = 8;  // engine 2 kernels come in 4 and 8 slots
@@ -758,7 +781,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     const int vslots2 = (1 + g->m * bp->nch) * (16 / tsize);
     if (bp->engine >= 3) {
       bp->NS = 1;
-      bp->lds_bytes = (int)r_lds_bytes((int)r_layout(bp->engine, vslots2, g->m, tsize).total, kChunkMax);
+      bp->lds_bytes = (int)r_lds_bytes((int)r_layout(bp->engine, vslots2, g->m, tsize, bp->tail).total, kChunkMax);
     } else {
       rc = choose_sgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL);
       if (rc) return fail(rc);
@@ -808,7 +831,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
                              : -1;
     // fp64 engine-3 kernels are built with D3K = 0 only, except the <= 256-thread family
     if (precision != 32 && !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch) &&
-        !use_f64x(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift))
+        !use_f64x(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift) && !bp->tail)
       bp->d3k = 0;
     std::vector<int> lab;
     // fp64 (measured +3 % with the bank-aware fp64 v2c placement); fp32 gathers of the
@@ -821,8 +844,8 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       if (g->m && hipMemcpy(bp->rperm.p, inv.data(), (size_t)g->m * 4, hipMemcpyHostToDevice) != hipSuccess)
         return fail(set_err(QLDPC_EHIP, "upload check labels"));
     }
-    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab);
-    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch).dec_k;
+    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab, bp->tail);
+    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch, bp->tail).dec_k;
     if (bp->engine >= 3) {
       // row degrees by check label: engine 4 keeps them in F, engine 3 their parity (bp_reg.h, w domain)
       std::vector<uint8_t> deg(std::max(1, g->m));
@@ -992,7 +1015,8 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     }
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
-    SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch);
+    SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch,
+                              bp->tail);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;
@@ -1021,7 +1045,8 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
                     qldpc_mc** out) {
   if (!out || (!dec_x && !dec_z)) return set_err(QLDPC_EINVAL, "need at least one sector decoder");
   qldpc_bp* d0 = dec_x ? dec_x : dec_z;
-  const bool staged = (dec_x && dec_x->engine >= 5) || (dec_z && dec_z->engine >= 5) ||
+  const bool staged = (dec_x && dec_x->engine >= 5) || (dec_z && dec_z->engine >= 5) || (dec_x && dec_x->tail) ||
+                      (dec_z && dec_z->tail) ||
                       env_int("QLDPC_MC_STAGED", 0) == 1;
   if (staged) {  // staged pipeline around decode_batch (staged.hip): any decoder pair
     if (dec_x && dec_z && (dec_x->g->n != dec_z->g->n || dec_x->g->device != dec_z->g->device))

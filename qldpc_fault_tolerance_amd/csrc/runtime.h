@@ -72,6 +72,7 @@ struct qldpc_bp {
   int gather_conf[2] = {0, 0};  // engine 3: extra gather cycles per pass before / after labelling
   int d3k = 0;
   int ea_shift = 0;  // engine 3: 2 = dword-scaled LDS addresses in the edge words (images > 64 KiB)
+  int tail = 0;      // engine 3: 1 = rows of nch chunks + one tail slot per row (bp_reg.h eng_tail)
   // engine 5 (product-sum, bp_ps.hip): CSR / CSC on the device, optional HBM message workspace
   qldpc_rt::DevBuf ps_rp, ps_ci, ps_cp, ps_ce, ps_ws;
   long long ps_grid = 0;

@@ -48,6 +48,8 @@ SVariant get_rvariant_f64_w3(int vpl, int d3k);
 SVariant get_rvariant_f64_w_d5(int vpl, int d3k, int nch);  // kern_r_f64_d5.hip: column degree 5
 SVariant get_rvariant_f64_x(int vpl, int d3k);  // kern_r_f64_x.hip: 257-512 threads, 128 VGPRs (opt-in)
 SVariant get_rvariant_f64_w4(int vpl, int d3k);
+SVariant get_rvariant_f64_st(int vpl, int d3k);  // kern_r_f64_st*.hip: tail layout, 1024 threads (engine id 1013)
+SVariant get_rvariant_f64_st_hi(int vpl, int d3k);
 SVariant get_r4variant_f32(int vpl);
 SVariant get_r4variant_f64(int vpl);
 SVariant get_r4variant_f64_w(int vpl);  // <= 256 threads
