@@ -416,6 +416,28 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   return x;
 }
 
+// Rows loaded ahead of the reduced one in the compile-time-width check phase (A/B builds:
+// QLDPC_PFC=0/1/2).  n1600: 0 (each row loaded where it is reduced) is 4 % faster than 1 in
+// fp64 (928k -> 968k shots/s) and fp32 (1.79M -> 1.86M); 2 is 5 % / 10 % slower than 1.
+#ifndef QLDPC_PFC
+#define QLDPC_PFC 0
+#endif
+// How many variables ahead the CS gathers are issued: 2 in the fp64 <= 256-thread family
+// (engine id 103, 256-VGPR budget: +4 VGPRs, n1600 fp64 909k -> 927k shots/s), 1 elsewhere
+// (fp32 measured unchanged).  QLDPC_PF=1 / 2 overrides it in an A/B build.
+#ifndef QLDPC_PF
+#define QLDPC_PF 0
+#endif
+template <typename T, int DMAX, int VPL, int D3K, int ENG>
+__device__ inline void r_gather_k(unsigned char* smem, const RState<T, DMAX, VPL, ENG>& R, int k,
+                                  typename CSEntry<T>::type (&pn)[DMAX], typename FT<T>::U (&on)[DMAX]) {
+  constexpr int N3 = DMAX > 3 ? 3 : DMAX;
+  if (k < D3K)
+    r_gather<T, DMAX, VPL, N3, ENG>(smem, R, k, pn, on);
+  else
+    r_gather<T, DMAX, VPL, DMAX, ENG>(smem, R, k, pn, on);
+}
+
 template <typename T, int DMAX, int VPL, int D3K, int ENG>
 __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, uint32_t fdelta, T alpha,
                                  uint32_t xprev, bool last_live, double* post = nullptr, const int32_t* perm = nullptr,
@@ -423,29 +445,26 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   using U = typename FT<T>::U;
   constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
   constexpr int N3 = DMAX > 3 ? 3 : DMAX;  // low-degree slots use 3 edge slots
+  constexpr int PF0 = QLDPC_PF >= 1 ? QLDPC_PF : (RState<T, DMAX, VPL, ENG>::kSplit ? 2 : 1);
+  constexpr int PF = PF0 < VPL ? PF0 : VPL;
   r_launder(R);
   uint32_t xbits = 0;
-  typename CSEntry<T>::type pn[DMAX];
-  U on[DMAX];
-  if (0 < D3K)
-    r_gather<T, DMAX, VPL, N3, ENG>(smem, R, 0, pn, on);
-  else
-    r_gather<T, DMAX, VPL, DMAX, ENG>(smem, R, 0, pn, on);
+  // gather ring: variable k's CS entries (and, without kKeepV, own v2c) live in slot k % PF
+  typename CSEntry<T>::type pb[PF][DMAX];
+  U ob[PF][DMAX];
+#pragma unroll
+  for (int k = 0; k < PF; ++k) r_gather_k<T, DMAX, VPL, D3K, ENG>(smem, R, k, pb[k], ob[k]);
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     typename CSEntry<T>::type pr[DMAX];
     U o[DMAX];
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
-      pr[t] = pn[t];
-      o[t] = KV ? R.ov[KV ? k : 0][KV ? t : 0] : on[t];
+      pr[t] = pb[k % PF][t];
+      o[t] = KV ? R.ov[KV ? k : 0][KV ? t : 0] : ob[k % PF][t];
     }
-    if (k + 1 < VPL) {  // next variable's gathers go out before this one's arithmetic
-      if (k + 1 < D3K)
-        r_gather<T, DMAX, VPL, N3, ENG>(smem, R, k + 1, pn, on);
-      else
-        r_gather<T, DMAX, VPL, DMAX, ENG>(smem, R, k + 1, pn, on);
-    }
+    // variable k + PF's gathers go out before this one's arithmetic
+    if (k + PF < VPL) r_gather_k<T, DMAX, VPL, D3K, ENG>(smem, R, k + PF, pb[k % PF], ob[k % PF]);
     if (k == VPL - 1 && !last_live) break;  // every lane of this wave holds padding
     const bool xp = ((xprev >> k) & 1u) != 0;
     const int32_t* pk = perm ? perm + k * TB : nullptr;
@@ -540,7 +559,7 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
 // non-negative, non-NaN doubles the float order is the bit order and the
 // results are inputs unchanged, i.e. the integer min / second min of |v2c| bits
 // (three instructions per edge instead of three 64-bit compares + six selects).
-template <typename T, bool FIRST, int NCH, int TAIL = 0>
+template <typename T, bool FIRST, int NCH, int TAIL = 0, int PFC = 1>
 __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, int tid, int TB, uint32_t& sbits) {
   using U = typename FT<T>::U;
   using VT = typename V16<T>::type;
@@ -559,29 +578,30 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
   uint32_t coff[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) coff[c] = kRot ? (((uint32_t)c + rot) & (uint32_t)(NCH - 1)) * 16u : (uint32_t)c * 16u;
-  VT cur[NCH];
-  T tcur = (T)0;  // TAIL: the row's slot in the tail array (sentinel when the row has no 9th edge)
-  uint32_t fcur = 0;
-  int i = tid;
-  if (i < m) {
-    const unsigned char* row = smem + Ly.v + 16 + (uint32_t)i * rstride;
+  // rows are loaded PFC (1 or 2) rows ahead of the one being reduced
+  auto load = [&](int r, VT (&v)[NCH], T& tv, uint32_t& fv) {
+    if (r < m) {
+      const unsigned char* row = smem + Ly.v + 16 + (uint32_t)r * rstride;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) cur[c] = *reinterpret_cast<const VT*>(row + coff[c]);
-    if (TAIL) tcur = lds_at<T>(smem, Ly.t + (uint32_t)i * (uint32_t)sizeof(T));
-    fcur = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
-  }
+      for (int c = 0; c < NCH; ++c) v[c] = *reinterpret_cast<const VT*>(row + coff[c]);
+      if (TAIL) tv = lds_at<T>(smem, Ly.t + (uint32_t)r * (uint32_t)sizeof(T));
+      fv = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(r + 1));
+    }
+  };
+  VT cur[NCH], mid[NCH];
+  T tcur = (T)0, tmid = (T)0;  // TAIL: the row's slot in the tail array (sentinel when the row has no 9th edge)
+  uint32_t fcur = 0, fmid = 0;
+  int i = tid;
+  if (PFC >= 1) load(i, cur, tcur, fcur);
+  if (PFC == 2) load(i + TB, mid, tmid, fmid);
   for (; i < m; i += TB, ++q) {
     VT nxt[NCH];
     T tnxt = (T)0;
     uint32_t fnxt = 0;
-    const int i2 = i + TB;
-    if (i2 < m) {
-      const unsigned char* row = smem + Ly.v + 16 + (uint32_t)i2 * rstride;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) nxt[c] = *reinterpret_cast<const VT*>(row + coff[c]);
-      if (TAIL) tnxt = lds_at<T>(smem, Ly.t + (uint32_t)i2 * (uint32_t)sizeof(T));
-      fnxt = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i2 + 1));
-    }
+    if (PFC == 0)
+      load(i, cur, tcur, fcur);
+    else
+      load(i + PFC * TB, nxt, tnxt, fnxt);
     uint32_t s;
     if (FIRST) {
       s = ((fcur >> 1) ^ (fcur >> 2)) & 1u;  // as r_check: syndrome ^ row-degree parity
@@ -647,10 +667,22 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
       st.b = FT<T>::bits(f2);
     }
     lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
+    if (PFC == 2) {
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) cur[c] = nxt[c];
-    tcur = tnxt;
-    fcur = fnxt;
+      for (int c = 0; c < NCH; ++c) {
+        cur[c] = mid[c];
+        mid[c] = nxt[c];
+      }
+      tcur = tmid;
+      tmid = tnxt;
+      fcur = fmid;
+      fmid = fnxt;
+    } else if (PFC == 1) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) cur[c] = nxt[c];
+      tcur = tnxt;
+      fcur = fnxt;
+    }
   }
   return mism;
 }
@@ -951,7 +983,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     if constexpr (eng_base(ENG) == 4)
       c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     else if constexpr (NCH > 0)
-      r_check_c<T, true, NCH, eng_tail(ENG)>(smem, Ly, m, tid, TB, sb);
+      r_check_c<T, true, NCH, eng_tail(ENG), QLDPC_PFC>(smem, Ly, m, tid, TB, sb);
     else
       r_check<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     __syncthreads();
@@ -1001,7 +1033,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         // check state for iteration it + 1 (float: pre-scaled by its alpha)
         const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
         if constexpr (NCH > 0)
-          mism = r_check_c<T, false, NCH, eng_tail(ENG)>(smem, Ly, m, tid, TB, sb);
+          mism = r_check_c<T, false, NCH, eng_tail(ENG), QLDPC_PFC>(smem, Ly, m, tid, TB, sb);
         else
           mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha_next);
         if (QLDPC_STAMPS) {

@@ -102,8 +102,9 @@ SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int 
                       int nch = 0, int tail = 0) {
   // fp64 tail layout (rows of 4 chunks + a tail slot, dword-scaled addresses, 1024 threads)
   if (tail) {
-    const bool ok = engine == 3 && precision == 64 && dmax == 4 && ea_shift == 2 && nch == 4 && tb > 512;
-    return ok ? get_rvariant_f64_st(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
+    const bool ok = engine == 3 && dmax == 4 && ea_shift == 2 && nch == (precision == 64 ? 4 : 2) && tb > 512;
+    if (!ok) return SVariant{nullptr, nullptr, nullptr, nullptr};
+    return precision == 64 ? get_rvariant_f64_st(vpl, d3k) : get_rvariant_f32_st(vpl, d3k);
   }
   if (use_f64w(engine, precision, dmax, tb, vpl, ea_shift, nch))
     return dmax == 5 ? get_rvariant_f64_w_d5(vpl, d3k, nch) : get_rvariant_f64_w(vpl, d3k, nch);
@@ -753,16 +754,19 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     if (bp->engine == 3 && precision == 32 && DM == 4 && !r_fits(3, vslots, g->m, tsize) &&
         r_fits(3, vslots, g->m, tsize, 2) && env_int("QLDPC_E3_BIG", 1) != 0)
       bp->ea_shift = 2;
-    // fp64 images over 160 KiB whose rows are one message wider than 4 chunks (space-time
-    // graphs: rows of 9): 4-chunk rows + a tail slot per row, dword-scaled addresses
-    if (bp->engine == 3 && precision == 64 && DM == 4 && bp->nch == 5 && g->max_row == 9 &&
-        !r_fits(3, vslots, g->m, tsize, 2) && env_int("QLDPC_E3_TAIL", 1) != 0) {
-      const int vs4 = (1 + g->m * 4) * 2;
+    // rows one message wider than whole chunks (space-time graphs: rows of 9 = 4 fp64 / 2 fp32
+    // chunks + 1): chunk rows + a tail slot per row, dword-scaled addresses, 1024-thread
+    // workgroups.  fp64: the image fits LDS at all (162.7 KB instead of 176 KB); fp32: the check
+    // phase reads 36 instead of 48 bytes per row through the compile-time-width loop.
+    if (bp->engine == 3 && DM == 4 && g->max_row == 9 && env_int("QLDPC_E3_TAIL", 1) != 0 &&
+        (precision == 32 || !r_fits(3, vslots, g->m, tsize, 2))) {
+      const int nch_t = 8 * tsize / 16;
+      const int vst = (1 + g->m * nch_t) * (16 / tsize);
       int tb = 0, vpl = 0;
-      if (r_fits(3, vs4, g->m, tsize, 2, 1) && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb > 512 &&
+      if (r_fits(3, vst, g->m, tsize, 2, 1) && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb > 512 &&
           vpl >= 4 && vpl <= 8) {
         bp->tail = 1;
-        bp->nch = 4;
+        bp->nch = nch_t;
         bp->ea_shift = 2;
       }
     }

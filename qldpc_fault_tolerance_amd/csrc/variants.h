@@ -50,6 +50,7 @@ SVariant get_rvariant_f64_x(int vpl, int d3k);  // kern_r_f64_x.hip: 257-512 thr
 SVariant get_rvariant_f64_w4(int vpl, int d3k);
 SVariant get_rvariant_f64_st(int vpl, int d3k);  // kern_r_f64_st*.hip: tail layout, 1024 threads (engine id 1013)
 SVariant get_rvariant_f64_st_hi(int vpl, int d3k);
+SVariant get_rvariant_f32_st(int vpl, int d3k);  // kern_r_f32_st.hip: tail layout in float (engine id 1013)
 SVariant get_r4variant_f32(int vpl);
 SVariant get_r4variant_f64(int vpl);
 SVariant get_r4variant_f64_w(int vpl);  // <= 256 threads
