@@ -573,7 +573,11 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
   // way conflict).  Each lane reads its row's chunks rotated by (lane / rows-per-256-B):
   // conflict-free, and the row's min / second min / parity do not depend on the order.
   constexpr int kRows256 = 256 / (16 * NCH) > 0 ? 256 / (16 * NCH) : 1;
-  constexpr bool kRot = (NCH == 4 || NCH == 8) && sizeof(T) == 8;  // fp32 2-chunk rows: 2-way only, not worth its VGPRs
+#ifndef QLDPC_ROT
+#define QLDPC_ROT 1
+#endif
+  // fp32 2-chunk rows: 2-way only, not worth its VGPRs
+  constexpr bool kRot = QLDPC_ROT && (NCH == 4 || NCH == 8) && sizeof(T) == 8;
   const uint32_t rot = kRot ? ((uint32_t)(tid / kRows256) & (uint32_t)(NCH - 1)) : 0u;
   uint32_t coff[NCH];
 #pragma unroll
