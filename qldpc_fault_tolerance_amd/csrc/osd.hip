@@ -379,6 +379,7 @@ struct OsdGpuArgs {
   int m, n, W, RW, rank, method, order, NP;
   int m_lds;  // 1: the matrix lives in LDS, aliasing the sort tables (copied out first), else in the HBM slice
   int bits_off;  // LDS byte offset of the used / syndrome bit-vectors
+  int pbuf_off;  // register-row mode: LDS byte offset of the pivot-row broadcast buffer
   long long ws_words, iws_ints;
 };
 
@@ -395,7 +396,12 @@ __device__ inline u64 ord_key(double x) {
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 
-template <int LB>
+// WR > 0: register-row mode (m <= LB, W <= WR): thread i keeps row i of the permuted H in WR
+// u64 registers through the whole Gauss-Jordan; a pivot's owner publishes the pivot row's words
+// q.. in an LDS buffer and the rows that have the pivot bit xor them in registers, so a row
+// update costs no LDS writes (the word-major LDS / HBM image paid one 8-byte store per word and
+// row).  The reduced rows go to the HBM slice afterwards for the candidate bit-vectors.
+template <int LB, int WR = 0>
 __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
@@ -412,8 +418,9 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   // matrix: LDS when it fits (at offset 0, over the sort tables, which are copied to the
   // workgroup's HBM ints first), else the per-workgroup HBM slice
   // (compile-time per instantiation, so the accesses are ds_* or global_*, never flat)
-  constexpr bool kMLds = LB == kOsdThreadsLds;
-  u64* M = kMLds ? reinterpret_cast<u64*>(smem) : Mg;
+  constexpr bool kRR = WR > 0;
+  constexpr bool kMLds = !kRR && LB == kOsdThreadsLds;
+  u64* M = kMLds ? reinterpret_cast<u64*>(smem) : Mg;  // register-row mode: Mg holds the reduced rows
   int32_t* pivrow = A.iws + (size_t)blockIdx.x * A.iws_ints;
   int32_t* pivpos = pivrow + rank;
   int32_t* swp = pivpos + rank;
@@ -488,6 +495,74 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
       s_piv[0] = s_piv[1] = s_piv[2] = 0x7FFFFFFF;
     }
     __syncthreads();
+    if constexpr (kRR) {
+      // 2-3 (register rows): row i = thread i, words by compile-time index
+      const int i = tid;
+      u64 row[WR];
+#pragma unroll
+      for (int q = 0; q < WR; ++q) row[q] = 0;
+      uint32_t sbit = 0;
+      bool used_r = false;
+      if (i < m) {
+        for (int e = A.rp[i]; e < A.rp[i + 1]; ++e) {
+          const int p = pos[A.ci[e]];
+          const int pq = p >> 6;
+          const u64 bit = 1ull << (p & 63);
+#pragma unroll
+          for (int q = 0; q < WR; ++q) row[q] ^= (pq == q) ? bit : 0ull;
+        }
+        sbit = synd[i] & 1u;
+      }
+      u64* pbuf = reinterpret_cast<u64*>(smem + A.pbuf_off);  // [WR] pivot row, [WR] its syndrome bit
+      OSD_ST(1)
+      int npiv = 0;  // uniform
+#pragma unroll
+      for (int q = 0; q < WR; ++q) {
+        if (q * 64 >= n || npiv >= rank) break;  // uniform
+        const int bend = n - q * 64 < 64 ? n - q * 64 : 64;
+        for (int b = 0; b < bend; ++b) {
+          if (npiv >= rank) break;  // uniform
+          const int p = q * 64 + b;
+          const int slot = p % 3;
+          const bool hb = ((row[q] >> b) & 1ull) != 0;
+          const unsigned long long bal = __ballot(hb && !used_r);
+          if ((tid & 63) == 0 && bal) atomicMin(&s_piv[slot], (tid & ~63) + (__ffsll((long long)bal) - 1));
+          __syncthreads();
+          const int r = s_piv[slot];
+          if (tid == 0) s_piv[(p + 2) % 3] = 0x7FFFFFFF;
+          if (r == 0x7FFFFFFF) continue;  // dependent position (uniform)
+          if (i == r) {
+            used_r = true;
+#pragma unroll
+            for (int q2 = q; q2 < WR; ++q2) pbuf[q2] = row[q2];
+            pbuf[WR] = sbit;
+            pivrow[npiv] = r;
+            pivpos[npiv] = p;
+          }
+          ++npiv;
+          __syncthreads();
+          if (hb && i != r) {
+#pragma unroll
+            for (int q2 = q; q2 < WR; ++q2) row[q2] ^= pbuf[q2];
+            sbit ^= (uint32_t)pbuf[WR];
+          }
+        }
+      }
+      // reduced rows -> the HBM slice (word-major), syndrome bits -> sb
+      if (i < m) {
+#pragma unroll
+        for (int q = 0; q < WR; ++q)
+          if (q < W) Mg[(size_t)q * m + i] = row[q];
+      }
+      const unsigned long long sbal = __ballot(i < m && sbit);
+      if ((tid & 63) == 0) {
+        const int w0 = (tid & ~63) >> 5;
+        if (w0 < (m + 31) / 32) sb[w0] = (uint32_t)sbal;
+        if (w0 + 1 < (m + 31) / 32) sb[w0 + 1] = (uint32_t)(sbal >> 32);
+      }
+      if (tid == 0) s_npiv = npiv;
+      __syncthreads();
+    } else {
     // 2. H with permuted columns, word-major; each thread owns whole rows (LDS mode: the
     // barrier above ended every read of the sort tables this overwrites)
     const int32_t* posr = kMLds ? gpos : pos;
@@ -589,6 +664,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
         }
       }
       __syncthreads();
+    }
     }
     const int r = s_npiv;
     OSD_ST(2)
@@ -726,6 +802,8 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
 struct qldpc_osd_gpu {
   qldpc_osd host;  // shape, method, order, rank
   int device = 0, grid = 0, W = 0, RW = 0, NP = 0, nh = 0, m_lds = 0, bits_off = 0;
+  int wr = 0, pbuf_off = 0;  // register-row mode: compile-time words per row (0 = off), LDS pivot buffer
+  int rr_tb = 0;             // register-row mode: threads per workgroup = m rounded up to waves
   size_t lds = 0;
   long long ws_words = 0, iws_ints = 0;
   qldpc_rt::DevBuf rp, ci, ws, iws;
@@ -782,6 +860,27 @@ __global__ void __launch_bounds__(256) osd_recheck_kernel(const int32_t* rp, con
   }
 }
 
+}  // namespace
+
+namespace {
+// register-row kernels: the compile-time row widths (words) built, smallest first
+// (rows up to 16 words: 1024-thread workgroups, 128 VGPRs; 20-25 words: 768 threads = 3 waves
+// per SIMD, 168 VGPRs, so m <= 768 -- hgp_34_n1600's 768 x 1600 exactly; wider rows spill)
+constexpr int kOsdWR[] = {2, 4, 8, 12, 16, 20, 25};
+constexpr int osd_rr_threads(int wr) { return wr <= 16 ? 1024 : 768; }
+using OsdKern = void (*)(OsdGpuArgs);
+OsdKern osd_rr_kernel(int wr) {
+  switch (wr) {
+    case 2: return &osd_gpu_kernel<1024, 2>;
+    case 4: return &osd_gpu_kernel<1024, 4>;
+    case 8: return &osd_gpu_kernel<1024, 8>;
+    case 12: return &osd_gpu_kernel<1024, 12>;
+    case 16: return &osd_gpu_kernel<1024, 16>;
+    case 20: return &osd_gpu_kernel<768, 20>;
+    case 25: return &osd_gpu_kernel<768, 25>;
+    default: return nullptr;
+  }
+}
 }  // namespace
 
 namespace qldpc_rt {
@@ -844,9 +943,22 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   const size_t lbits = (size_t)((m + 31) / 32) * 8 + 64;
   const char* lds_env = std::getenv("QLDPC_OSD_LDS");
   const bool want_lds = !lds_env || std::atoi(lds_env) != 0;
-  G->m_lds = (want_lds && std::max(lsort, mbytes) + lbits <= (size_t)160 * 1024 - 256) ? 1 : 0;  // 256: static LDS
+  // register-row mode (one row per thread of a 1024-thread workgroup, row words in VGPRs) when
+  // m <= 1024 and n <= 2048; QLDPC_OSD_RR=0 keeps the LDS / HBM image
+  const char* rr_env = std::getenv("QLDPC_OSD_RR");
+  if (!rr_env || std::atoi(rr_env) != 0)
+    for (int wr : kOsdWR)
+      if (wr >= G->W) {
+        if (m <= osd_rr_threads(wr)) {
+          G->wr = wr;
+          G->rr_tb = std::max(64, (m + 63) / 64 * 64);  // one row per thread, no idle waves
+        }
+        break;
+      }
+  G->m_lds = (!G->wr && want_lds && std::max(lsort, mbytes) + lbits <= (size_t)160 * 1024 - 256) ? 1 : 0;  // 256: static LDS
   G->bits_off = (int)(G->m_lds ? std::max(lsort, mbytes) : lsort);
-  G->lds = (size_t)G->bits_off + lbits;
+  G->pbuf_off = (int)(((size_t)G->bits_off + lbits + 15) & ~(size_t)15);
+  G->lds = G->wr ? (size_t)G->pbuf_off + (size_t)(G->wr + 1) * 8 : (size_t)G->bits_off + lbits;
   G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW;
   G->iws_ints = 2ll * rank + 3ll * n;
   auto fail = [&](int code) {
@@ -859,9 +971,11 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)
     return fail(set_err(QLDPC_EHIP, "device CU count"));
   int nb = 0;
-  const void* kf = G->m_lds ? reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreadsLds>)
-                            : reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreads>);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf, G->m_lds ? kOsdThreadsLds : kOsdThreads,
+  const void* kf = G->wr ? reinterpret_cast<const void*>(osd_rr_kernel(G->wr))
+                  : G->m_lds ? reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreadsLds>)
+                             : reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreads>);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf,
+                                                   G->wr ? G->rr_tb : G->m_lds ? kOsdThreadsLds : kOsdThreads,
                                                    G->lds) != hipSuccess || nb <= 0)
     nb = 1;
   G->grid = cus * nb;
@@ -908,9 +1022,12 @@ int qldpc_osd_gpu_decode(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double
   a.B = B;
   a.m = osd->host.m; a.n = osd->host.n; a.W = osd->W; a.RW = osd->RW; a.rank = osd->host.rank;
   a.method = osd->host.method; a.order = osd->host.order; a.NP = osd->NP; a.m_lds = osd->m_lds; a.bits_off = osd->bits_off;
+  a.pbuf_off = osd->pbuf_off;
   a.ws_words = osd->ws_words; a.iws_ints = osd->iws_ints;
   const int grid = (int)std::min<long long>(B, osd->grid);
-  if (osd->m_lds)
+  if (osd->wr)
+    hipLaunchKernelGGL(osd_rr_kernel(osd->wr), dim3(grid), dim3(osd->rr_tb), osd->lds, (hipStream_t)stream, a);
+  else if (osd->m_lds)
     hipLaunchKernelGGL(osd_gpu_kernel<kOsdThreadsLds>, dim3(grid), dim3(kOsdThreadsLds), osd->lds, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(osd_gpu_kernel<kOsdThreads>, dim3(grid), dim3(kOsdThreads), osd->lds, (hipStream_t)stream, a);
