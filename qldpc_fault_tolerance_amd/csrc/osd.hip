@@ -364,6 +364,7 @@ __device__ inline unsigned long long osd_stamp() {
 }
 constexpr int kOsdMaxN = 8192;
 
+
 struct OsdGpuArgs {
   const int32_t* rp;
   const int32_t* ci;
@@ -401,7 +402,7 @@ __device__ inline u64 ord_key(double x) {
 // q.. in an LDS buffer and the rows that have the pivot bit xor them in registers, so a row
 // update costs no LDS writes (the word-major LDS / HBM image paid one 8-byte store per word and
 // row).  The reduced rows go to the HBM slice afterwards for the candidate bit-vectors.
-template <int LB, int WR = 0>
+template <int LB, int WR = 0, int RPT = 1>
 __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
@@ -496,22 +497,27 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
     }
     __syncthreads();
     if constexpr (kRR) {
-      // 2-3 (register rows): row i = thread i, words by compile-time index
-      const int i = tid;
-      u64 row[WR];
+      // 2-3 (register rows): rows tid + j*TB (j < RPT) of the permuted H, words by compile-time index
+      u64 row[RPT][WR];
+      uint32_t sbit[RPT];
+      bool used_r[RPT];
 #pragma unroll
-      for (int q = 0; q < WR; ++q) row[q] = 0;
-      uint32_t sbit = 0;
-      bool used_r = false;
-      if (i < m) {
-        for (int e = A.rp[i]; e < A.rp[i + 1]; ++e) {
-          const int p = pos[A.ci[e]];
-          const int pq = p >> 6;
-          const u64 bit = 1ull << (p & 63);
+      for (int j = 0; j < RPT; ++j) {
+        const int i = tid + j * TB;
 #pragma unroll
-          for (int q = 0; q < WR; ++q) row[q] ^= (pq == q) ? bit : 0ull;
+        for (int q = 0; q < WR; ++q) row[j][q] = 0;
+        sbit[j] = 0;
+        used_r[j] = i >= m;  // rows past m never become candidates
+        if (i < m) {
+          for (int e = A.rp[i]; e < A.rp[i + 1]; ++e) {
+            const int p = pos[A.ci[e]];
+            const int pq = p >> 6;
+            const u64 bit = 1ull << (p & 63);
+#pragma unroll
+            for (int q = 0; q < WR; ++q) row[j][q] ^= (pq == q) ? bit : 0ull;
+          }
+          sbit[j] = synd[i] & 1u;
         }
-        sbit = synd[i] & 1u;
       }
       u64* pbuf = reinterpret_cast<u64*>(smem + A.pbuf_off);  // [WR] pivot row, [WR] its syndrome bit
       OSD_ST(1)
@@ -524,41 +530,65 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
           if (npiv >= rank) break;  // uniform
           const int p = q * 64 + b;
           const int slot = p % 3;
-          const bool hb = ((row[q] >> b) & 1ull) != 0;
-          const unsigned long long bal = __ballot(hb && !used_r);
-          if ((tid & 63) == 0 && bal) atomicMin(&s_piv[slot], (tid & ~63) + (__ffsll((long long)bal) - 1));
+          bool hb[RPT];
+          int wc = 0x7FFFFFFF;  // the wave's first candidate row (rows of slot j precede slot j+1's)
+#pragma unroll
+          for (int j = 0; j < RPT; ++j) {
+            hb[j] = ((row[j][q] >> b) & 1ull) != 0;
+            const unsigned long long bal = __ballot(hb[j] && !used_r[j]);
+            if (wc == 0x7FFFFFFF && bal) wc = (tid & ~63) + j * TB + (__ffsll((long long)bal) - 1);
+          }
+          if ((tid & 63) == 0 && wc != 0x7FFFFFFF) atomicMin(&s_piv[slot], wc);
           __syncthreads();
           const int r = s_piv[slot];
           if (tid == 0) s_piv[(p + 2) % 3] = 0x7FFFFFFF;
           if (r == 0x7FFFFFFF) continue;  // dependent position (uniform)
-          if (i == r) {
-            used_r = true;
 #pragma unroll
-            for (int q2 = q; q2 < WR; ++q2) pbuf[q2] = row[q2];
-            pbuf[WR] = sbit;
-            pivrow[npiv] = r;
-            pivpos[npiv] = p;
-          }
+          for (int j = 0; j < RPT; ++j)
+            if (tid + j * TB == r) {
+              used_r[j] = true;
+#pragma unroll
+              for (int q2 = q; q2 < WR; ++q2) pbuf[q2] = row[j][q2];
+              pbuf[WR] = sbit[j];
+              pivrow[npiv] = r;
+              pivpos[npiv] = p;
+            }
           ++npiv;
           __syncthreads();
-          if (hb && i != r) {
+          bool upd[RPT], any = false;
 #pragma unroll
-            for (int q2 = q; q2 < WR; ++q2) row[q2] ^= pbuf[q2];
-            sbit ^= (uint32_t)pbuf[WR];
+          for (int j = 0; j < RPT; ++j) {
+            upd[j] = hb[j] && tid + j * TB != r;
+            any = any || upd[j];
+          }
+          if (any) {  // one broadcast read of each pivot word serves all of the thread's rows
+#pragma unroll
+            for (int q2 = q; q2 < WR; ++q2) {
+              const u64 pv = pbuf[q2];
+#pragma unroll
+              for (int j = 0; j < RPT; ++j) row[j][q2] ^= upd[j] ? pv : 0ull;
+            }
+            const uint32_t ps = (uint32_t)pbuf[WR];
+#pragma unroll
+            for (int j = 0; j < RPT; ++j) sbit[j] ^= upd[j] ? ps : 0u;
           }
         }
       }
       // reduced rows -> the HBM slice (word-major), syndrome bits -> sb
-      if (i < m) {
 #pragma unroll
-        for (int q = 0; q < WR; ++q)
-          if (q < W) Mg[(size_t)q * m + i] = row[q];
-      }
-      const unsigned long long sbal = __ballot(i < m && sbit);
-      if ((tid & 63) == 0) {
-        const int w0 = (tid & ~63) >> 5;
-        if (w0 < (m + 31) / 32) sb[w0] = (uint32_t)sbal;
-        if (w0 + 1 < (m + 31) / 32) sb[w0 + 1] = (uint32_t)(sbal >> 32);
+      for (int j = 0; j < RPT; ++j) {
+        const int i = tid + j * TB;
+        if (i < m) {
+#pragma unroll
+          for (int q = 0; q < WR; ++q)
+            if (q < W) Mg[(size_t)q * m + i] = row[j][q];
+        }
+        const unsigned long long sbal = __ballot(i < m && sbit[j]);
+        if ((tid & 63) == 0) {
+          const int w0 = ((tid & ~63) + j * TB) >> 5;
+          if (w0 < (m + 31) / 32) sb[w0] = (uint32_t)sbal;
+          if (w0 + 1 < (m + 31) / 32) sb[w0 + 1] = (uint32_t)(sbal >> 32);
+        }
       }
       if (tid == 0) s_npiv = npiv;
       __syncthreads();
@@ -864,11 +894,18 @@ __global__ void __launch_bounds__(256) osd_recheck_kernel(const int32_t* rp, con
 
 namespace {
 // register-row kernels: the compile-time row widths (words) built, smallest first
-// (rows up to 16 words: 1024-thread workgroups, 128 VGPRs; 20-25 words: 768 threads = 3 waves
-// per SIMD, 168 VGPRs, so m <= 768 -- hgp_34_n1600's 768 x 1600 exactly; wider rows spill)
+// Rows up to 16 words: 1024-thread workgroups (128 VGPRs); 20-25 words: 768 threads = 3 waves
+// per SIMD, 168 VGPRs (m <= 768: hgp_34_n1600's 768 x 1600 exactly; wider rows spill).  One row
+// per thread: 2 or 3 rows per thread in 384 / 256 threads (fewer waves reading each broadcast
+// pivot word) measured 16 % / 26 % slower on n1600 (the per-pivot chain is latency-bound).
 constexpr int kOsdWR[] = {2, 4, 8, 12, 16, 20, 25};
-constexpr int osd_rr_threads(int wr) { return wr <= 16 ? 1024 : 768; }
+constexpr int osd_rpt(int) { return 1; }
+inline int osd_rr_threads(int wr) { return wr <= 16 ? 1024 : 768; }
 using OsdKern = void (*)(OsdGpuArgs);
+template <int WR>
+OsdKern osd_rr_wide(int) {
+  return &osd_gpu_kernel<768, WR, 1>;
+}
 OsdKern osd_rr_kernel(int wr) {
   switch (wr) {
     case 2: return &osd_gpu_kernel<1024, 2>;
@@ -876,8 +913,8 @@ OsdKern osd_rr_kernel(int wr) {
     case 8: return &osd_gpu_kernel<1024, 8>;
     case 12: return &osd_gpu_kernel<1024, 12>;
     case 16: return &osd_gpu_kernel<1024, 16>;
-    case 20: return &osd_gpu_kernel<768, 20>;
-    case 25: return &osd_gpu_kernel<768, 25>;
+    case 20: return osd_rr_wide<20>(osd_rpt(wr));
+    case 25: return osd_rr_wide<25>(osd_rpt(wr));
     default: return nullptr;
   }
 }
@@ -949,9 +986,10 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   if (!rr_env || std::atoi(rr_env) != 0)
     for (int wr : kOsdWR)
       if (wr >= G->W) {
-        if (m <= osd_rr_threads(wr)) {
+        const int rpt = osd_rpt(wr);
+        if (m <= osd_rr_threads(wr) * rpt) {
           G->wr = wr;
-          G->rr_tb = std::max(64, (m + 63) / 64 * 64);  // one row per thread, no idle waves
+          G->rr_tb = std::max(64, ((m + rpt - 1) / rpt + 63) / 64 * 64);  // RPT rows per thread, no idle waves
         }
         break;
       }
