@@ -44,6 +44,11 @@
 #ifndef QLDPC_FLIP_BRANCHFREE
 #define QLDPC_FLIP_BRANCHFREE 0
 #endif
+// A/B build: the F-word xors of flipped variables after the whole variable loop (one divergent
+// region) instead of after each variable
+#ifndef QLDPC_FLIPLATE
+#define QLDPC_FLIPLATE 0
+#endif
 #include "bp_slot.h"
 
 namespace qldpc {
@@ -403,7 +408,9 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     lds_st<U, RState<T, DMAX, VPL, ENG>::kSplit>(smem, r_va(R, k, t), nv[t]);
     if (KV) R.ov[KV ? k : 0][KV ? t : 0] = nv[t];
   }
-#if QLDPC_FLIP_BRANCHFREE
+#if QLDPC_FLIPLATE
+  (void)xprev;  // flips applied by r_var after the loop
+#elif QLDPC_FLIP_BRANCHFREE
   // diagnostic variant: every edge xors (x != xprev) into its check's F word, no branch
 #pragma unroll
   for (int t = 0; t < ND; ++t) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), (uint32_t)(x != xprev));
@@ -421,6 +428,15 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
 // fp64 (928k -> 968k shots/s) and fp32 (1.79M -> 1.86M); 2 is 5 % / 10 % slower than 1.
 #ifndef QLDPC_PFC
 #define QLDPC_PFC 0
+#endif
+// Wave priority (s_setprio) in the variable phase / the check phase.  Variable phase at 2 (the
+// other workgroups of the CU are mostly in their check phases or barriers then): n1600 fp32
+// 1.88M -> 1.98M shots/s, fp64 +0.4 %; the check phase raised instead: -1 % / -2 %.
+#ifndef QLDPC_PRIO_V
+#define QLDPC_PRIO_V 2
+#endif
+#ifndef QLDPC_PRIO_C
+#define QLDPC_PRIO_C 0
 #endif
 // How many variables ahead the CS gathers are issued: 2 in the fp64 <= 256-thread family
 // (engine id 103, 256-VGPR budget: +4 VGPRs, n1600 fp64 909k -> 927k shots/s), 1 elsewhere
@@ -472,6 +488,18 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
                            : r_var_one<T, DMAX, VPL, DMAX, ENG>(smem, R, k, pr, o, fdelta, alpha, xp, post, pk);
     xbits |= (x ? 1u : 0u) << k;
   }
+#if QLDPC_FLIPLATE
+  const uint32_t fl = xbits ^ xprev;
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    if ((fl >> k) & 1u) {
+      const int nd = k < D3K ? N3 : DMAX;
+#pragma unroll
+      for (int t = 0; t < DMAX; ++t)
+        if (t < nd) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), 1u);
+    }
+  }
+#endif
   return xbits;
 }
 
@@ -577,7 +605,10 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
 #define QLDPC_ROT 1
 #endif
   // fp32 2-chunk rows: 2-way only, not worth its VGPRs
-  constexpr bool kRot = QLDPC_ROT && (NCH == 4 || NCH == 8) && sizeof(T) == 8;
+#ifndef QLDPC_ROT32
+#define QLDPC_ROT32 1
+#endif
+  constexpr bool kRot = QLDPC_ROT && ((NCH == 4 || NCH == 8) && sizeof(T) == 8 || (QLDPC_ROT32 && NCH == 2 && sizeof(T) == 4));
   const uint32_t rot = kRot ? ((uint32_t)(tid / kRows256) & (uint32_t)(NCH - 1)) : 0u;
   uint32_t coff[NCH];
 #pragma unroll
@@ -1023,7 +1054,11 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         mism = c_check_any<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha);
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
+        // (the tail family runs one workgroup per CU: nothing to take priority over)
+        constexpr int kPV = eng_tail(ENG) ? 0 : QLDPC_PRIO_V;
+        if (kPV) __builtin_amdgcn_s_setprio(kPV);
         xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
+        if (kPV) __builtin_amdgcn_s_setprio(0);
         unsigned long long t1 = 0;
         if (QLDPC_STAMPS) {
           t1 = qstamp();
@@ -1036,10 +1071,12 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         }
         // check state for iteration it + 1 (float: pre-scaled by its alpha)
         const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
+        if (QLDPC_PRIO_C) __builtin_amdgcn_s_setprio(QLDPC_PRIO_C);
         if constexpr (NCH > 0)
           mism = r_check_c<T, false, NCH, eng_tail(ENG), QLDPC_PFC>(smem, Ly, m, tid, TB, sb);
         else
           mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha_next);
+        if (QLDPC_PRIO_C) __builtin_amdgcn_s_setprio(0);
         if (QLDPC_STAMPS) {
           const unsigned long long t = qstamp();
           st_acc[2] += t - st_a;
