@@ -132,14 +132,25 @@ def test_bposd_shot_loop_matches_oracle_per_shot(gpu, oracle):
     assert wer == word_error_rate(fails, S, code.K)[0]
 
 
-@pytest.mark.parametrize("name,t0,method,order", [
-    ("hgp_34_n225", 0, "osd_e", 10), ("hgp_34_n225", 0, "osd_cs", 8), ("hgp_34_n225", 0, "osd_0", 0),
-    ("hgp_34_n1600", 0, "osd_e", 10), ("hgp_34_n1600", 0, "osd_cs", 6), ("hgp_34_n225", 3, "osd_e", 8)])
-def test_gpu_osd_matches_host_osd(gpu, name, t0, method, order):
+# elimination modes of osd_gpu_kernel: the default (register rows for m <= 768 / 1024), the
+# LDS-resident word-major image (QLDPC_OSD_RR=0) and the HBM slice (QLDPC_OSD_RR=0 QLDPC_OSD_LDS=0)
+_OSD_MODES = {"default": {}, "lds": {"QLDPC_OSD_RR": "0"}, "hbm": {"QLDPC_OSD_RR": "0", "QLDPC_OSD_LDS": "0"}}
+
+
+@pytest.mark.parametrize("name,t0,method,order,mode", [
+    ("hgp_34_n225", 0, "osd_e", 10, "default"), ("hgp_34_n225", 0, "osd_cs", 8, "default"), ("hgp_34_n225", 0, "osd_0", 0, "default"),
+    ("hgp_34_n1600", 0, "osd_e", 10, "default"), ("hgp_34_n1600", 0, "osd_cs", 6, "default"), ("hgp_34_n225", 3, "osd_e", 8, "default"),
+    ("hgp_34_n225", 0, "osd_e", 10, "lds"), ("hgp_34_n1600", 0, "osd_e", 10, "lds"), ("hgp_34_n225", 3, "osd_e", 8, "lds"),
+    ("hgp_34_n225", 0, "osd_e", 10, "hbm"), ("hgp_34_n1600", 0, "osd_cs", 6, "hbm"), ("hgp_34_n225", 3, "osd_e", 8, "hbm")])
+def test_gpu_osd_matches_host_osd(gpu, monkeypatch, name, t0, method, order, mode):
     """GPU OSD kernel == native host OSD stage (itself pinned to the oracle in
-    tests/test_osd_cpu.py) on GPU soft-BP posteriors, incl. a rank-deficient
-    space-time graph (t0 = 3 repetitions)."""
+    tests/test_osd_cpu.py) on GPU soft-BP posteriors, incl. a rank-deficient space-time graph
+    (t0 = 3 repetitions), in each elimination mode of the kernel (every reference code takes the
+    register rows by default; the LDS image and the HBM slice serve wider graphs)."""
     from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceOSD, HostOSD
+
+    for k, v in _OSD_MODES[mode].items():
+        monkeypatch.setenv(k, v)
 
     code = codes.get_code(name)
     H = code.hz if t0 == 0 else codes.space_time_csr(code.hz, t0).to_dense().astype(np.uint8)
