@@ -349,7 +349,8 @@ constexpr int kOsdThreadsLds = 1024;  // LDS-resident image: one workgroup per C
 #endif
 // diagnostic builds (QLDPC_STAMPS): per-step cycle sums of osd_gpu_kernel, wave 0 of each
 // workgroup: [0] sort, [1] H load, [2] Gauss-Jordan, [3] swaps + bit-vectors, [4] candidates,
-// [5] outputs, [6] syndromes, [7] positions visited, [8] of [2]: pivot searches + their barrier
+// [5] outputs, [6] syndromes, [7] positions visited, [8] of [2]: pivot searches + their barrier,
+// [9] of [2] (register rows): pivot-row publication + its barrier
 __device__ unsigned long long g_osd_stamps[10];
 __device__ inline unsigned long long osd_stamp() {
 #if QLDPC_STAMPS
@@ -389,6 +390,18 @@ struct OsdGpuArgs {
 __device__ inline void row_xor(u64* __restrict__ dst, const u64* __restrict__ src, int W, int m) {
 #pragma unroll 8
   for (int q = 0; q < W; ++q) dst[(size_t)q * m] ^= src[(size_t)q * m];
+}
+
+// minimum of a 32-bit value over the 64 lanes of a wave (all lanes active): DPP quad and row
+// rotations give each lane its 16-lane row's minimum, four readlanes combine the rows
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+  auto mn = [](uint32_t a, uint32_t b) { return a < b ? a : b; };
+  v = mn(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v = mn(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v = mn(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
+  v = mn(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
+  return mn(mn((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+            mn((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
 }
 
 __device__ inline u64 ord_key(double x) {
@@ -521,30 +534,52 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
       }
       u64* pbuf = reinterpret_cast<u64*>(smem + A.pbuf_off);  // [WR] pivot row, [WR] its syndrome bit
       OSD_ST(1)
-      int npiv = 0;  // uniform
+      int npiv = 0;   // uniform
+      int step3 = 0;  // search step mod 3: s_piv slot of the step (triple-buffered as above)
 #pragma unroll
       for (int q = 0; q < WR; ++q) {
         if (q * 64 >= n || npiv >= rank) break;  // uniform
         const int bend = n - q * 64 < 64 ? n - q * 64 : 64;
-        for (int b = 0; b < bend; ++b) {
-          if (npiv >= rank) break;  // uniform
-          const int p = q * 64 + b;
-          const int slot = p % 3;
-          bool hb[RPT];
-          int wc = 0x7FFFFFFF;  // the wave's first candidate row (rows of slot j precede slot j+1's)
+        // Positions without a candidate row change nothing, so one search step finds the next
+        // pivot of this word directly: the lexicographic minimum of (first set bit >= b, row)
+        // over the unused rows = the first position with a candidate and its lowest row, as the
+        // position-by-position greedy scan picks it (ldpc's pivot set), without a barrier per
+        // dependent position.
+        const u64 wmask = bend < 64 ? (1ull << bend) - 1ull : ~0ull;
+        int b = 0;
+        while (b < bend && npiv < rank) {  // uniform
+          const int slot = step3;
+          step3 = step3 == 2 ? 0 : step3 + 1;
+          unsigned long long ts0 = 0;
+          if (QLDPC_STAMPS) {
+            ts0 = osd_stamp();
+            st[7] += 1;
+          }
+          const u64 lowm = (~0ull << b) & wmask;
+          uint32_t key = 0x7FFFFFFFu;  // (first set bit << 11) | row
 #pragma unroll
           for (int j = 0; j < RPT; ++j) {
-            hb[j] = ((row[j][q] >> b) & 1ull) != 0;
-            const unsigned long long bal = __ballot(hb[j] && !used_r[j]);
-            if (wc == 0x7FFFFFFF && bal) wc = (tid & ~63) + j * TB + (__ffsll((long long)bal) - 1);
+            const u64 mm = used_r[j] ? 0ull : (row[j][q] & lowm);
+            const uint32_t kj = mm ? ((uint32_t)(__ffsll((long long)mm) - 1) << 11) | (uint32_t)(tid + j * TB) : 0x7FFFFFFFu;
+            key = kj < key ? kj : key;
           }
-          if ((tid & 63) == 0 && wc != 0x7FFFFFFF) atomicMin(&s_piv[slot], wc);
+          key = wave_min_u32(key);
+          if ((tid & 63) == 0 && key != 0x7FFFFFFFu) atomicMin(&s_piv[slot], (int)key);
           __syncthreads();
-          const int r = s_piv[slot];
-          if (tid == 0) s_piv[(p + 2) % 3] = 0x7FFFFFFF;
-          if (r == 0x7FFFFFFF) continue;  // dependent position (uniform)
+          if (QLDPC_STAMPS) {
+            const unsigned long long t = osd_stamp();
+            st[8] += t - ts0;
+            ts0 = t;
+          }
+          const int kk = s_piv[slot];
+          if (tid == 0) s_piv[step3 == 2 ? 0 : step3 + 1] = 0x7FFFFFFF;  // re-arm the slot two steps ahead
+          if (kk == 0x7FFFFFFF) break;  // no pivot left in this word (uniform)
+          const int fb = kk >> 11, r = kk & 2047;
+          const int p = q * 64 + fb;
+          bool hb[RPT];
 #pragma unroll
-          for (int j = 0; j < RPT; ++j)
+          for (int j = 0; j < RPT; ++j) {
+            hb[j] = ((row[j][q] >> fb) & 1ull) != 0;
             if (tid + j * TB == r) {
               used_r[j] = true;
 #pragma unroll
@@ -553,8 +588,10 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
               pivrow[npiv] = r;
               pivpos[npiv] = p;
             }
+          }
           ++npiv;
           __syncthreads();
+          if (QLDPC_STAMPS) st[9] += osd_stamp() - ts0;
           bool upd[RPT], any = false;
 #pragma unroll
           for (int j = 0; j < RPT; ++j) {
@@ -572,6 +609,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
 #pragma unroll
             for (int j = 0; j < RPT; ++j) sbit[j] ^= upd[j] ? ps : 0u;
           }
+          b = fb + 1;
         }
       }
       // reduced rows -> the HBM slice (word-major), syndrome bits -> sb
@@ -698,33 +736,44 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
     }
     const int r = s_npiv;
     OSD_ST(2)
-    // 4. Neal's column swaps -> non-pivot order Ht (positions swp[r + j])
-    for (int q = tid; q < n; q += TB) swp[q] = q;
-    __syncthreads();
-    if (tid == 0)
-      for (int i = 0; i < r; ++i) {
-        const int a = swp[i];
-        swp[i] = swp[pivpos[i]];
-        swp[pivpos[i]] = a;
+    // 4. Neal's column swaps -> non-pivot order Ht.  Only the non-pivot positions swp[r + j],
+    // j < nh, are used: each is the identity traced backwards through the transpositions
+    // (i, pivpos[i]), i = r-1 .. 0 -- one thread per needed position, no serial replay.
+    // (Register-row mode stages pivpos in LDS first: the trace reads it r times.)
+    const int32_t* pp = pivpos;
+    if constexpr (kRR) {
+      int32_t* lpp = reinterpret_cast<int32_t*>(smem + A.pbuf_off + (WR + 1) * 8);
+      for (int i = tid; i < r; i += TB) lpp[i] = pivpos[i];
+      __syncthreads();
+      pp = lpp;
+    }
+    for (int x = r + tid; x < r + nh && x < n; x += TB) {
+      int cur = x;
+      for (int i = r - 1; i >= 0; --i) {
+        const int pi = pp[i];
+        cur = cur == i ? pi : (cur == pi ? i : cur);
       }
+      swp[x] = cur;
+    }
     __syncthreads();
-    // 5. S0 and x(h_j) as bit-vectors over the pivot index
+    // 5. S0 and x(h_j) as bit-vectors over the pivot index: one wave per 64-bit word, lane c
+    // forms bit c (pivot q*64 + c) and a ballot packs the word
     const int RWr = (r + 63) / 64;
-    for (int t = tid; t < (1 + nh) * RWr; t += TB) {
+    for (int t = tid >> 6; t < (1 + nh) * RWr; t += TB >> 6) {  // uniform per wave
       const int j = t / RWr, q = t % RWr;
-      u64 v = 0;
-      for (int c = 0; c < 64 && q * 64 + c < r; ++c) {
-        const int row = pivrow[q * 64 + c];
-        u64 bitv;
+      const int c = tid & 63, i = q * 64 + c;
+      bool bitv = false;
+      if (i < r) {
+        const int row = pivrow[i];
         if (j == 0) {
-          bitv = (sb[row >> 5] >> (row & 31)) & 1u;
+          bitv = ((sb[row >> 5] >> (row & 31)) & 1u) != 0;
         } else {
           const int hp = swp[r + j - 1];
-          bitv = (M[(size_t)(hp >> 6) * m + row] >> (hp & 63)) & 1ull;
+          bitv = ((M[(size_t)(hp >> 6) * m + row] >> (hp & 63)) & 1ull) != 0;
         }
-        v |= bitv << c;
       }
-      X[(size_t)j * RW + q] = v;
+      const unsigned long long v = __ballot(bitv);
+      if (c == 0) X[(size_t)j * RW + q] = v;
     }
     if (tid == 0) s_best = ~0ull;
     __syncthreads();
@@ -996,7 +1045,9 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   G->m_lds = (!G->wr && want_lds && std::max(lsort, mbytes) + lbits <= (size_t)160 * 1024 - 256) ? 1 : 0;  // 256: static LDS
   G->bits_off = (int)(G->m_lds ? std::max(lsort, mbytes) : lsort);
   G->pbuf_off = (int)(((size_t)G->bits_off + lbits + 15) & ~(size_t)15);
-  G->lds = G->wr ? (size_t)G->pbuf_off + (size_t)(G->wr + 1) * 8 : (size_t)G->bits_off + lbits;
+  // register-row mode: pivot-row buffer, then pivpos staged for the swap trace (rank ints)
+  G->lds = G->wr ? (size_t)G->pbuf_off + (size_t)(G->wr + 1) * 8 + (size_t)std::max(1, rank) * 4
+                 : (size_t)G->bits_off + lbits;
   G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW;
   G->iws_ints = 2ll * rank + 3ll * n;
   auto fail = [&](int code) {
