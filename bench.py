@@ -311,7 +311,7 @@ def phenl_main(a, torch, dist, world, rank, dev):
                               "kernel": f"whole staged pipeline (wall clock, per GPU); space-time decoder engine {st_engine}"},
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
@@ -368,15 +368,33 @@ def bposd_main(a, torch, dist, world, rank, dev):
                 "residuals (qldpc_mc_set_osd)",
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
 
+_JSON_FD = None  # the real stdout: the JSON line is the only thing written there
+
+
+def emit(out):
+    line = (json.dumps(out) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line)
+
+
 def main():
+    global _JSON_FD
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         sys.exit(spawn_ranks(a.gpus))
+    # library chatter on fd 1 (gloo's connection lines, runtime notices) goes to stderr, so rank 0's
+    # stdout carries exactly one JSON line
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     traffic = None
     if a.workload == "data" and world == 1 and a.pmc_traffic:
@@ -467,7 +485,7 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(code, p, max_iter, a.logical, a.cpu_seconds)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
