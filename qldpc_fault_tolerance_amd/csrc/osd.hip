@@ -364,6 +364,11 @@ __device__ inline unsigned long long osd_stamp() {
 #endif
 }
 constexpr int kOsdMaxN = 8192;
+// A/B build: one barrier per pivot in register-row mode (the candidate row published before the
+// search barrier, per-wave slots of two step parities)
+#ifndef QLDPC_OSD_1B
+#define QLDPC_OSD_1B 0
+#endif
 
 
 struct OsdGpuArgs {
@@ -536,6 +541,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
       OSD_ST(1)
       int npiv = 0;   // uniform
       int step3 = 0;  // search step mod 3: s_piv slot of the step (triple-buffered as above)
+      int spar = 0;   // search step mod 2
 #pragma unroll
       for (int q = 0; q < WR; ++q) {
         if (q * 64 >= n || npiv >= rank) break;  // uniform
@@ -550,6 +556,9 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
         while (b < bend && npiv < rank) {  // uniform
           const int slot = step3;
           step3 = step3 == 2 ? 0 : step3 + 1;
+          const int par = spar;  // QLDPC_OSD_1B: slot half of this step (alternates every step)
+          spar ^= 1;
+          (void)par;
           unsigned long long ts0 = 0;
           if (QLDPC_STAMPS) {
             ts0 = osd_stamp();
@@ -564,6 +573,23 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
             key = kj < key ? kj : key;
           }
           key = wave_min_u32(key);
+#if QLDPC_OSD_1B
+          // one barrier per pivot: the wave's winning row goes to the wave's slot of this step's
+          // parity before the barrier (rewritten two steps later, behind the next barrier)
+          u64* wsl = pbuf + (size_t)((par * (LB / 64) + (tid >> 6)) * (WR + 1));
+          (void)wsl;
+#endif
+          if (QLDPC_OSD_1B && key != 0x7FFFFFFFu) {
+#pragma unroll
+            for (int j = 0; j < RPT; ++j)
+              if ((uint32_t)(tid + j * TB) == (key & 2047u)) {
+#if QLDPC_OSD_1B
+#pragma unroll
+                for (int q2 = q; q2 < WR; ++q2) wsl[q2] = row[j][q2];
+                wsl[WR] = sbit[j];
+#endif
+              }
+          }
           if ((tid & 63) == 0 && key != 0x7FFFFFFFu) atomicMin(&s_piv[slot], (int)key);
           __syncthreads();
           if (QLDPC_STAMPS) {
@@ -582,15 +608,22 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
             hb[j] = ((row[j][q] >> fb) & 1ull) != 0;
             if (tid + j * TB == r) {
               used_r[j] = true;
+              if (!QLDPC_OSD_1B) {
 #pragma unroll
-              for (int q2 = q; q2 < WR; ++q2) pbuf[q2] = row[j][q2];
-              pbuf[WR] = sbit[j];
+                for (int q2 = q; q2 < WR; ++q2) pbuf[q2] = row[j][q2];
+                pbuf[WR] = sbit[j];
+              }
               pivrow[npiv] = r;
               pivpos[npiv] = p;
             }
           }
           ++npiv;
+#if QLDPC_OSD_1B
+          const u64* prow = pbuf + (size_t)(par * (LB / 64) + (r >> 6)) * (WR + 1);
+#else
           __syncthreads();
+          const u64* prow = pbuf;
+#endif
           if (QLDPC_STAMPS) st[9] += osd_stamp() - ts0;
           bool upd[RPT], any = false;
 #pragma unroll
@@ -601,11 +634,11 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
           if (any) {  // one broadcast read of each pivot word serves all of the thread's rows
 #pragma unroll
             for (int q2 = q; q2 < WR; ++q2) {
-              const u64 pv = pbuf[q2];
+              const u64 pv = prow[q2];
 #pragma unroll
               for (int j = 0; j < RPT; ++j) row[j][q2] ^= upd[j] ? pv : 0ull;
             }
-            const uint32_t ps = (uint32_t)pbuf[WR];
+            const uint32_t ps = (uint32_t)prow[WR];
 #pragma unroll
             for (int j = 0; j < RPT; ++j) sbit[j] ^= upd[j] ? ps : 0u;
           }
@@ -742,7 +775,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
     // (Register-row mode stages pivpos in LDS first: the trace reads it r times.)
     const int32_t* pp = pivpos;
     if constexpr (kRR) {
-      int32_t* lpp = reinterpret_cast<int32_t*>(smem + A.pbuf_off + (WR + 1) * 8);
+      int32_t* lpp = reinterpret_cast<int32_t*>(smem + A.pbuf_off + (QLDPC_OSD_1B ? 2 * (LB / 64) : 1) * (WR + 1) * 8);
       for (int i = tid; i < r; i += TB) lpp[i] = pivpos[i];
       __syncthreads();
       pp = lpp;
@@ -1045,8 +1078,10 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   G->m_lds = (!G->wr && want_lds && std::max(lsort, mbytes) + lbits <= (size_t)160 * 1024 - 256) ? 1 : 0;  // 256: static LDS
   G->bits_off = (int)(G->m_lds ? std::max(lsort, mbytes) : lsort);
   G->pbuf_off = (int)(((size_t)G->bits_off + lbits + 15) & ~(size_t)15);
-  // register-row mode: pivot-row buffer, then pivpos staged for the swap trace (rank ints)
-  G->lds = G->wr ? (size_t)G->pbuf_off + (size_t)(G->wr + 1) * 8 + (size_t)std::max(1, rank) * 4
+  // register-row mode: pivot-row buffer (QLDPC_OSD_1B: a slot per wave and step parity), then
+  // pivpos staged for the swap trace (rank ints)
+  const size_t prows = QLDPC_OSD_1B ? 2 * (size_t)(osd_rr_threads(std::max(2, G->wr)) / 64) : 1;
+  G->lds = G->wr ? (size_t)G->pbuf_off + prows * (size_t)(G->wr + 1) * 8 + (size_t)std::max(1, rank) * 4
                  : (size_t)G->bits_off + lbits;
   G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW;
   G->iws_ints = 2ll * rank + 3ll * n;
