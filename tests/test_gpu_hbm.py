@@ -83,7 +83,7 @@ def test_st_decoder_class_default_precision_n1225(gpu, oracle):
     g = dec.space_decoder.geometry()
     assert g["engine"] == 3 and g["lds_bytes"] <= 160 * 1024, g
     mi = int(code.N / 10)
-    for p, B in ((0.01, 150), (0.04, 130)):
+    for p, B in ((0.01, 150), (0.04, 130), (0.025, 600)):
         rng = np.random.default_rng(17 + B)
         e = (rng.random((B, dec.ST_csr.n)) < p).astype(np.uint8)
         synd = dec.ST_csr.matvec(e).astype(np.uint8)
