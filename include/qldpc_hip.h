@@ -250,7 +250,8 @@ int qldpc_bp_degree3_slots(const qldpc_bp *bp, int32_t *d3k);
  * create call falls back to when no LDS engine holds a decode's image (> 160
  * KiB: e.g. the fp64 space-time graph of hgp_34_n1225_q3 at num_rep 3) or a
  * column degree exceeds 8; this entry point forces it for any graph (row and
- * column degree <= 16).  Same decode contract as qldpc_bp_create (the ldpc
+ * column degree <= 12: the compile-time edge blocks kHRow / kHCol of bp_hbm.hip;
+ * larger degrees return QLDPC_ENOTSUP).  Same decode contract as qldpc_bp_create (the ldpc
  * bp_decoder replacement, src/Decoders.py:80-84); min-sum only. */
 int qldpc_bp_create_hbm(qldpc_graph *g, const double *channel_probs, int32_t max_iter, double ms_scaling_factor,
                         int32_t precision, qldpc_bp **out);
@@ -261,7 +262,11 @@ int qldpc_bp_create_hbm(qldpc_graph *g, const double *channel_probs, int32_t max
  * error) on the device, runs the GPU OSD stage (qldpc_osd_gpu) on those, re-checks their
  * residual against H and the logicals, and corrects the per-shot fail flags and the failure
  * counters -- no host copies beyond the per-sector candidate counts.  Engine-3 MC handles
- * only; each OSD handle must be built on its sector decoder's graph (NULL = plain BP). */
+ * only; each OSD handle must be built on its sector decoder's graph (NULL = plain BP).
+ * With an OSD handle set, qldpc_mc_launch is SYNCHRONOUS on its stream (it reads the
+ * candidate counts back to size the OSD launch).  Capture memory per sector is bounded by
+ * QLDPC_OSD_CAPTURE_MB (default 2048; n*11 + m + 8 bytes per slot); a launch with more shots
+ * than slots runs as consecutive pieces, so no candidate is ever dropped. */
 int qldpc_mc_set_osd(qldpc_mc *mc, qldpc_osd_gpu *osd_x, qldpc_osd_gpu *osd_z);
 
 /* Engine 3: extra LDS cycles of one variable-phase pass's CS gathers (summed

@@ -227,6 +227,28 @@ def osd_decode(H, channel_probs, synd, post, osd_method="osd_e", osd_order=10):
     return osd0, best
 
 
+def osd_decode_batch(H, channel_probs, synd, post, osd_method="osd_e", osd_order=10, nthreads=0):
+    """:func:`osd_decode` restated in C (oracle_osd_decode_batch): the same algorithm step
+    for step, fast enough for n1600 OSD-E(10).  Every syndrome is decoded (the caller keeps
+    BP's answer where BP converged).  Returns (osd0, osdw) uint8 [B, n]."""
+    m, n, rp, ci = _csr(H)
+    synd = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.uint8) & 1)
+    post = np.ascontiguousarray(np.atleast_2d(np.asarray(post, np.float64)))
+    B = synd.shape[0]
+    assert synd.shape[1] == m and post.shape == (B, n)
+    probs = np.ascontiguousarray(np.broadcast_to(np.asarray(channel_probs, np.float64), (n,)))
+    o0 = np.zeros((B, n), np.uint8)
+    ow = np.zeros((B, n), np.uint8)
+    meth = OSD_METHODS[osd_method] if isinstance(osd_method, str) else int(osd_method)
+    L = lib()
+    L.oracle_osd_decode_batch.restype = ctypes.c_int
+    L.oracle_osd_decode_batch.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int,
+                                          ctypes.c_int, _u8p, _f64p, _u8p, _u8p, ctypes.c_int64, ctypes.c_int]
+    if L.oracle_osd_decode_batch(m, n, rp, ci, probs, meth, int(osd_order), synd, post, o0, ow, B, int(nthreads)):
+        raise RuntimeError("oracle_osd_decode_batch failed")
+    return o0, ow
+
+
 def philox4x32_10(ctr, key):
     c = (ctypes.c_uint32 * 4)(*ctr)
     k = (ctypes.c_uint32 * 2)(*key)
@@ -307,8 +329,12 @@ def phenl_trace_len(code, num_rep, num_rounds):
 
 def phenl_run(code, px, py, pz, q, seed, shot_begin, shot_count, num_rounds, num_rep, logical_mode="Total",
               p_data=None, p_synd=None, max_iter_st=None, max_iter_2=None, bp_method="minimum_sum",
-              ms_scaling_factor=0.625, precision=64, uniforms=None, per_shot=False, nthreads=0):
-    """Phenomenological space-time shot loop on the CPU (CodeSimulator_Phenon_SpaceTime restated)."""
+              ms_scaling_factor=0.625, precision=64, uniforms=None, per_shot=False, nthreads=0,
+              osd_method=None, osd_order=10):
+    """Phenomenological space-time shot loop on the CPU (CodeSimulator_Phenon_SpaceTime restated).
+
+    ``osd_method`` (e.g. "osd_e"): decoder2 is BPOSD_Decoder (min-sum BP, then the C OSD
+    restatement on the final posteriors when BP did not converge), as the notebooks use."""
     n = code.N
     hz, lz, hx, lx = code.csr("hz"), code.csr("lz"), code.csr("hx"), code.csr("lx")
     mz, mx = hz.m, hx.m
@@ -342,19 +368,26 @@ def phenl_run(code, px, py, pz, q, seed, shot_begin, shot_count, num_rounds, num
     keep = [np.ascontiguousarray(a, np.int32) for a in
             (hz.row_ptr, hz.col_idx, lz.row_ptr, lz.col_idx, hx.row_ptr, hx.col_idx, lx.row_ptr, lx.col_idx)]
     L = lib()
-    L.oracle_phenl_run.restype = ctypes.c_int
-    rc = L.oracle_phenl_run(
-        ctypes.c_int(n),
-        ctypes.c_int(mz), p(keep[0], i32), p(keep[1], i32),
-        ctypes.c_int(lz.m), p(keep[2], i32), p(keep[3], i32),
-        ctypes.c_int(mx), p(keep[4], i32), p(keep[5], i32),
-        ctypes.c_int(lx.m), p(keep[6], i32), p(keep[7], i32),
-        p(pst_x, f64), p(pst_z, f64), p(p2, f64), p(p2, f64),
-        ctypes.c_int(num_rep), ctypes.c_int(int(max_iter_st)), ctypes.c_int(int(max_iter_2)),
-        ctypes.c_int(METHODS[bp_method]), f64(ms_scaling_factor), ctypes.c_int(precision),
-        f64(px), f64(py), f64(pz), f64(q), ctypes.c_uint64(seed), ctypes.c_uint64(shot_begin), ctypes.c_int64(S),
-        ctypes.c_int(num_rounds), ctypes.c_int(mode), p(uniforms, f64), ctypes.byref(cnt),
-        p(fail, ctypes.c_uint8), p(trace, ctypes.c_uint8), ctypes.c_int(int(nthreads)))
+    head = [ctypes.c_int(n),
+            ctypes.c_int(mz), p(keep[0], i32), p(keep[1], i32),
+            ctypes.c_int(lz.m), p(keep[2], i32), p(keep[3], i32),
+            ctypes.c_int(mx), p(keep[4], i32), p(keep[5], i32),
+            ctypes.c_int(lx.m), p(keep[6], i32), p(keep[7], i32),
+            p(pst_x, f64), p(pst_z, f64), p(p2, f64), p(p2, f64),
+            ctypes.c_int(num_rep), ctypes.c_int(int(max_iter_st)), ctypes.c_int(int(max_iter_2))]
+    tail = [f64(px), f64(py), f64(pz), f64(q), ctypes.c_uint64(seed), ctypes.c_uint64(shot_begin), ctypes.c_int64(S),
+            ctypes.c_int(num_rounds), ctypes.c_int(mode), p(uniforms, f64), ctypes.byref(cnt),
+            p(fail, ctypes.c_uint8), p(trace, ctypes.c_uint8), ctypes.c_int(int(nthreads))]
+    if osd_method is None:
+        L.oracle_phenl_run.restype = ctypes.c_int
+        rc = L.oracle_phenl_run(*head, ctypes.c_int(METHODS[bp_method]), f64(ms_scaling_factor),
+                                ctypes.c_int(precision), *tail)
+    else:
+        assert bp_method == "minimum_sum", "BPOSD_Decoder runs min-sum BP"
+        L.oracle_phenl_run_osd.restype = ctypes.c_int
+        meth = OSD_METHODS[osd_method] if isinstance(osd_method, str) else int(osd_method)
+        rc = L.oracle_phenl_run_osd(*head, f64(ms_scaling_factor), ctypes.c_int(precision), *tail,
+                                    ctypes.c_int(meth), ctypes.c_int(int(osd_order)))
     del keep
     if rc:
         raise RuntimeError("oracle_phenl_run failed")

@@ -294,6 +294,206 @@ static int bp_decode_batch_impl(int m, int n, const int32_t *row_ptr, const int3
     return rc ? -1 : 0;
 }
 
+/* ------------------------------------------------------------ OSD (bposd) */
+/*
+ * ldpc 0.1 `bposd_decoder.osd` (the reference's BPOSD_Decoder, src/Decoders.py:26-41)
+ * restated in C: the same algorithm, step for step, as oracle.py's osd_decode (pure
+ * Python, small codes only), so that the n1600 OSD-E(10) candidates can be checked.
+ *   1. stable ascending sort of the columns by the BP posteriors (log_prob_ratios);
+ *   2. Neal's mod2sparse_decomp, "first" strategy, on that column order: for pivot i
+ *      the first column at or after position i with a set bit in a row not yet used
+ *      (rows scanned in index order), swapped into position i; that row becomes row i
+ *      and is added to every later row with the pivot bit;
+ *   3. OSD-0 by forward (recorded row additions) and back substitution;
+ *   4. candidates: osd_e all 2^w inputs on the first w = min(order, n-rank) non-pivot
+ *      columns in natural binary order; osd_cs weight-1 on every non-pivot column then
+ *      weight-2 inside the first w; each solved the same way, the first of strictly
+ *      smaller sum_{j: x_j=1} log(1/p_j) (summed in index order) wins.
+ * Bit-vectors (rows as words over columns / over pivot positions) carry the same GF(2)
+ * values as the byte loops of osd_decode; a column found empty in the remaining rows
+ * stays empty (remaining rows are only ever added to remaining rows), so the pivot scan
+ * skips it thereafter.  Parity of this against bposd itself is unpinned (absent).
+ */
+typedef struct {
+    int m, n, MW, NW, rank, method, order;
+    uint64_t *hrow;  /* [m][NW] H rows over columns  */
+    uint64_t *hcol;  /* [n][MW] H columns over rows  */
+    double *wts;     /* log(1/p_j)                   */
+} osd_ctx_t;
+
+#define BIT(v, i) (((v)[(i) >> 6] >> ((i) & 63)) & 1ull)
+#define FLIP(v, i) ((v)[(i) >> 6] ^= 1ull << ((i) & 63))
+
+static int osd_rank(int m, int NW, const uint64_t *hrow, int n) {
+    uint64_t *A = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)m * NW + 8);
+    if (!A) return -1;
+    memcpy(A, hrow, sizeof(uint64_t) * (size_t)m * NW);
+    int r = 0;
+    for (int c = 0; c < n && r < m; c++) {
+        int p = -1;
+        for (int i = r; i < m; i++) if (BIT(A + (size_t)i * NW, c)) { p = i; break; }
+        if (p < 0) continue;
+        if (p != r) for (int w = 0; w < NW; w++) { uint64_t t = A[(size_t)p * NW + w]; A[(size_t)p * NW + w] = A[(size_t)r * NW + w]; A[(size_t)r * NW + w] = t; }
+        for (int i = 0; i < m; i++)
+            if (i != r && BIT(A + (size_t)i * NW, c))
+                for (int w = 0; w < NW; w++) A[(size_t)i * NW + w] ^= A[(size_t)r * NW + w];
+        r++;
+    }
+    free(A);
+    return r;
+}
+
+static int osd_ctx_init(osd_ctx_t *C, int m, int n, const int32_t *rp, const int32_t *ci, const double *probs,
+                        int method, int order) {
+    C->m = m; C->n = n; C->MW = (m + 63) / 64; C->NW = (n + 63) / 64; C->method = method; C->order = order;
+    C->hrow = (uint64_t *)calloc((size_t)m * C->NW + 1, sizeof(uint64_t));
+    C->hcol = (uint64_t *)calloc((size_t)n * C->MW + 1, sizeof(uint64_t));
+    C->wts = (double *)malloc(sizeof(double) * (size_t)(n + 1));
+    if (!C->hrow || !C->hcol || !C->wts) return -1;
+    for (int i = 0; i < m; i++)
+        for (int e = rp[i]; e < rp[i + 1]; e++) {
+            FLIP(C->hrow + (size_t)i * C->NW, ci[e]);
+            FLIP(C->hcol + (size_t)ci[e] * C->MW, i);
+        }
+    for (int j = 0; j < n; j++) C->wts[j] = log(1.0 / probs[j]);
+    C->rank = osd_rank(m, C->NW, C->hrow, n);
+    return C->rank < 0 ? -1 : 0;
+}
+
+static void osd_ctx_free(osd_ctx_t *C) { free(C->hrow); free(C->hcol); free(C->wts); }
+
+/* stable merge sort of idx by key ascending (`<`: -0 ties +0, as numpy's stable argsort) */
+static void stable_argsort(const double *key, int32_t *idx, int32_t *tmp, int n) {
+    for (int i = 0; i < n; i++) idx[i] = i;
+    for (int wdt = 1; wdt < n; wdt *= 2)
+        for (int lo = 0; lo < n; lo += 2 * wdt) {
+            int mid = lo + wdt < n ? lo + wdt : n, hi = lo + 2 * wdt < n ? lo + 2 * wdt : n;
+            int a = lo, b = mid, k = lo;
+            while (a < mid && b < hi) tmp[k++] = (key[idx[b]] < key[idx[a]]) ? idx[b++] : idx[a++];
+            while (a < mid) tmp[k++] = idx[a++];
+            while (b < hi) tmp[k++] = idx[b++];
+            memcpy(idx + lo, tmp + lo, sizeof(int32_t) * (size_t)(hi - lo));
+        }
+}
+
+static int osd_decode_one(const osd_ctx_t *C, const uint8_t *synd, const double *post, uint8_t *osd0, uint8_t *osdw) {
+    const int m = C->m, n = C->n, MW = C->MW, NW = C->NW, rank = C->rank;
+    const int RW = (rank + 63) / 64 + 1;
+    int32_t *cols = (int32_t *)malloc(sizeof(int32_t) * (size_t)(2 * n + 2 * m + 2 * rank + 4));
+    uint64_t *Bm = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)m * NW + 1));
+    uint64_t *tgt = (uint64_t *)calloc((size_t)rank * MW + 1, sizeof(uint64_t));
+    uint64_t *U = (uint64_t *)calloc((size_t)rank * RW + 1, sizeof(uint64_t));
+    uint64_t *g = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(MW + 1));
+    uint64_t *xp = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)RW);
+    uint8_t *dead = (uint8_t *)calloc((size_t)n + 1, 1), *x = (uint8_t *)malloc((size_t)n + 1);
+    if (!cols || !Bm || !tgt || !U || !g || !xp || !dead || !x) {
+        free(cols); free(Bm); free(tgt); free(U); free(g); free(xp); free(dead); free(x);
+        return -1;
+    }
+    int32_t *tmp = cols + n, *rows = tmp + n, *rinv = rows + m, *opr = rinv + m, *piv = opr + rank;
+    stable_argsort(post, cols, tmp, n);
+    for (int r = 0; r < m; r++) rows[r] = rinv[r] = r;
+    memcpy(Bm, C->hrow, sizeof(uint64_t) * (size_t)m * NW);
+    for (int i = 0; i < rank; i++) {
+        int fk = -1, fr = -1;
+        for (int k = i; k < n && fk < 0; k++) {
+            const int c = cols[k];
+            if (dead[c]) continue;
+            for (int r = 0; r < m; r++)
+                if (BIT(Bm + (size_t)r * NW, c) && rinv[r] >= i) { fk = k; fr = r; break; }
+            if (fk < 0) dead[c] = 1;
+        }
+        if (fk < 0) break; /* cannot happen below rank */
+        int32_t t = cols[fk]; cols[fk] = cols[i]; cols[i] = t;
+        const int kr = rinv[fr];
+        t = rows[kr]; rows[kr] = rows[i]; rows[i] = t;
+        rinv[rows[kr]] = kr;
+        rinv[rows[i]] = i;
+        const int c = cols[i];
+        for (int r2 = 0; r2 < m; r2++)
+            if (BIT(Bm + (size_t)r2 * NW, c) && rinv[r2] > i) {
+                FLIP(tgt + (size_t)i * MW, r2);
+                for (int w = 0; w < NW; w++) Bm[(size_t)r2 * NW + w] ^= Bm[(size_t)fr * NW + w];
+            }
+        opr[i] = fr;
+    }
+    for (int i = 0; i < rank; i++) piv[i] = cols[i];
+    for (int i = 0; i < rank; i++)  /* U[i][j] = Bm[rows[i], piv[j]] for j > i */
+        for (int j = i + 1; j < rank; j++)
+            if (BIT(Bm + (size_t)rows[i] * NW, piv[j])) FLIP(U + (size_t)i * RW, j);
+    const int32_t *ht = cols + rank;
+    const int k = n - rank;
+    /* solve(g): forward over the recorded additions, back substitution over the pivots */
+#define OSD_SOLVE()                                                                          \
+    do {                                                                                     \
+        for (int i = 0; i < rank; i++)                                                       \
+            if (BIT(g, opr[i])) for (int w = 0; w < MW; w++) g[w] ^= tgt[(size_t)i * MW + w];\
+        memset(xp, 0, sizeof(uint64_t) * (size_t)RW);                                       \
+        for (int i = rank - 1; i >= 0; i--) {                                                \
+            uint64_t acc = BIT(g, rows[i]);                                                  \
+            const uint64_t *u = U + (size_t)i * RW;                                          \
+            for (int w = (i + 1) >> 6; w < RW; w++) acc ^= (uint64_t)__builtin_parityll(u[w] & xp[w]);\
+            if (acc & 1ull) FLIP(xp, i);                                                     \
+        }                                                                                    \
+        memset(x, 0, (size_t)n);                                                             \
+        for (int i = 0; i < rank; i++) x[piv[i]] = (uint8_t)BIT(xp, i);                      \
+    } while (0)
+    memset(g, 0, sizeof(uint64_t) * (size_t)(MW + 1));
+    for (int i = 0; i < m; i++) if (synd[i] & 1) FLIP(g, i);
+    OSD_SOLVE();
+    memcpy(osd0, x, (size_t)n);
+    memcpy(osdw, x, (size_t)n);
+    if (C->method != 0 && C->order != 0 && k > 0) {
+        double best_w = 0.0;
+        for (int j = 0; j < n; j++) if (osd0[j]) best_w += C->wts[j];
+        const int w = C->order < k ? C->order : k;
+        const long long ncand = C->method == 1 ? (1ll << w) : (long long)k + (long long)w * (w - 1) / 2;
+        int a = 0, b = 1; /* osd_cs weight-2 pair cursor (i < j inside w) */
+        for (long long l = 0; l < ncand; l++) {
+            int in[24], nin = 0;
+            if (C->method == 1) {
+                for (int j = 0; j < w; j++) if ((l >> j) & 1) in[nin++] = j;
+            } else if (l < k) {
+                in[nin++] = (int)l;
+            } else {
+                in[nin++] = a; in[nin++] = b;
+                if (++b >= w) { ++a; b = a + 1; }
+            }
+            memset(g, 0, sizeof(uint64_t) * (size_t)(MW + 1));
+            for (int i = 0; i < m; i++) if (synd[i] & 1) FLIP(g, i);
+            for (int t = 0; t < nin; t++)
+                for (int q = 0; q < MW; q++) g[q] ^= C->hcol[(size_t)ht[in[t]] * MW + q];
+            OSD_SOLVE();
+            for (int t = 0; t < nin; t++) x[ht[in[t]]] = 1;
+            double wx = 0.0;
+            for (int j = 0; j < n; j++) if (x[j]) wx += C->wts[j];
+            if (wx < best_w) { best_w = wx; memcpy(osdw, x, (size_t)n); }
+        }
+    }
+#undef OSD_SOLVE
+    free(cols); free(Bm); free(tgt); free(U); free(g); free(xp); free(dead); free(x);
+    return 0;
+}
+
+/* Batch entry: synd [B][m], post [B][n] -> osd0 / osdw [B][n] (every syndrome decoded;
+ * the caller applies bposd's "only when BP did not converge"). method 0/1/2 = osd_0/e/cs. */
+ORACLE_API int oracle_osd_decode_batch(int m, int n, const int32_t *row_ptr, const int32_t *col_idx,
+                                       const double *channel_probs, int method, int order, const uint8_t *synd,
+                                       const double *post, uint8_t *osd0, uint8_t *osdw, int64_t B, int nthreads) {
+    if (method == 1 && order > 24) return -1;
+    osd_ctx_t C;
+    if (osd_ctx_init(&C, m, n, row_ptr, col_idx, channel_probs, method, order)) { osd_ctx_free(&C); return -1; }
+    int rc = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1) reduction(| : rc)
+#endif
+    for (int64_t b = 0; b < B; b++)
+        rc |= osd_decode_one(&C, synd + b * m, post + b * n, osd0 + b * n, osdw + b * n) ? 1 : 0;
+    osd_ctx_free(&C);
+    return rc ? -1 : 0;
+}
+
 /* ------------------------------------------------------------- Philox4x32 */
 #define PHILOX_M0 0xD2511F53u
 #define PHILOX_M1 0xCD9E8D57u
@@ -490,6 +690,19 @@ static void csr_mulvec(const int32_t *rp, const int32_t *ci, int m, const uint8_
  * per noisy round the Z then X detector histories, then the final Z then X
  * syndromes (the arrays the decoders are handed).
  */
+static int phenl_run_impl(int n,
+                          int mz, const int32_t *hz_rp, const int32_t *hz_ci,
+                          int kx, const int32_t *lz_rp, const int32_t *lz_ci,
+                          int mx, const int32_t *hx_rp, const int32_t *hx_ci,
+                          int kz, const int32_t *lx_rp, const int32_t *lx_ci,
+                          const double *probs_st_x, const double *probs_st_z,
+                          const double *probs2_x, const double *probs2_z,
+                          int reps, int max_iter_st, int max_iter_2, int method, double alpha, int precision,
+                          double px, double py, double pz, double q, uint64_t seed, uint64_t shot_begin,
+                          int64_t shot_count, int num_rounds, int logical_mode, const double *uniforms,
+                          oracle_counters_t *out, uint8_t *fail_out, uint8_t *trace_out, int nthreads,
+                          int osd_method, int osd_order);
+
 ORACLE_API int oracle_phenl_run(int n,
                                 int mz, const int32_t *hz_rp, const int32_t *hz_ci,
                                 int kx, const int32_t *lz_rp, const int32_t *lz_ci,
@@ -501,6 +714,46 @@ ORACLE_API int oracle_phenl_run(int n,
                                 double px, double py, double pz, double q, uint64_t seed, uint64_t shot_begin,
                                 int64_t shot_count, int num_rounds, int logical_mode, const double *uniforms,
                                 oracle_counters_t *out, uint8_t *fail_out, uint8_t *trace_out, int nthreads) {
+    return phenl_run_impl(n, mz, hz_rp, hz_ci, kx, lz_rp, lz_ci, mx, hx_rp, hx_ci, kz, lx_rp, lx_ci, probs_st_x,
+                          probs_st_z, probs2_x, probs2_z, reps, max_iter_st, max_iter_2, method, alpha, precision, px,
+                          py, pz, q, seed, shot_begin, shot_count, num_rounds, logical_mode, uniforms, out, fail_out,
+                          trace_out, nthreads, -1, 0);
+}
+
+/* The same with decoder2 = BPOSD_Decoder (src/Decoders.py:26-41; the Threshold notebook's
+ * CodeFamilyPhenlThreshold final round): min-sum BP on the perfect round, then, when it did
+ * not converge, the OSD restated above on its final log_prob_ratios (osd_method 0/1/2). */
+ORACLE_API int oracle_phenl_run_osd(int n,
+                                    int mz, const int32_t *hz_rp, const int32_t *hz_ci,
+                                    int kx, const int32_t *lz_rp, const int32_t *lz_ci,
+                                    int mx, const int32_t *hx_rp, const int32_t *hx_ci,
+                                    int kz, const int32_t *lx_rp, const int32_t *lx_ci,
+                                    const double *probs_st_x, const double *probs_st_z,
+                                    const double *probs2_x, const double *probs2_z,
+                                    int reps, int max_iter_st, int max_iter_2, double alpha, int precision,
+                                    double px, double py, double pz, double q, uint64_t seed, uint64_t shot_begin,
+                                    int64_t shot_count, int num_rounds, int logical_mode, const double *uniforms,
+                                    oracle_counters_t *out, uint8_t *fail_out, uint8_t *trace_out, int nthreads,
+                                    int osd_method, int osd_order) {
+    if (osd_method < 0 || osd_method > 2) return -1;
+    return phenl_run_impl(n, mz, hz_rp, hz_ci, kx, lz_rp, lz_ci, mx, hx_rp, hx_ci, kz, lx_rp, lx_ci, probs_st_x,
+                          probs_st_z, probs2_x, probs2_z, reps, max_iter_st, max_iter_2, 1, alpha, precision, px,
+                          py, pz, q, seed, shot_begin, shot_count, num_rounds, logical_mode, uniforms, out, fail_out,
+                          trace_out, nthreads, osd_method, osd_order);
+}
+
+static int phenl_run_impl(int n,
+                          int mz, const int32_t *hz_rp, const int32_t *hz_ci,
+                          int kx, const int32_t *lz_rp, const int32_t *lz_ci,
+                          int mx, const int32_t *hx_rp, const int32_t *hx_ci,
+                          int kz, const int32_t *lx_rp, const int32_t *lx_ci,
+                          const double *probs_st_x, const double *probs_st_z,
+                          const double *probs2_x, const double *probs2_z,
+                          int reps, int max_iter_st, int max_iter_2, int method, double alpha, int precision,
+                          double px, double py, double pz, double q, uint64_t seed, uint64_t shot_begin,
+                          int64_t shot_count, int num_rounds, int logical_mode, const double *uniforms,
+                          oracle_counters_t *out, uint8_t *fail_out, uint8_t *trace_out, int nthreads,
+                          int osd_method, int osd_order) {
     const int m[2] = {mz, mx};
     const int32_t *hrp[2] = {hz_rp, hx_rp}, *hci[2] = {hz_ci, hx_ci};
     const int32_t *lrp[2] = {lz_rp, lx_rp}, *lci[2] = {lz_ci, lx_ci};
@@ -517,6 +770,11 @@ ORACLE_API int oracle_phenl_run(int n,
     bp_params_t PSs[2] = {{norm_max_iter(max_iter_st, GS[0].n), method, alpha},
                           {norm_max_iter(max_iter_st, GS[1].n), method, alpha}};
     bp_params_t P2 = {norm_max_iter(max_iter_2, n), method, alpha};
+    osd_ctx_t OC[2];
+    memset(OC, 0, sizeof(OC));
+    if (osd_method >= 0)
+        for (int s = 0; s < 2; s++)
+            if (osd_ctx_init(&OC[s], m[s], n, hrp[s], hci[s], p2[s], osd_method, osd_order)) return -1;
     const int need[2] = {logical_mode != 1, logical_mode != 0};
     const double t1 = pz, t2 = pz + px, t3 = (pz + px) + py;
     const int Pw = n + mx + mz;
@@ -540,6 +798,8 @@ ORACLE_API int oracle_phenl_run(int n,
         uint8_t *cur[2], *hist[2], *det = (uint8_t *)malloc((size_t)reps * mm + 1);
         uint8_t *ser[2], *syn = (uint8_t *)malloc((size_t)mm + 1), *chk = (uint8_t *)malloc((size_t)mm + 1);
         uint8_t *r = (uint8_t *)malloc((size_t)n);
+        uint8_t *o0 = (uint8_t *)malloc((size_t)n), *ow = (uint8_t *)malloc((size_t)n);
+        double *post = (double *)malloc(sizeof(double) * (size_t)n);
         for (int s = 0; s < 2; s++) {
             cur[s] = (uint8_t *)malloc((size_t)n);
             hist[s] = (uint8_t *)malloc((size_t)reps * m[s] + 1);
@@ -605,6 +865,11 @@ ORACLE_API int oracle_phenl_run(int n,
                 if (precision == 32) { conv = bp_run_f32(&G2[s], &P2, &w32f[s], syn, &it); e = w32f[s].dec; }
                 else { conv = bp_run_f64(&G2[s], &P2, &w64f[s], syn, &it); e = w64f[s].dec; }
                 loc.sector_decodes[s]++; loc.sector_iters[s] += it; loc.sector_nonconv[s] += !conv;
+                if (osd_method >= 0 && !conv) {  /* bposd_decoder: OSD on the final log_prob_ratios */
+                    for (int p = 0; p < n; p++) post[p] = precision == 32 ? (double)w32f[s].lpr[p] : w64f[s].lpr[p];
+                    if (osd_decode_one(&OC[s], syn, post, o0, ow)) rc |= 1;
+                    e = ow;
+                }
                 for (int p = 0; p < n; p++) r[p] = cur[s][p] ^ e[p];
                 csr_mulvec(hrp[s], hci[s], m[s], r, chk);
                 int f = 0;
@@ -627,7 +892,7 @@ ORACLE_API int oracle_phenl_run(int n,
             else { ws_free_f64(&w64s[s]); ws_free_f64(&w64f[s]); }
             free(cur[s]); free(hist[s]); free(ser[s]);
         }
-        free(det); free(syn); free(chk); free(r);
+        free(det); free(syn); free(chk); free(r); free(o0); free(ow); free(post);
 #ifdef _OPENMP
 #pragma omp critical
 #endif
@@ -640,6 +905,7 @@ ORACLE_API int oracle_phenl_run(int n,
         }
     }
     for (int s = 0; s < 2; s++) { graph_free(&G2[s]); graph_free(&GS[s]); free(srp[s]); free(sci[s]); }
+    if (osd_method >= 0) { osd_ctx_free(&OC[0]); osd_ctx_free(&OC[1]); }
     if (out) *out = tot;
     return rc ? -1 : 0;
 }

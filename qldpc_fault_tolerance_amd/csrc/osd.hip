@@ -377,6 +377,7 @@ struct OsdGpuArgs {
   const uint8_t* synd;     // [B][m]
   const double* post;      // [B][n]
   const uint8_t* conv;     // [B] or null
+  const long long* shot;   // [B] or null: fused-loop capture slots, < 0 = BP converged (skipped)
   const uint8_t* bp_corr;  // [B][n] or null
   uint8_t* out0;           // [B][n] or null
   uint8_t* outw;           // [B][n]
@@ -461,6 +462,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   for (long long b = blockIdx.x; b < A.B; b += gridDim.x) {
     uint8_t* ow = A.outw + b * (long long)n;
     uint8_t* o0 = A.out0 ? A.out0 + b * (long long)n : nullptr;
+    if (A.shot && A.shot[b] < 0) continue;  // captured decode that converged at max_iter: no OSD
     if (A.conv && A.conv[b]) {  // BP converged: bposd_decoder returns the BP decoding
       for (int j = tid; j < n; j += TB) {
         const uint8_t v = A.bp_corr[b * (long long)n + j];
@@ -1009,7 +1011,7 @@ int osd_gpu_bposd_stage(qldpc_osd_gpu* osd, const uint8_t* synd, const double* p
                         const long long* shot, uint8_t* outw, long long ncand, const unsigned long long* lmask, int kw,
                         int q, int logical_mode, uint8_t* fail, unsigned long long* counters, hipStream_t stream) {
   if (ncand <= 0) return 0;
-  int rc = qldpc_osd_gpu_decode(osd, synd, post, nullptr, nullptr, nullptr, outw, ncand, stream);
+  int rc = osd_gpu_decode_slots(osd, synd, post, nullptr, shot, nullptr, nullptr, outw, ncand, stream);
   if (rc) return rc;
   const int grid = (int)std::min<long long>(ncand, 4096);
   hipLaunchKernelGGL(osd_recheck_kernel, dim3(grid), dim3(256), 0, stream, static_cast<const int32_t*>(osd->rp.p),
@@ -1131,8 +1133,13 @@ int qldpc_debug_osd_stamps(unsigned long long* out) {
 }
 #endif
 
-int qldpc_osd_gpu_decode(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double* d_post, const uint8_t* d_conv,
-                         const uint8_t* d_bp_corr, uint8_t* d_out0, uint8_t* d_outw, int64_t B, void* stream) {
+}  // extern "C"
+
+namespace qldpc_rt {
+// qldpc_osd_gpu_decode with the fused loop's capture-slot shot indices (slots < 0 are skipped)
+int osd_gpu_decode_slots(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double* d_post, const uint8_t* d_conv,
+                         const long long* d_shot, const uint8_t* d_bp_corr, uint8_t* d_out0, uint8_t* d_outw,
+                         int64_t B, void* stream) {
   if (!osd || (B > 0 && (!d_synd || !d_post || !d_outw))) return set_err(QLDPC_EINVAL, "NULL argument");
   if (d_conv && !d_bp_corr) return set_err(QLDPC_EINVAL, "conv needs bp_corr");
   if (B <= 0) return 0;
@@ -1140,7 +1147,8 @@ int qldpc_osd_gpu_decode(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double
   OsdGpuArgs a;
   a.rp = static_cast<const int32_t*>(osd->rp.p);
   a.ci = static_cast<const int32_t*>(osd->ci.p);
-  a.synd = d_synd; a.post = d_post; a.conv = d_conv; a.bp_corr = d_bp_corr; a.out0 = d_out0; a.outw = d_outw;
+  a.synd = d_synd; a.post = d_post; a.conv = d_conv; a.shot = d_shot; a.bp_corr = d_bp_corr; a.out0 = d_out0;
+  a.outw = d_outw;
   a.ws = static_cast<u64*>(osd->ws.p);
   a.iws = static_cast<int32_t*>(osd->iws.p);
   a.B = B;
@@ -1157,6 +1165,13 @@ int qldpc_osd_gpu_decode(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double
     hipLaunchKernelGGL(osd_gpu_kernel<kOsdThreads>, dim3(grid), dim3(kOsdThreads), osd->lds, (hipStream_t)stream, a);
   QLDPC_HIP(hipGetLastError());
   return 0;
+}
+}  // namespace qldpc_rt
+
+extern "C" {
+int qldpc_osd_gpu_decode(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double* d_post, const uint8_t* d_conv,
+                         const uint8_t* d_bp_corr, uint8_t* d_out0, uint8_t* d_outw, int64_t B, void* stream) {
+  return qldpc_rt::osd_gpu_decode_slots(osd, d_synd, d_post, d_conv, nullptr, d_bp_corr, d_out0, d_outw, B, stream);
 }
 
 }  // extern "C"

@@ -1154,6 +1154,7 @@ int qldpc_mc_set_osd(qldpc_mc* mc, qldpc_osd_gpu* osd_x, qldpc_osd_gpu* osd_z) {
   }
   mc->osd[0] = osd_x;
   mc->osd[1] = osd_z;
+  mc->c_cap = 0;  // the next launch (re)allocates the capture buffers of every enabled sector
   return 0;
 }
 
@@ -1199,6 +1200,32 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
                             d_err, d_corr, d_iters, (hipStream_t)stream);
   }
   QLDPC_HIP(hipSetDevice((mc->dec[0] ? mc->dec[0] : mc->dec[1])->g->device));
+  const bool bposd = mc->engine != 1 && ((need[0] && mc->osd[0]) || (need[1] && mc->osd[1]));
+  if (bposd) {
+    // capture slots per sector, bounded by a memory budget (QLDPC_OSD_CAPTURE_MB per sector,
+    // default 2048); a launch larger than that runs as pieces of at most c_cap shots, each
+    // shot claims at most one slot per sector, so no candidate can ever be dropped
+    long long slot_bytes = 0;
+    for (int q = 0; q < 2; ++q)
+      if (need[q] && mc->osd[q]) {
+        const long long n = mc->dec[q]->g->n, m = mc->dec[q]->g->m;
+        slot_bytes = std::max(slot_bytes, n * 8 + m + n + 8 + n);
+      }
+    const long long budget = (long long)std::max(1, env_int("QLDPC_OSD_CAPTURE_MB", 2048)) << 20;
+    const long long slots = std::max<long long>(1024, budget / slot_bytes);
+    if (shot_count > slots) {
+      const long long n = (mc->dec[0] ? mc->dec[0] : mc->dec[1])->g->n;
+      for (long long off = 0; off < shot_count; off += slots) {
+        const long long c = std::min(slots, shot_count - off);
+        int rc = qldpc_mc_launch(mc, px, py, pz, seed, shot_begin + (uint64_t)off, c, logical_mode,
+                                 d_uniforms ? d_uniforms + off * n : nullptr, d_counters, d_fail ? d_fail + off : nullptr,
+                                 d_err ? d_err + off * n : nullptr, d_corr ? d_corr + off * 2 * n : nullptr,
+                                 d_iters ? d_iters + off * 2 : nullptr, grid_blocks, stream);
+        if (rc) return rc;
+      }
+      return 0;
+    }
+  }
   const long long cap = (long long)mc->blocks_per_cu * mc->cus;
   // thresholds of the 3-way split, in the evaluation order of src/Simulators.py:102-108
   const double t1 = pz, t2 = pz + px, t3 = (pz + px) + py;
@@ -1258,8 +1285,7 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
     if (nchunks > 0x7fffffffLL) return set_err(QLDPC_EINVAL, "too many shots for one launch (chunk count >= 2^31)");
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
-    // BP+OSD: capture buffers sized for every decode of the launch
-    const bool bposd = (need[0] && mc->osd[0]) || (need[1] && mc->osd[1]);
+    // BP+OSD: capture buffers with one slot per shot of this launch (<= the budgeted slots)
     hipStream_t st = (hipStream_t)stream;
     if (bposd) {
       if (mc->c_cap < shot_count) {
@@ -1298,7 +1324,9 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
       QLDPC_HIP(hipStreamSynchronize(st));
       for (int q = 0; q < 2; ++q) {
         if (!(need[q] && mc->osd[q]) || nc[q] == 0) continue;
-        const long long ncand = std::min<long long>(nc[q], a.c_cap);
+        if ((long long)nc[q] > a.c_cap)  // cannot happen (one slot per shot and sector): never drop silently
+          return set_err(QLDPC_EINVAL, "BP+OSD capture overflow: more candidates than capture slots");
+        const long long ncand = nc[q];
         int rc = osd_gpu_bposd_stage(mc->osd[q], static_cast<const uint8_t*>(mc->c_synd[q].p),
                                      static_cast<const double*>(mc->c_post[q].p), static_cast<const uint8_t*>(mc->c_err[q].p),
                                      static_cast<const long long*>(mc->c_shot[q].p), static_cast<uint8_t*>(mc->c_outw[q].p),

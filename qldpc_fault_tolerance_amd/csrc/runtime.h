@@ -94,7 +94,9 @@ struct qldpc_mc {
   // staged pipeline (staged.hip): product-sum decoders, or QLDPC_MC_STAGED=1
   bool staged = false;
   long long sbatch = 0;
-  // BP+OSD (qldpc_mc_set_osd): GPU OSD per sector on the decodes that reached max_iter
+  // BP+OSD (qldpc_mc_set_osd): GPU OSD per sector on the decodes that reached max_iter.
+  // c_cap capture slots per sector (bounded by QLDPC_OSD_CAPTURE_MB); a launch is split into
+  // pieces of at most c_cap shots, so a slot can never be lost (one slot per shot and sector)
   qldpc_osd_gpu* osd[2] = {nullptr, nullptr};
   long long c_cap = 0;
   qldpc_rt::DevBuf c_post[2], c_synd[2], c_err[2], c_shot[2], c_outw[2], c_n, c_fail;
@@ -117,6 +119,10 @@ bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g);
 int osd_gpu_bposd_stage(qldpc_osd_gpu* osd, const uint8_t* synd, const double* post, const uint8_t* err,
                         const long long* shot, uint8_t* outw, long long ncand, const unsigned long long* lmask, int kw,
                         int q, int logical_mode, uint8_t* fail, unsigned long long* counters, hipStream_t stream);
+// qldpc_osd_gpu_decode that skips the capture slots whose shot index is < 0 (osd.hip)
+int osd_gpu_decode_slots(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double* d_post, const uint8_t* d_conv,
+                         const long long* d_shot, const uint8_t* d_bp_corr, uint8_t* d_out0, uint8_t* d_outw,
+                         int64_t B, void* stream);
 
 // engine 6 (bp_hbm.hip)
 int hbm_prepare(qldpc_bp* bp);

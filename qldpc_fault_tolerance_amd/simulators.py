@@ -227,29 +227,45 @@ class CodeSimulator_DataError:
         need_x = self.eval_logical_type != "Z"
         need_z = self.eval_logical_type != "X"
         decs = [d for d, need in ((self.decoder_x, need_x), (self.decoder_z, need_z)) if need]
-        if all(getattr(d, "gpu_osd", None) is not None for d in decs):
+        if all(getattr(d, "gpu_osd", None) is not None for d in decs) and self._bposd_device_mc(need_x, need_z):
             return self._bposd_counts_device(num_run, batch, keep_shots, need_x, need_z)
         return self._bposd_counts_host(num_run, min(int(batch), 16384), keep_shots)
 
-    def _bposd_counts_device(self, num_run, batch, keep_shots, need_x, need_z):
-        from .engine import DeviceBP, DeviceMC, MCResult, _torch
-
-        torch = _torch()
-        if self.seed is None:
-            self.seed = random.getrandbits(64)
+    def _bposd_device_mc(self, need_x, need_z):
+        """The device-resident BP+OSD loop needs the fused engine-3 MC kernel
+        (``qldpc_mc_set_osd``); graphs outside its envelope, a forced engine
+        (``QLDPC_ENGINE``) or the staged pipeline (``QLDPC_MC_STAGED=1``) keep the
+        host-assisted loop.  Returns the MC handle, or None (decided once)."""
         if getattr(self, "_bposd_dev", None) is None:
+            from ._native import QldpcError
+            from .engine import DeviceBP, DeviceMC
+
             def fast(dec, vpl=0):
                 b = dec.decoder  # the soft (engine-1) BP: same graph, priors, max_iter, alpha, precision
                 return DeviceBP(None, b.channel_probs, max_iter=b.max_iter, bp_method="minimum_sum",
                                 ms_scaling_factor=b.ms_scaling_factor, precision=b.precision, graph=b.graph,
                                 vars_per_thread=vpl)
 
+            self._bposd_dev = False
             bx = fast(self.decoder_x) if need_x else None
             # one fused kernel serves both sectors: the Z sector takes the X sector's geometry
             bz = fast(self.decoder_z, bx.geometry()["vars_per_thread"] if bx is not None else 0) if need_z else None
-            mc = DeviceMC(self.code, bx, bz)
-            mc.set_osd(self.decoder_x.gpu_osd if need_x else None, self.decoder_z.gpu_osd if need_z else None)
-            self._bposd_dev = mc
+            if all(b is None or b.geometry()["engine"] == 3 for b in (bx, bz)):
+                mc = DeviceMC(self.code, bx, bz)
+                try:
+                    mc.set_osd(self.decoder_x.gpu_osd if need_x else None,
+                               self.decoder_z.gpu_osd if need_z else None)
+                    self._bposd_dev = mc
+                except QldpcError:  # staged MC or another engine: the host-assisted loop
+                    pass
+        return self._bposd_dev or None
+
+    def _bposd_counts_device(self, num_run, batch, keep_shots, need_x, need_z):
+        from .engine import MCResult, _torch
+
+        torch = _torch()
+        if self.seed is None:
+            self.seed = random.getrandbits(64)
         mc = self._bposd_dev
         rank, ws = parallel.world()
         b, c = parallel.shard_range(num_run, rank, ws, begin=self._shot_offset)

@@ -62,8 +62,10 @@ class OracleBP:
                                  alpha=float(ms_scaling_factor), probs=self.channel_probs.copy()))
 
     def decode(self, synd):
-        corr, _, _ = oracle.bp_decode_batch(self.H, self.channel_probs, self.max_iter, self.bp_method, self.alpha,
-                                            np.asarray(synd).reshape(1, -1), 64)
+        if not hasattr(self, "_csr"):  # converted once per decoder object (dense H -> CSR)
+            self._csr = codes.CSR.from_dense(self.H)
+        corr, _, _ = oracle.bp_decode_batch(self._csr, self.channel_probs, self.max_iter, self.bp_method, self.alpha,
+                                            np.asarray(synd).reshape(1, -1), 64, nthreads=1)
         return corr[0].astype(int)
 
 
@@ -342,7 +344,7 @@ def main_configs():
             out[f"{tag}_gen_{gtag}_ex"] = np.packbits(np.array(E_x, dtype=np.uint8), axis=-1)
             out[f"{tag}_gen_{gtag}_ez"] = np.packbits(np.array(E_z, dtype=np.uint8), axis=-1)
         # ---- A1-A3, A6-A8: _single_run with the reference decoder factory (EvalWER data branch)
-        S = 24 if n > 1000 else 40
+        S = 500  # shots per (code, p): >= 500 (VERDICT r02 asked for thicker fixtures)
         for p in (0.04, 0.08):
             dx = cls.GetDecoder({"h": code.hz, "p_data": p})
             dz = cls.GetDecoder({"h": code.hx, "p_data": p})
@@ -377,7 +379,7 @@ def main_configs():
         code=code, decoder1_x=d1x, decoder1_z=d1z, decoder2_x=d2x, decoder2_z=d2z,
         pauli_error_probs=[p / 2] * 3, q=p, eval_logical_type="Total", num_rep=3)
     flags = []
-    for s in range(6):
+    for s in range(100):
         random.seed(51000 + s)
         flags.append(int(sim._single_run(3)))  # 2 noisy rounds of 3 repetitions + the perfect round
     out["st1225_seed0"] = np.array([51000])
@@ -463,8 +465,55 @@ def main_fits():
     print("wrote", path, len(out), "arrays")
 
 
+def main_notebook():
+    """The Threshold notebook's own fit (``.ipynb_checkpoints/Threshold-checkpoint.ipynb`` cells 1-2:
+    ``FitDistance`` / ``EmpericalFit`` / ``ThresholdEst``, lines 33-120) -> tests/golden/notebook_fits.npz.
+
+    The two cells' source is executed as the notebook did (no plot), on fixed WER arrays over the
+    p grids of cells 16 and 25: inputs and the returned ``(A, p_c)`` are stored, to pin the
+    restatement in tests/notebook_pin.py that the threshold pin (tests/test_gpu_notebook_pin.py) uses.
+    """
+    import contextlib
+    import copy
+    import io
+    import json
+
+    import matplotlib.pyplot as plt
+    from scipy.optimize import curve_fit
+
+    nb = json.load(open(os.path.join(os.path.dirname(REF_SRC), ".ipynb_checkpoints", "Threshold-checkpoint.ipynb")))
+    ns = {"np": np, "copy": copy, "plt": plt, "curve_fit": curve_fit}
+    for c in (1, 2):
+        exec("".join(nb["cells"][c]["source"]), ns)
+    rng = np.random.default_rng(2024)
+    out = {}
+    grids = {"lp": np.linspace(2e-2, 3.5e-2, 6), "toric": np.linspace(0.8e-2, 2e-2, 6)}
+    k = 0
+    for gname, P in grids.items():
+        for d, pc, A in (((6, 8, 10), 0.05, 0.02), ((3, 5, 7), 0.03, 0.05), ((2, 3, 4), 0.06, 0.1)):
+            for noise in (0.0, 0.1, 0.3):
+                wer = np.array([A * (P / pc) ** (dd / 2) for dd in d]) * (1 + noise * rng.standard_normal((3, 6)))
+                wer = np.abs(wer)
+                buf = io.StringIO()
+                try:
+                    with contextlib.redirect_stdout(buf):  # ThresholdEst returns p_c and prints "A: .. p_c: .."
+                        pc_fit = ns["ThresholdEst"](P, wer, False)
+                    words = buf.getvalue().split()
+                    res = np.array([float(words[words.index("A:") + 1]), float(pc_fit)])
+                except Exception:  # noqa: BLE001
+                    res = np.array([np.nan, np.nan])
+                out[f"case{k}_p"], out[f"case{k}_wer"], out[f"case{k}_A_pc"] = P, wer, res
+                k += 1
+    out["ncases"] = np.array([k])
+    path = os.path.join(HERE, "notebook_fits.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, k, "cases")
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "phen":
+    if len(sys.argv) > 1 and sys.argv[1] == "notebook":
+        main_notebook()
+    elif len(sys.argv) > 1 and sys.argv[1] == "phen":
         main_phen()
     elif len(sys.argv) > 1 and sys.argv[1] == "configs":
         main_configs()

@@ -179,13 +179,13 @@ def test_bposd_decoder_host_and_gpu_osd_agree(gpu):
     assert np.array_equal(a.decode_batch(synd), b.decode_batch(synd))
 
 
-def test_phenl_space_time_with_bposd_final_round(gpu):
+def test_phenl_space_time_with_bposd_final_round(gpu, oracle):
     """CodeSimulator_Phenon_SpaceTime with decoder2 = BPOSD_Decoder (the notebooks'
     final-round decoder): the staged GPU pipeline runs soft BP + GPU OSD on the
     perfect round.  Same seed as with a BP final round: identical detector
-    traces (noise and ST decodes do not depend on decoder2), and per sample the
-    BP+OSD verdict fails only where the BP verdict fails (OSD leaves no
-    syndrome mismatch), with strictly fewer sector failures here."""
+    traces (noise and ST decodes do not depend on decoder2); per sample the BP+OSD
+    verdicts equal the oracle's (BP then the C OSD restatement on the final round), and
+    fail only where the BP verdicts fail, with strictly fewer sector failures here."""
     from qldpc_fault_tolerance_amd.decoders import BPOSD_Decoder_Class, ST_BP_Decoder_Class
     from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceOSD, DevicePhenl
 
@@ -210,6 +210,11 @@ def test_phenl_space_time_with_bposd_final_round(gpu):
 
     bp, bo = run(False), run(True)
     assert np.array_equal(bp.trace, bo.trace)
+    # per-sample parity with the oracle's BP + OSD restatement of the final round
+    ref = oracle.phenl_run(code, p / 2, p / 2, p / 2, p, 4242, 0, S, rounds, rep, "Total", p_data=p, p_synd=p,
+                           per_shot=True, osd_method="osd_e", osd_order=10)
+    assert np.array_equal(bo.trace, ref["trace"]) and np.array_equal(bo.fail, ref["fail"])
+    assert bo.failures == ref["failures"] and bo.sector_fail == ref["sector_fail"]
     assert not np.any((bo.fail != 0) & (bp.fail == 0))
     assert bo.failures <= bp.failures
     assert sum(bo.sector_fail) < sum(bp.sector_fail)
@@ -232,7 +237,8 @@ def test_phen_single_shot_bpdecoder_bposd_notebook_config(gpu, oracle):
     """The Threshold notebook's CodeFamilyPhenlThreshold pair: decoder1 = BPDecoder on [h | I],
     decoder2 = BPOSD_Decoder osd_e(10).  CodeSimulator_Phenon routes it onto the fused
     pipeline (qldpc_phenl_set_final_osd): the detector trace equals the oracle's (num_rep = 1) and
-    the BP-final-round run's, and per sample BP+OSD fails only where BP fails."""
+    the BP-final-round run's, the per-sample BP+OSD verdicts equal the oracle's BP + OSD
+    restatement, and BP+OSD fails only where BP fails."""
     from qldpc_fault_tolerance_amd.decoders import BP_Decoder_Class, BPOSD_Decoder_Class
     from qldpc_fault_tolerance_amd.simulators import CodeSimulator_Phenon
 
@@ -265,6 +271,9 @@ def test_phen_single_shot_bpdecoder_bposd_notebook_config(gpu, oracle):
                            per_shot=True)
     assert np.array_equal(bp.trace, ref["trace"]) and np.array_equal(bp.fail, ref["fail"])
     assert np.array_equal(bo.trace, bp.trace)
+    ref_osd = oracle.phenl_run(code, p / 2, p / 2, p / 2, p, 31, 0, S, rounds, 1, "Total", p_data=p, p_synd=p,
+                               per_shot=True, osd_method="osd_e", osd_order=10)
+    assert np.array_equal(bo.fail, ref_osd["fail"]) and bo.sector_fail == ref_osd["sector_fail"]
     assert not np.any((bo.fail != 0) & (bp.fail == 0))
     assert bo.failures <= bp.failures
     # the drop-in's fused path returns the same count as the device run of the same stream
@@ -286,3 +295,92 @@ def test_final_osd_graph_mismatch_is_rejected(gpu):
     with pytest.raises(_native.QldpcError, match="different graph"):
         ph.set_final_osd(oz, ox)  # swapped sectors
     ph.set_final_osd(ox, oz)
+
+
+def _oracle_sector_fails(oracle, code, err, p, mi, order, method="osd_e"):
+    """Per shot and sector: the reference's BPOSD verdict on the engine's sampled errors —
+    oracle BP (soft), then the C OSD restatement where BP did not converge, then the
+    _single_run failure check (src/Simulators.py:135-160)."""
+    from qldpc_fault_tolerance_amd.simulators import gf2_rows
+
+    out = np.zeros((err.shape[0], 2), dtype=bool)
+    for q, H, L, k in ((0, code.hz, code.lz, "hz"), (1, code.hx, code.lx, "hx")):
+        e = ((err >> q) & 1).astype(np.uint8)
+        synd = gf2_rows(code.csr(k), e)
+        oc, _, ov, op = oracle.bp_decode_batch_soft(H, p, mi, 0.625, synd, 64)
+        x = oc.copy()
+        nc = np.flatnonzero(~ov)
+        if nc.size:
+            x[nc] = oracle.osd_decode_batch(H, p * np.ones(code.N), synd[nc], op[nc], method, order)[1]
+        r = (e ^ x).astype(np.uint8)
+        out[:, q] = gf2_rows(code.csr(k), r).any(1) | gf2_rows(code.csr("lz" if q == 0 else "lx"), r).any(1)
+    return out
+
+
+def test_bposd_shot_loop_n1600_osd_e10_matches_oracle_per_shot(gpu, oracle):
+    """The fused BP+OSD shot loop (qldpc_mc_set_osd) at the headline code with the notebooks'
+    OSD-E(10): per shot and sector the verdict equals the oracle's BP + OSD restatement on the
+    same Philox errors (n1600 OSD-E(10) parity through the fused loop)."""
+    from qldpc_fault_tolerance_amd.decoders import BPOSD_Decoder_Class
+    from qldpc_fault_tolerance_amd.simulators import CodeSimulator_DataError
+
+    code = codes.get_code("hgp_34_n1600")
+    p, S = 0.05, 384
+    cls = BPOSD_Decoder_Class(10, "minimum_sum", 0.625, "osd_e", 10)
+    dx, dz = cls.GetDecoder({"h": code.hz, "p_data": p}), cls.GetDecoder({"h": code.hx, "p_data": p})
+    sim = CodeSimulator_DataError(code, dx, dz, [p / 2] * 3, "Total", seed=1600)
+    fails, shots, osd_n = sim.bposd_counts(S, keep_shots=True)
+    assert sim._bposd_dev, "the device-resident loop must serve the headline code"
+    assert shots == S and osd_n >= 40
+    err, sf = sim.last_shots
+    ref = _oracle_sector_fails(oracle, code, err, p, int(code.N / 10), 10)
+    assert np.array_equal(sf, ref)
+    assert fails == int((ref[:, 0] | ref[:, 1]).sum())
+
+
+@pytest.mark.parametrize("env", [{"QLDPC_MC_STAGED": "1"}, {"QLDPC_ENGINE": "2"}])
+def test_bposd_shot_loop_off_engine3_takes_host_path(gpu, oracle, monkeypatch, env):
+    """with the fused engine-3 MC unavailable (staged pipeline, a forced engine)
+    bposd_counts keeps the host-assisted loop instead of raising, with the oracle's verdicts."""
+    from qldpc_fault_tolerance_amd.decoders import BPOSD_Decoder_Class
+    from qldpc_fault_tolerance_amd.simulators import CodeSimulator_DataError
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    code = codes.get_code("hgp_34_n225")
+    p, order, S = 0.08, 4, 160
+    cls = BPOSD_Decoder_Class(10, "minimum_sum", 0.625, "osd_e", order)
+    dx, dz = cls.GetDecoder({"h": code.hz, "p_data": p}), cls.GetDecoder({"h": code.hx, "p_data": p})
+    sim = CodeSimulator_DataError(code, dx, dz, [p / 2] * 3, "Total", seed=77)
+    fails, shots, osd_n = sim.bposd_counts(S, batch=64, keep_shots=True)
+    assert not sim._bposd_dev  # routed to the host-assisted loop
+    assert shots == S and osd_n > 0
+    err, sf = sim.last_shots
+    ref = _oracle_sector_fails(oracle, code, err, p, int(code.N / 10), order)
+    assert np.array_equal(sf, ref)
+    assert fails == int((ref[:, 0] | ref[:, 1]).sum())
+
+
+def test_bposd_capture_budget_splits_launch_identically(gpu, monkeypatch):
+    """capture slots are bounded (QLDPC_OSD_CAPTURE_MB); a launch with more shots
+    than slots runs as pieces.  1 MB -> 1024 slots at n225: a 5000-shot launch in 5 pieces gives
+    the same per-shot errors, verdicts and counters as one piece."""
+    from qldpc_fault_tolerance_amd.decoders import BPOSD_Decoder_Class
+    from qldpc_fault_tolerance_amd.simulators import CodeSimulator_DataError
+
+    code = codes.get_code("hgp_34_n225")
+    p, S = 0.09, 5000
+    cls = BPOSD_Decoder_Class(10, "minimum_sum", 0.625, "osd_e", 6)
+
+    def run():
+        dx, dz = cls.GetDecoder({"h": code.hz, "p_data": p}), cls.GetDecoder({"h": code.hx, "p_data": p})
+        sim = CodeSimulator_DataError(code, dx, dz, [p / 2] * 3, "Total", seed=5)
+        r = sim.bposd_counts(S, batch=S, keep_shots=True)
+        return r, sim.last_shots, sim.last_result
+
+    a, (ea, fa), ra = run()
+    monkeypatch.setenv("QLDPC_OSD_CAPTURE_MB", "1")
+    b, (eb, fb), rb = run()
+    assert a == b and a[2] > 1024  # more candidates than one piece's slots
+    assert np.array_equal(ea, eb) and np.array_equal(fa, fb)
+    assert ra.sector_fail == rb.sector_fail and ra.sector_iters == rb.sector_iters

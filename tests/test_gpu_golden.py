@@ -83,24 +83,30 @@ def test_config_harness_replayed_on_gpu(gpu, name):
 
 def test_config5_space_time_replayed_on_gpu_fp64(gpu):
     """Config 5 in ldpc's float64 arithmetic: the 1764 x 5439 space-time decoder at the drop-in's default
-    precision (an image over the 160 KiB LDS: the HBM-resident message engine)."""
+    precision — engine 3's tail layout (rows of 9 = 4 fp64 chunks + a tail slot, a 162.7 KB image),
+    and the same histories forced onto the HBM-resident message engine (engine 6)."""
     from qldpc_fault_tolerance_amd.engine import DeviceBP, DevicePhenl
 
     g = np.load(CONFIGS, allow_pickle=False)
     code = codes.get_code("hgp_34_n1225_q3")
     m, n, p = code.hz.shape[0], code.N, 0.01
     mi = int(n / 10)
-    st = [DeviceBP(codes.space_time_csr(h, 3), np.hstack([p * np.ones(n), p * np.ones(m)] * 3), max_iter=mi,
-                   precision=64) for h in (code.hz, code.hx)]
-    d2 = [DeviceBP(code.csr(k), p * np.ones(n), max_iter=mi, precision=64) for k in ("hz", "hx")]
-    ph = DevicePhenl(code, st[0], st[1], d2[0], d2[1], num_rep=3)
     S = g["st1225_fail"].shape[0]
-    u = uniforms(int(g["st1225_seed0"][0]), S, ph.uniforms_per_sample(3))
-    res = ph.run(p / 2, p / 2, p / 2, p, 0, 0, S, 3, "Total", uniforms=u, per_shot=True)
-    tr = res.trace
-    body = tr[:, :2 * 2 * 3 * m].reshape(S, 2, 2, 3, m)
-    assert np.array_equal(body[:, :, 0].reshape(2 * S, 3, m), unpack(g["st1225_d1z_hist"], m))
-    assert np.array_equal(body[:, :, 1].reshape(2 * S, 3, m), unpack(g["st1225_d1x_hist"], m))
-    assert np.array_equal(tr[:, 12 * m:13 * m], unpack(g["st1225_d2z_synd"], m))
-    assert np.array_equal(tr[:, 13 * m:], unpack(g["st1225_d2x_synd"], m))
-    assert np.array_equal((res.fail != 0).astype(np.uint8), g["st1225_fail"])
+    for hbm in (False, True):
+        st = [DeviceBP(codes.space_time_csr(h, 3), np.hstack([p * np.ones(n), p * np.ones(m)] * 3), max_iter=mi,
+                       precision=64, hbm=hbm) for h in (code.hz, code.hx)]
+        geo = st[0].geometry()
+        assert geo["engine"] == (6 if hbm else 3), geo
+        if not hbm:
+            assert geo["lds_bytes"] > 64 * 1024 and geo["threads"] == 1024, geo  # the tail-layout family
+        d2 = [DeviceBP(code.csr(k), p * np.ones(n), max_iter=mi, precision=64) for k in ("hz", "hx")]
+        ph = DevicePhenl(code, st[0], st[1], d2[0], d2[1], num_rep=3)
+        u = uniforms(int(g["st1225_seed0"][0]), S, ph.uniforms_per_sample(3))
+        res = ph.run(p / 2, p / 2, p / 2, p, 0, 0, S, 3, "Total", uniforms=u, per_shot=True)
+        tr = res.trace
+        body = tr[:, :2 * 2 * 3 * m].reshape(S, 2, 2, 3, m)
+        assert np.array_equal(body[:, :, 0].reshape(2 * S, 3, m), unpack(g["st1225_d1z_hist"], m)), hbm
+        assert np.array_equal(body[:, :, 1].reshape(2 * S, 3, m), unpack(g["st1225_d1x_hist"], m)), hbm
+        assert np.array_equal(tr[:, 12 * m:13 * m], unpack(g["st1225_d2z_synd"], m)), hbm
+        assert np.array_equal(tr[:, 13 * m:], unpack(g["st1225_d2x_synd"], m)), hbm
+        assert np.array_equal((res.fail != 0).astype(np.uint8), g["st1225_fail"]), hbm

@@ -98,3 +98,39 @@ def test_osd_order_clipped_and_errors(n225):
     # empty batch
     o0, ow = osd.decode_batch(np.zeros((0, H.shape[0]), np.uint8), np.zeros((0, H.shape[1])))
     assert o0.shape == (0, H.shape[1])
+
+
+@pytest.mark.parametrize("method,order", [("osd_e", 7), ("osd_cs", 8), ("osd_0", 0), ("osd_e", 4)])
+def test_c_osd_restatement_matches_python_restatement(oracle, n225, method, order):
+    """oracle_osd_decode_batch (C, bit-vector rows) == osd_decode (literal Python) on n225
+    BP posteriors, tied integer posteriors and non-uniform priors: the C restatement is then
+    trusted as the checker at n1600 OSD-E(10), where the Python loops are too slow."""
+    H = n225
+    p = 0.09
+    synd, _ = _syndromes(H, p, 6, seed=23 + order)
+    probs = np.full(H.shape[1], p)
+    _, _, conv, post = oracle.bp_decode_batch_soft(H, probs, 22, 0.625, synd)
+    rng = np.random.default_rng(order)
+    cases = [(synd, post, probs),
+             (synd[:4], rng.integers(-2, 3, size=(4, H.shape[1])).astype(np.float64), probs),
+             (synd[:4], post[:4], rng.uniform(0.01, 0.2, size=H.shape[1]))]
+    for s, ps, pr in cases:
+        c0, cw = oracle.osd_decode_batch(H, pr, s, ps, method, order)
+        for b in range(s.shape[0]):
+            r0, rw = oracle.osd_decode(H, pr, s[b], ps[b], method, order)
+            assert np.array_equal(c0[b], r0) and np.array_equal(cw[b], rw), b
+
+
+def test_native_osd_matches_c_restatement_n1600_osd_e10(oracle):
+    """The native host OSD stage == the C restatement at hgp_34_n1600, OSD-E(10) (the
+    notebooks' decoder2 on the headline code), on the oracle's BP posteriors."""
+    H = codes.get_code("hgp_34_n1600").hz.astype(np.uint8)
+    p = 0.06
+    synd, _ = _syndromes(H, p, 48, seed=1600)
+    probs = np.full(H.shape[1], p)
+    corr, _, conv, post = oracle.bp_decode_batch_soft(H, probs, 160, 0.625, synd)
+    nc = np.flatnonzero(~conv)
+    assert nc.size >= 8
+    o0, ow = HostOSD(H, probs, "osd_e", 10).decode_batch(synd, post, conv, corr, threads=4)
+    c0, cw = oracle.osd_decode_batch(H, probs, synd[nc], post[nc], "osd_e", 10)
+    assert np.array_equal(o0[nc], c0) and np.array_equal(ow[nc], cw)

@@ -61,3 +61,31 @@ def test_sustainable_threshold(g, monkeypatch, cls, key):
     p_sus = cls([], None, None).EvalSustainableThreshold("phenl", "Total", "extrapolation", 0.05, 12000, cycles)
     np.testing.assert_allclose(p_sus, g[f"{key}_sus"][0], rtol=1e-9)
     assert calls == g[f"{key}_sus_calls"].tolist()
+
+
+def test_notebook_threshold_est_restatement_matches_notebook():
+    """tests/notebook_pin.threshold_est == the Threshold notebook's own ThresholdEst (cells 1-2,
+    executed from the notebook source by tests/golden/make_golden.py notebook) on 18 WER arrays."""
+    import os
+
+    import notebook_pin as nbp
+
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "notebook_fits.npz"),
+                allow_pickle=False)
+    for k in range(int(g["ncases"][0])):
+        A, pc = g[f"case{k}_A_pc"]
+        got = nbp.threshold_est(g[f"case{k}_p"], g[f"case{k}_wer"])
+        assert np.isclose(got[0], A, rtol=1e-9, atol=0) and np.isclose(got[1], pc, rtol=1e-9, atol=0), (k, got, A, pc)
+
+
+def test_notebook_pin_wer_transforms():
+    """The two WER transforms of CodeSimulator_Phenon.WordErrorRate (src/Simulators.py:341-351,
+    commented; :353-360, current) agree with each other for small rates, and the current one
+    equals the drop-in's word_error_rate_phenl at odd round counts."""
+    import notebook_pin as nbp
+    from qldpc_fault_tolerance_amd.simulators import word_error_rate_phenl
+
+    for c, S, K, R in ((3, 1000, 80, 5), (40, 400, 136, 9), (0, 500, 2, 7), (300, 600, 2, 3)):
+        assert np.isclose(nbp.wer_current(c, S, K, R), word_error_rate_phenl(c, S, K, R), rtol=1e-12, atol=0)
+    a, b = nbp.wer_commented(1, 10000, 100, 6), nbp.wer_current(1, 10000, 100, 6)
+    assert np.isclose(a, b, rtol=1e-3)
