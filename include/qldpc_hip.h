@@ -276,6 +276,60 @@ int qldpc_mc_set_osd(qldpc_mc *mc, qldpc_osd_gpu *osd_x, qldpc_osd_gpu *osd_z);
  * disables it).  0 / 0 for the other engines. */
 int qldpc_bp_bank_stats(const qldpc_bp *bp, int32_t *before, int32_t *after);
 
+/*
+ * Multi-GPU.  Shots shard by global index with no data-path
+ * exchange; the one collective is the sum of the int64 qldpc_counters vector,
+ * which replaces the reference's fork-pool reduction (`parmap` + `np.sum`,
+ * src/Simulators.py:37-61 and :170-188).  RCCL (over xGMI) is loaded at first use
+ * (dlopen librccl.so.1); without it these return QLDPC_ENOTSUP.
+ *   qldpc_comm_unique_id / qldpc_comm_init_rank : one process per GPU (rank 0
+ *       makes the id, the host side ships its 128 bytes to every rank);
+ *   qldpc_comm_init_all : one process driving ndev GPUs (devices NULL = 0..ndev-1),
+ *       out = array of ndev handles;
+ *   qldpc_comm_allreduce_counters : in-place sum of a device qldpc_counters on
+ *       `stream` (async);
+ *   qldpc_comm_allreduce_counters_group : the same for the handles of one
+ *       process (qldpc_comm_init_all), one RCCL group call.
+ */
+#define QLDPC_COMM_ID_BYTES 128
+typedef struct qldpc_comm qldpc_comm;
+int qldpc_comm_unique_id(uint8_t *id_out);
+int qldpc_comm_init_rank(int device, int32_t nranks, int32_t rank, const uint8_t *id, qldpc_comm **out);
+int qldpc_comm_init_all(int32_t ndev, const int32_t *devices, qldpc_comm **out);
+int qldpc_comm_rank(const qldpc_comm *comm, int32_t *rank, int32_t *nranks, int32_t *device);
+int qldpc_comm_allreduce_counters(qldpc_comm *comm, void *d_counters, void *stream);
+int qldpc_comm_allreduce_counters_group(qldpc_comm **comms, void **d_counters, void **streams, int32_t n);
+int qldpc_comm_destroy(qldpc_comm *comm);
+
+/*
+ * `WordErrorRate(num_run)` over several GPUs from ONE host thread
+ * (CodeSimulator_DataError.WordErrorRate, src/Simulators.py:170-188, whose
+ * `parmap` fans shots out over CPU cores): MC handle d (one per device, each on
+ * its own device's decoders) runs a contiguous block of the global shots (block
+ * sizes S/ndev or S/ndev + 1, the first S%ndev devices one longer: the split of
+ * parallel.shard_range), the counters are summed
+ * with one grouped all-reduce (comms from qldpc_comm_init_all, in the same
+ * device order) or, with comms NULL, on the host; the sum is added to *out.
+ * Synchronous.
+ * Shots keyed by global index: the totals do not depend on ndev.
+ */
+int qldpc_mc_run_sharded(qldpc_mc **mcs, qldpc_comm **comms, int32_t ndev, double px, double py, double pz,
+                         uint64_t seed, uint64_t shot_begin, int64_t shot_count, int32_t logical_mode,
+                         qldpc_counters *out);
+
+/*
+ * The sampling step alone (CodeSimulator_DataError._generate_error,
+ * src/Simulators.py:89-115): d_err uint8 [S][n], bit0 = x, bit1 = z, from the
+ * Philox stream of qldpc_mc_launch (shot shot_begin + s, qubit j) or from
+ * d_uniforms [S][n] (CPython's random() values) with the reference's 3-way
+ * split.  Bit-identical to the d_err output of qldpc_mc_launch.  Async.
+ */
+int qldpc_sample_errors(double px, double py, double pz, uint64_t seed, uint64_t shot_begin, int64_t shot_count,
+                        int32_t n, const double *d_uniforms, uint8_t *d_err, void *stream);
+
+/* hipStreamSynchronize(stream) for hosts without a HIP binding (NULL = legacy default stream). */
+int qldpc_stream_sync(void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,8 +23,12 @@ EXPORTED = [
     "qldpc_phenl_trace_len", "qldpc_phenl_launch", "qldpc_bp_degree3_slots", "qldpc_bp_create_soft",
     "qldpc_bp_decode_batch_soft", "qldpc_osd_create", "qldpc_osd_destroy", "qldpc_osd_rank",
     "qldpc_osd_decode_batch", "qldpc_osd_gpu_create", "qldpc_osd_gpu_destroy", "qldpc_osd_gpu_decode", "qldpc_phenl_set_final_osd",
-    "qldpc_bp_bank_stats", "qldpc_bp_create_hbm", "qldpc_mc_set_osd",
+    "qldpc_bp_bank_stats", "qldpc_bp_create_hbm", "qldpc_mc_set_osd", "qldpc_comm_unique_id",
+    "qldpc_comm_init_rank", "qldpc_comm_init_all", "qldpc_comm_rank", "qldpc_comm_allreduce_counters",
+    "qldpc_comm_allreduce_counters_group", "qldpc_comm_destroy", "qldpc_mc_run_sharded", "qldpc_sample_errors",
+    "qldpc_stream_sync",
 ]
+COMM_ID_BYTES = 128
 
 
 class NativeUnavailable(RuntimeError):
@@ -132,6 +136,27 @@ def _declare(L):
     L.qldpc_phenl_launch.restype = ctypes.c_int
     L.qldpc_phenl_launch.argtypes = [_vp, _dbl, _dbl, _dbl, _dbl, _u64, _u64, _i64, _i32, _i32, _vp, _vp, _vp, _vp,
                                      _vp]
+    L.qldpc_comm_unique_id.restype = ctypes.c_int
+    L.qldpc_comm_unique_id.argtypes = [_vp]
+    L.qldpc_comm_init_rank.restype = ctypes.c_int
+    L.qldpc_comm_init_rank.argtypes = [ctypes.c_int, _i32, _i32, _vp, _pp]
+    L.qldpc_comm_init_all.restype = ctypes.c_int
+    L.qldpc_comm_init_all.argtypes = [_i32, _vp, _pp]
+    L.qldpc_comm_rank.restype = ctypes.c_int
+    L.qldpc_comm_rank.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 3
+    L.qldpc_comm_allreduce_counters.restype = ctypes.c_int
+    L.qldpc_comm_allreduce_counters.argtypes = [_vp, _vp, _vp]
+    L.qldpc_comm_allreduce_counters_group.restype = ctypes.c_int
+    L.qldpc_comm_allreduce_counters_group.argtypes = [_pp, _pp, _pp, _i32]
+    L.qldpc_comm_destroy.restype = ctypes.c_int
+    L.qldpc_comm_destroy.argtypes = [_vp]
+    L.qldpc_mc_run_sharded.restype = ctypes.c_int
+    L.qldpc_mc_run_sharded.argtypes = [_pp, _pp, _i32, _dbl, _dbl, _dbl, _u64, _u64, _i64, _i32,
+                                       ctypes.POINTER(Counters)]
+    L.qldpc_sample_errors.restype = ctypes.c_int
+    L.qldpc_sample_errors.argtypes = [_dbl, _dbl, _dbl, _u64, _u64, _i64, _i32, _vp, _vp, _vp]
+    L.qldpc_stream_sync.restype = ctypes.c_int
+    L.qldpc_stream_sync.argtypes = [_vp]
 
 
 def lib():

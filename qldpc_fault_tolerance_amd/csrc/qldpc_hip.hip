@@ -675,7 +675,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
   auto* bp = new qldpc_bp();
   bp->g = g;
   bp->engine = ((want_engine >= 1 && want_engine <= 4) || want_engine == 6) ? want_engine : 3;
-  // column degree > 8: beyond the LDS engines' edge slots -> engine 6 (degree <= 16); soft BP stays engine 1
+  // column degree > 8: beyond the LDS engines' edge slots -> engine 6 (row and column degree <= 12); soft BP stays engine 1
   if ((g->max_col > 8 || min_col_slots > 8) && bp->engine != 6) {
     if (bp->engine == 1) {
       delete bp;

@@ -436,6 +436,60 @@ class DeviceMC:
             self.handle = None
 
 
+def sample_errors(n, px, py, pz, seed, shot_begin, shot_count, uniforms=None, device: int | None = None,
+                  stream=None):
+    """``qldpc_sample_errors``: the sampling step of the fused kernels alone
+    (``CodeSimulator_DataError._generate_error``, src/Simulators.py:89-115) as a uint8
+    ``[S, n]`` device tensor (bit0 = x, bit1 = z), from the Philox stream keyed by the
+    global shot index or from external uniforms ``[S, n]`` (CPython ``random()`` values)."""
+    torch = _torch()
+    if device is None:
+        from .parallel import local_device_index
+
+        device = local_device_index()
+    dev = torch.device("cuda", device)
+    S = int(shot_count)
+    out = torch.empty((S, int(n)), dtype=torch.uint8, device=dev)
+    u = None
+    if uniforms is not None:
+        u = uniforms if isinstance(uniforms, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(uniforms, dtype=np.float64))
+        u = u.to(dev, dtype=torch.float64).contiguous()
+        if tuple(u.shape) != (S, int(n)):
+            raise ValueError(f"uniforms must be [{S}, {n}]")
+    s = stream if stream is not None else _stream_handle(torch, dev)
+    with torch.cuda.device(dev):
+        _native.check(_native.lib().qldpc_sample_errors(
+            float(px), float(py), float(pz), int(seed) & (2**64 - 1), int(shot_begin), S, int(n),
+            ctypes.c_void_p(u.data_ptr()) if u is not None else None, ctypes.c_void_p(out.data_ptr()), s),
+            "qldpc_sample_errors")
+    return out
+
+
+def run_sharded(mcs, comms, px, py, pz, seed, shot_begin, shot_count, logical_mode="Total") -> MCResult:
+    """``qldpc_mc_run_sharded``: one host thread drives one :class:`DeviceMC` per GPU (each on its
+    own device's decoders) over contiguous blocks of the global shots, and sums the counters with
+    one grouped RCCL all-reduce (``comms`` from :meth:`parallel.NativeComm.init_all`, same device
+    order; None for one device).  The totals equal one device running all the shots."""
+    mcs = list(mcs)
+    nd = len(mcs)
+    arr = (ctypes.c_void_p * nd)(*[m.handle.value for m in mcs])
+    carr = None
+    if comms is not None:
+        comms = list(comms)
+        if len(comms) != nd:
+            raise ValueError("one communicator per MC handle")
+        carr = (ctypes.c_void_p * nd)(*[c.handle.value for c in comms])
+    out = _native.Counters()
+    mode = LOGICAL_MODES[logical_mode] if isinstance(logical_mode, str) else int(logical_mode)
+    _native.check(_native.lib().qldpc_mc_run_sharded(
+        ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)),
+        ctypes.cast(carr, ctypes.POINTER(ctypes.c_void_p)) if carr is not None else None, nd, float(px), float(py),
+        float(pz), int(seed) & (2**64 - 1), int(shot_begin), int(shot_count), mode, ctypes.byref(out)),
+        "qldpc_mc_run_sharded")
+    return MCResult.from_words(np.frombuffer(bytes(out), dtype=np.int64))
+
+
 class DevicePhenl:
     """Phenomenological space-time shot loop of ``CodeSimulator_Phenon_SpaceTime`` on one GPU (``qldpc_phenl_*``).
 

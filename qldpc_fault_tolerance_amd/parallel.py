@@ -12,6 +12,7 @@ all-reduce — RCCL over xGMI on MI355X nodes (backend ``nccl``), gloo on CPU.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 
@@ -59,3 +60,81 @@ def local_device_index() -> int:
 
         local %= max(1, torch.cuda.device_count())
     return local
+
+
+class NativeComm:
+    """An RCCL communicator owned by the engine's C ABI (``qldpc_comm_*``, include/qldpc_hip.h).
+
+    The same counter all-reduce as :func:`allreduce_counters` without torch.distributed: a host
+    that binds only ``libqldpc_hip.so`` (the ctypes stub of INTEGRATION.md §3) shards shots over
+    GPUs with it.  One process per GPU: rank 0 calls :func:`unique_id`, the host ships the 128
+    bytes to every rank, each rank calls ``NativeComm(device, nranks, rank, uid)``.  One process
+    driving several GPUs: :meth:`init_all`.
+    """
+
+    def __init__(self, device: int = 0, nranks: int = 1, rank: int = 0, uid: bytes | None = None, _handle=None):
+        from . import _native
+
+        self.device, self.nranks, self.rank = int(device), int(nranks), int(rank)
+        if _handle is not None:
+            self.handle = _handle
+            return
+        if uid is None or len(uid) != _native.COMM_ID_BYTES:
+            raise ValueError(f"uid must be the {_native.COMM_ID_BYTES} bytes of unique_id()")
+        buf = ctypes.create_string_buffer(bytes(uid), _native.COMM_ID_BYTES)
+        h = ctypes.c_void_p()
+        _native.check(_native.lib().qldpc_comm_init_rank(self.device, self.nranks, self.rank, buf, ctypes.byref(h)),
+                      "qldpc_comm_init_rank")
+        self.handle = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        from . import _native
+
+        buf = ctypes.create_string_buffer(_native.COMM_ID_BYTES)
+        _native.check(_native.lib().qldpc_comm_unique_id(buf), "qldpc_comm_unique_id")
+        return buf.raw
+
+    @staticmethod
+    def init_all(devices) -> list:
+        """One communicator per listed device, all owned by this process (``ncclCommInitAll``)."""
+        from . import _native
+
+        devices = [int(d) for d in devices]
+        nd = len(devices)
+        darr = (ctypes.c_int32 * nd)(*devices)
+        out = (ctypes.c_void_p * nd)()
+        _native.check(_native.lib().qldpc_comm_init_all(nd, darr, ctypes.cast(out, ctypes.POINTER(ctypes.c_void_p))),
+                      "qldpc_comm_init_all")
+        return [NativeComm(d, nd, r, _handle=ctypes.c_void_p(out[r])) for r, d in enumerate(devices)]
+
+    def info(self):
+        from . import _native
+
+        v = [ctypes.c_int32() for _ in range(3)]
+        _native.check(_native.lib().qldpc_comm_rank(self.handle, *[ctypes.byref(x) for x in v]), "qldpc_comm_rank")
+        return {"rank": v[0].value, "nranks": v[1].value, "device": v[2].value}
+
+    def allreduce_counters(self, counters, stream=None):
+        """In-place sum of a device ``qldpc_counters`` buffer (an int64 CUDA tensor) on ``stream``
+        (default: torch's current stream of the counters' device)."""
+        from . import _native
+
+        if stream is None:
+            import torch
+
+            stream = ctypes.c_void_p(torch.cuda.current_stream(counters.device).cuda_stream)
+        _native.check(_native.lib().qldpc_comm_allreduce_counters(self.handle, ctypes.c_void_p(counters.data_ptr()),
+                                                                  stream), "qldpc_comm_allreduce_counters")
+        return counters
+
+    def close(self):
+        from . import _native
+
+        h = getattr(self, "handle", None)
+        if h and _native._lib is not None:
+            _native.lib().qldpc_comm_destroy(h)
+        self.handle = None
+
+    def __del__(self):
+        self.close()
