@@ -239,6 +239,13 @@ int qldpc_bp_geometry(const qldpc_bp *bp, int32_t *threads, int32_t *vars_per_th
  * QLDPC_ENGINE in the environment selects 1, 2 or 4 explicitly. */
 int qldpc_bp_engine(const qldpc_bp *bp, int32_t *engine);
 
+/* Compile-time family of the decoder's kernels (the ENG template argument of rmc_kernel /
+ * rdec_kernel as rocprofv3 prints it): engine 3 = 3, 13 (dword-scaled addresses), 103 (fp64
+ * <= 256 threads), 303 (fp64 257-512 threads), 1013 (tail layout, 1024 threads), 11103 (fp64
+ * m2-in-slot, rows of 3 chunks + a tail slot, 3 workgroups per CU); other engines their number.
+ * row_chunks = 16-byte chunks per check row (engines 2-4). */
+int qldpc_bp_kernel_id(const qldpc_bp *bp, int32_t *kernel_id, int32_t *row_chunks);
+
 /* Engine 3: leading variable slots per thread that hold only variables of
  * column degree <= 3 (variables are host-sorted by degree; those slots skip the
  * 4th edge slot at compile time).  0 for the other engines and for the fp64

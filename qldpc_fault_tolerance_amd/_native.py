@@ -26,7 +26,7 @@ EXPORTED = [
     "qldpc_bp_bank_stats", "qldpc_bp_create_hbm", "qldpc_mc_set_osd", "qldpc_comm_unique_id",
     "qldpc_comm_init_rank", "qldpc_comm_init_all", "qldpc_comm_rank", "qldpc_comm_allreduce_counters",
     "qldpc_comm_allreduce_counters_group", "qldpc_comm_destroy", "qldpc_mc_run_sharded", "qldpc_sample_errors",
-    "qldpc_stream_sync",
+    "qldpc_stream_sync", "qldpc_bp_kernel_id",
 ]
 COMM_ID_BYTES = 128
 
@@ -155,6 +155,8 @@ def _declare(L):
                                        ctypes.POINTER(Counters)]
     L.qldpc_sample_errors.restype = ctypes.c_int
     L.qldpc_sample_errors.argtypes = [_dbl, _dbl, _dbl, _u64, _u64, _i64, _i32, _vp, _vp, _vp]
+    L.qldpc_bp_kernel_id.restype = ctypes.c_int
+    L.qldpc_bp_kernel_id.argtypes = [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]
     L.qldpc_stream_sync.restype = ctypes.c_int
     L.qldpc_stream_sync.argtypes = [_vp]
 

@@ -49,6 +49,14 @@
 #ifndef QLDPC_FLIPLATE
 #define QLDPC_FLIPLATE 0
 #endif
+// A/B build: the m2s check phase derives tid from an SGPR wave base + mbcnt
+#ifndef QLDPC_M2S_MBCNT
+#define QLDPC_M2S_MBCNT 0
+#endif
+// m2s family: one uniform prior in SGPRs instead of one per variable slot in VGPRs
+#ifndef QLDPC_M2S_UNIL
+#define QLDPC_M2S_UNIL 0
+#endif
 #include "bp_slot.h"
 
 namespace qldpc {
@@ -63,13 +71,21 @@ constexpr bool eng_kv64(int E) { return (E / 100) % 10 != 0; }
 // + 1000 = rows of NCH chunks plus one "tail" slot per row in a separate array (rows one
 // message wider than the chunks: the fp64 space-time graphs, 8 + 1 slots), engine 3 only
 constexpr int eng_tail(int E) { return (E / 1000) % 10; }
+// + 10000 = "m2 in slot" (fp64 <= 256-thread family with tail rows, engine id 11103): the check
+// state is ONE word per check, CS = {m1 | parity << 63}, and the check phase stores m2 | parity in
+// the V slot of the row's argmin edge.  A variable edge gathers CS and its own V slot: a slot that
+// no longer holds the edge's own previous v2c (kept in VGPRs) is the argmin, and its value is m2.
+// The image shrinks by 8 bytes per check; with rows of 7 as 3 chunks + a tail slot the n1600 fp64
+// image is 52.3 KB, so 3 workgroups share a CU (168-VGPR budget).
+constexpr bool eng_m2s(int E) { return (E / 10000) % 10 != 0; }
 // launch bounds: LB threads per workgroup at most; 256-thread fp64 kernels are
 // built for 2 workgroups per CU (2 waves per SIMD: up to 256 VGPRs, no spills)
 template <typename T, int ENG>
 constexpr int lb_waves(int LB) {
   // engine 4 fp64 images (no CS array) fit 3 workgroups per CU: <= 168 VGPRs
   // (the fp64 512-thread family: 2 workgroups of 8 waves per CU, 128 VGPRs)
-  return LB <= 256 ? (sizeof(T) == 8 ? (eng_base(ENG) == 4 ? 3 : 2) : 4) : (LB <= 512 && eng_kv64(ENG)) ? 4 : 1;
+  return LB <= 256 ? (sizeof(T) == 8 ? ((eng_base(ENG) == 4 || eng_m2s(ENG)) ? 3 : 2) : 4)
+                   : (LB <= 512 && eng_kv64(ENG)) ? 4 : 1;
 }
 __device__ inline unsigned long long qstamp() {
 #if QLDPC_STAMPS
@@ -92,9 +108,10 @@ struct RLayout {
 };
 
 // [CS][V][tail: one slot per row label (tail layouts only)][F][sink][lred]
-__host__ __device__ inline RLayout r_layout(int eng, int vslots, int mmax, int tsize, int tail = 0) {
+// (m2s: CS entries of one message word instead of two)
+__host__ __device__ inline RLayout r_layout(int eng, int vslots, int mmax, int tsize, int tail = 0, int m2s = 0) {
   RLayout L;
-  L.v = eng == 4 ? 0u : (uint32_t)a16((size_t)(mmax + 1) * 2 * tsize);
+  L.v = eng == 4 ? 0u : (uint32_t)a16((size_t)(mmax + 1) * (m2s ? 1 : 2) * tsize);
   L.t = L.v + (uint32_t)a16((size_t)vslots * tsize);
   L.f = L.t + (tail ? (uint32_t)a16((size_t)mmax * tsize) : 0u);
   L.sink = L.f + (uint32_t)a16((size_t)(mmax + 1) * 4);
@@ -236,9 +253,12 @@ struct RState {
   // unpacked and absolute (ea = CS address, ev = V slot address): no unpack / base add
   // per access, 2 VALU per edge and iteration fewer
   static constexpr bool kSplit = (ENG / 100) % 10 == 1 && sizeof(T) == 8;  // engine id 103 (not 303)
+  // m2s with QLDPC_M2S_UNIL: one prior for every variable (uniform channel_probs, host-checked),
+  // loaded by a scalar load: 2 SGPRs instead of 2 * VPL VGPRs
+  static constexpr bool kUniL = eng_m2s(ENG) && QLDPC_M2S_UNIL;
   uint32_t ea[VPL][DMAX];
   uint32_t ev[kSplit ? VPL : 1][kSplit ? DMAX : 1];
-  T L[VPL];
+  T L[kUniL ? 1 : VPL];
   U ov[kKeepV ? VPL : 1][kKeepV ? DMAX : 1];
 };
 // CS / V slot address of edge (k, t): absolute when split, else offsets from smem
@@ -270,15 +290,24 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
       if (eng_base(ENG) == 4) {
         R.ea[k][t] = e == kNoEdgeS ? (Ly.v | (Ly.sink << 16)) : (va | (va << 16));
       } else if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) {
-        R.ea[k][t] = sbase + echk(e) * (uint32_t)(2 * sizeof(T));
+        R.ea[k][t] = sbase + echk(e) * (uint32_t)((eng_m2s(ENG) ? 1 : 2) * sizeof(T));
         R.ev[k][t] = sbase + va;
       } else {
         R.ea[k][t] = ((echk(e) * (uint32_t)(2 * sizeof(T))) >> eng_sh(ENG)) | ((va >> eng_sh(ENG)) << 16);
       }
     }
-    const T l = (S.perm[k * TB + tid] >= 0) ? llr[k * TB + tid] : (T)1;
-    R.L[k] = eng_base(ENG) == 3 ? w_prior<T>(l) : l;  // engine 3: w domain
+    if constexpr (!RState<T, DMAX, VPL, ENG>::kUniL) {
+      const T l = (S.perm[k * TB + tid] >= 0) ? llr[k * TB + tid] : (T)1;
+      R.L[k] = eng_base(ENG) == 3 ? w_prior<T>(l) : l;  // engine 3: w domain
+    }
   }
+  // uniform prior (slot 0 of lane 0 holds a real variable); padding lanes take it too (their
+  // results are never read)
+  if constexpr (RState<T, DMAX, VPL, ENG>::kUniL) R.L[0] = w_prior<T>(llr[0]);
+}
+template <typename T, int DMAX, int VPL, int ENG>
+__device__ inline T r_prior(const RState<T, DMAX, VPL, ENG>& R, int k) {
+  return R.L[RState<T, DMAX, VPL, ENG>::kUniL ? 0 : k];
 }
 
 // F word of an edge.  Engine 3: from the CS address.  Engine 4: from the row
@@ -298,18 +327,21 @@ __device__ inline uint32_t f_addr(uint32_t ea, const FMap& M) {
 // Ly.f - (LDS base >> 2)
 template <typename T, int DMAX, int VPL, int ENG>
 __device__ inline uint32_t r_fa(const RState<T, DMAX, VPL, ENG>& R, int k, int t, uint32_t fbase) {
-  return (r_csa(R, k, t) >> (sizeof(T) == 4 ? 1 : 2)) + fbase;
+  // CS entry (i + 1) of 2 words (fp32: 8 B, fp64: 16 B) or, m2s, one fp64 word (8 B) -> F word i + 1
+  return (r_csa(R, k, t) >> ((sizeof(T) == 4 || eng_m2s(ENG)) ? 1 : 2)) + fbase;
 }
 
 // Opaque redefinition of the edge words (no instruction): without it the
 // compiler hoists their derived CS / V / F addresses out of the iteration and
 // shot loops, tripling the VGPRs per edge and spilling.
-template <typename T, int DMAX, int VPL, int ENG>
+// m2s kernels (D3K > 0 passed) keep no edge words for the unused 4th edge of degree-3 slots.
+template <typename T, int DMAX, int VPL, int ENG, int D3K = 0>
 __device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
 #pragma unroll
   for (int k = 0; k < VPL; ++k)
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
+      if (eng_m2s(ENG) && k < D3K && t >= 3) continue;
       asm volatile("" : "+v"(R.ea[k][t]));
       if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) asm volatile("" : "+v"(R.ev[k][t]));
     }
@@ -724,6 +756,203 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
   return mism;
 }
 
+// ------------------------------------------------------------------ m2-in-slot family
+// (engine id + 10000, fp64, split absolute addresses, own v2c in VGPRs).  Per edge the variable
+// phase gathers CS = m1 | parity (ds_read_b64) and the edge's own V slot (ds_read_b64); the
+// check phase left m2 | parity in the slot of the row's argmin edge, so "slot != own previous
+// v2c" marks the argmin and c2v = alpha * m2, else alpha * m1.  Same values as ldpc's "m2 if
+// |own| == m1 else m1": with a tie m1 == m2; a slot equal to the own word by chance has
+// m2 == m1 and the own sign == parity, i.e. the same c2v either way.
+template <typename T, int DMAX, int VPL, int ND, int ENG>
+__device__ inline void m_gather(const RState<T, DMAX, VPL, ENG>& R, int k, typename FT<T>::U (&an)[DMAX],
+                                typename FT<T>::U (&vn)[DMAX]) {
+  using U = typename FT<T>::U;
+#pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    an[t] = lds_ld<U, true>(nullptr, R.ea[k][t]);
+    vn[t] = lds_ld<U, true>(nullptr, R.ev[k][t]);
+  }
+}
+
+template <typename T, int DMAX, int VPL, int ND, int ENG>
+__device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, int k,
+                                 const typename FT<T>::U (&an)[DMAX],
+                                 const typename FT<T>::U (&vn)[DMAX], uint32_t fdelta, T alpha, bool xprev,
+                                 double* post, const int32_t* perm) {
+  using U = typename FT<T>::U;
+  static_assert(sizeof(T) == 8 && RState<T, DMAX, VPL, ENG>::kSplit && RState<T, DMAX, VPL, ENG>::kKeepV,
+                "m2s: fp64 split-address family only");
+  T c[ND];
+#pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    const U o = R.ov[k][t];
+    // argmin edge <=> its slot no longer holds our own previous v2c: m2 | parity, else m1 | parity
+    const U sel = vn[t] != o ? vn[t] : an[t];
+    // sign(sel) = parity; sel * alpha is exactly +-(|sel| * alpha) (IEEE rounding is sign-symmetric),
+    // then the own sign: c2v sign = parity ^ own sign (one v_bitop3, truth table S1 ^ (S0 & S2))
+    const U pb = FT<T>::bits(FT<T>::val(sel) * alpha);
+    uint32_t hi;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c"
+        : "=v"(hi)
+        : "v"((uint32_t)(o >> 32)), "v"((uint32_t)(pb >> 32)), "v"(0x80000000u));
+    c[t] = FT<T>::val(((U)hi << 32) | (uint32_t)pb);
+  }
+  // ldpc column pass (as r_var_one)
+  T f[ND];
+  T acc = r_prior(R, k);
+#pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    f[t] = acc;
+    acc = acc + c[t];
+  }
+  const bool x = acc >= (T)0;  // w domain: v <= 0
+  if (post) {
+    const int j = *perm;
+    if (j >= 0) post[j] = -(double)acc;
+  }
+  T b = c[ND - 1];
+  U nv[ND];
+  nv[ND - 1] = FT<T>::bits(f[ND - 1]);
+#pragma unroll
+  for (int t = ND - 2; t >= 0; --t) {
+    nv[t] = FT<T>::bits(f[t] + b);
+    if (t > 0) b = b + c[t];
+  }
+#pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    lds_st<U, true>(nullptr, R.ev[k][t], nv[t]);
+    R.ov[k][t] = nv[t];
+  }
+  if (x != xprev) {
+#pragma unroll
+    for (int t = 0; t < ND; ++t) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), 1u);
+  }
+  return x;
+}
+
+template <typename T, int DMAX, int VPL, int D3K, int ENG>
+__device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, uint32_t fdelta, T alpha, uint32_t xprev,
+                                 bool last_live, double* post = nullptr, const int32_t* perm = nullptr, int TB = 0) {
+  using U = typename FT<T>::U;
+  constexpr int N3 = DMAX > 3 ? 3 : DMAX;
+  // gathers one variable ahead: two ahead needs 32 more VGPRs than the 168 of 3 workgroups per
+  // CU and spills (n1600: 849k vs 1.13M shots/s, profiles/r03/m2s_ab/)
+  constexpr int PF0 = QLDPC_PF >= 1 ? QLDPC_PF : 1;
+  constexpr int PF = PF0 < VPL ? PF0 : VPL;
+  r_launder<T, DMAX, VPL, ENG, D3K>(R);
+  uint32_t xbits = 0;
+  U ab[PF][DMAX], vb[PF][DMAX];
+  auto gk = [&](int k, U (&an)[DMAX], U (&vn)[DMAX]) {
+    if (k < D3K)
+      m_gather<T, DMAX, VPL, N3, ENG>(R, k, an, vn);
+    else
+      m_gather<T, DMAX, VPL, DMAX, ENG>(R, k, an, vn);
+  };
+#pragma unroll
+  for (int k = 0; k < PF; ++k) gk(k, ab[k], vb[k]);
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    U an[DMAX], vn[DMAX];
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) {
+      an[t] = ab[k % PF][t];
+      vn[t] = vb[k % PF][t];
+    }
+    if (k + PF < VPL) gk(k + PF, ab[k % PF], vb[k % PF]);
+    if (k == VPL - 1 && !last_live) break;
+    const bool xp = ((xprev >> k) & 1u) != 0;
+    const int32_t* pk = perm ? perm + k * TB : nullptr;
+    const bool x = k < D3K ? m_var_one<T, DMAX, VPL, N3, ENG>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk)
+                           : m_var_one<T, DMAX, VPL, DMAX, ENG>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk);
+    xbits |= (x ? 1u : 0u) << k;
+  }
+  return xbits;
+}
+
+// m2s check phase (rows of NCH chunks + a tail slot when TAIL; fp64): min / second min / parity
+// as r_check_c plus the row's argmin slot (first strict minimum); CS[i+1] = m1 | parity and
+// V[argmin] = m2 | parity.  Any edge holding m1 would do as the argmin: with a tie m2 == m1.
+template <typename T, bool FIRST, int NCH, int TAIL>
+__device__ inline int m_check(unsigned char* smem, const RLayout& Ly, int m, int wbase, int wtid, int TB, uint32_t& sbits) {
+  using U = typename FT<T>::U;
+  using VT = typename V16<T>::type;
+  constexpr int NV = V16<T>::N;
+  static_assert(sizeof(T) == 8, "m2s: fp64 only");
+  int mism = 0;
+  int q = 0;
+#if QLDPC_M2S_MBCNT
+  // tid from the wave's base (an SGPR) and the lane's mbcnt: no VGPR holds tid across the
+  // variable phase (A/B build: the register allocator then spills elsewhere)
+  const int tid = wbase + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+#else
+  // opaque tid: the row / F / tail offsets are recomputed per pass instead of being hoisted out
+  // of the iteration loop (where they outlive the variable phase and spill)
+  int tid = wtid;
+  asm volatile("" : "+v"(tid));
+  (void)wbase;
+#endif
+  const uint32_t rstride = (uint32_t)NCH * 16u;
+  // chunk rotation for power-of-two rows (as r_check_c); rows of 3 chunks are conflict-free
+  constexpr int kRows256 = 256 / (16 * NCH) > 0 ? 256 / (16 * NCH) : 1;
+  constexpr bool kRot = QLDPC_ROT && (NCH == 4 || NCH == 8);
+  const uint32_t rot = kRot ? ((uint32_t)(tid / kRows256) & (uint32_t)(NCH - 1)) : 0u;
+  uint32_t coff[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) coff[c] = kRot ? (((uint32_t)c + rot) & (uint32_t)(NCH - 1)) * 16u : (uint32_t)c * 16u;
+  for (int i = tid; i < m; i += TB, ++q) {
+    const uint32_t roff = Ly.v + 16u + (uint32_t)i * rstride;
+    VT cur[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) cur[c] = *reinterpret_cast<const VT*>(smem + roff + coff[c]);
+    const uint32_t toff = Ly.t + (uint32_t)i * (uint32_t)sizeof(T);
+    T tcur = (T)0;
+    if (TAIL) tcur = lds_at<T>(smem, toff);
+    const uint32_t fcur = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
+    uint32_t s;
+    if (FIRST) {
+      s = ((fcur >> 1) ^ (fcur >> 2)) & 1u;
+      sbits |= s << q;
+      lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1)) = (fcur & 4u) | ((fcur >> 2) & 1u);
+    } else {
+      s = (sbits >> q) & 1u;
+      mism |= (int)((fcur ^ s) & 1u);
+    }
+    double f1 = FT<T>::val(FT<T>::kSent), f2 = f1;
+    uint32_t px = s ? 0x80000000u : 0u;
+    uint32_t amin = roff + coff[0];  // argmin slot (byte offset); any slot when no edge is below the sentinel
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const double x = V16<T>::get(cur[c], k);
+        amin = __builtin_fabs(x) < f1 ? roff + coff[c] + 8u * (uint32_t)k : amin;
+        double t;
+        asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x));
+        asm("v_min_f64 %0, %1, %2" : "=v"(f2) : "v"(f2), "v"(t));
+        asm("v_min_f64 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
+      }
+      uint32_t p;
+      asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96"
+          : "=v"(p)
+          : "v"(px), "v"((uint32_t)(FT<T>::bits(cur[c].x) >> 32)), "v"((uint32_t)(FT<T>::bits(cur[c].y) >> 32)));
+      px = p;
+    }
+    if (TAIL) {
+      const double x = (double)tcur;
+      amin = __builtin_fabs(x) < f1 ? toff : amin;
+      double t;
+      asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x));
+      asm("v_min_f64 %0, %1, %2" : "=v"(f2) : "v"(f2), "v"(t));
+      asm("v_min_f64 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
+      px ^= (uint32_t)(FT<T>::bits(tcur) >> 32);
+    }
+    const U par = (U)(px & 0x80000000u) << 32;
+    lds_at<U>(smem, (uint32_t)(i + 1) * (uint32_t)sizeof(T)) = FT<T>::bits(f1) | par;
+    lds_at<U>(smem, amin) = FT<T>::bits(f2) | par;
+  }
+  return mism;
+}
+
 // Engine-4 variable phase: c2v from the slots, ldpc's column pass, v2c back.
 // Variable VPL-1 is skipped by waves whose lanes are all padding.
 template <typename T, int DMAX, int VPL>
@@ -900,6 +1129,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
 #endif
   RState<T, DMAX, VPL, ENG> R;
   constexpr bool SP = RState<T, DMAX, VPL, ENG>::kSplit;
+  const int wbase = (int)__builtin_amdgcn_readfirstlane((uint32_t)tid) & ~63;  // (m2s check phase)
   const uint32_t sbase = lds_base(smem);
   r_load<T, DMAX, VPL, ENG>(S, R, Ly, tidp, TB, sbase);
   r_fill<T, ENG>(S, smem, Ly, vslots, mmax, tidp, TB);
@@ -907,7 +1137,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   M.fbase = eng_base(ENG) == 4 ? Ly.f + 4u : Ly.f;
   M.rstart = Ly.v + 16u;
   M.rsh = 4 + __builtin_ctz((unsigned)nch);
-  if (SP) M.fbase = Ly.f - (sbase >> 2);  // split: absolute CS addresses (16-byte aligned base)
+  if (SP) M.fbase = Ly.f - (sbase >> (eng_m2s(ENG) ? 1 : 2));  // split: absolute CS addresses (16-byte aligned base)
   const uint32_t fdelta = eng_base(ENG) == 4 ? Ly.f : M.fbase;
   // waves whose lanes all hold padding variables skip the last variable (engine 4)
   const bool last_live = uni((VPL - 1) * TB + (tid & ~63) < n ? 1 : 0) != 0;
@@ -926,16 +1156,17 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   for (int sh = 0; sh <= cn; ++sh) {
     const bool have = sh < cn;
     uint32_t eb = 0, sb = 0;
-    r_launder(R);
+    r_launder<T, DMAX, VPL, ENG, D3K>(R);
     int tidl = tid;  // opaque copy: keeps per-variable addresses from being hoisted (VGPRs)
     asm volatile("" : "+v"(tidl));
     // ---------------------------------------------------------- priors / sampling
     if (have) {
 #pragma unroll
       for (int k = 0; k < VPL; ++k) {
-        const U cl = FT<T>::bits(R.L[k]);  // w domain: the prior as is
+        const U cl = FT<T>::bits(r_prior(R, k));  // w domain: the prior as is
 #pragma unroll
         for (int t = 0; t < DMAX; ++t) {
+          if (eng_m2s(ENG) && k < D3K && t >= 3) continue;  // (m2s: no dummy 4th edge kept)
           lds_st<U, SP>(smem, r_va(R, k, t), cl);
           if (KV) R.ov[KV ? k : 0][KV ? t : 0] = cl;
         }
@@ -966,8 +1197,10 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
             if (A->err && q == A->sec_id0) A->err[sl * (long long)n + j] = (uint8_t)cls;
             if (e) {
 #pragma unroll
-              for (int t = 0; t < DMAX; ++t)
+              for (int t = 0; t < DMAX; ++t) {
+                if (eng_m2s(ENG) && k < D3K && t >= 3) continue;
                 atomicXor(&lds_at<uint32_t>(smem, eng_base(ENG) == 4 ? f_addr<T, ENG>(R.ea[k][t], M) : r_fa(R, k, t, M.fbase)), 2u);
+              }
             }
           }
         }
@@ -1019,6 +1252,8 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     // ---------------------------------------------------------- first check pass (CS / c2v from priors)
     if constexpr (eng_base(ENG) == 4)
       c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
+    else if constexpr (eng_m2s(ENG))
+      m_check<T, true, NCH, eng_tail(ENG)>(smem, Ly, m, wbase, tid, TB, sb);
     else if constexpr (NCH > 0)
       r_check_c<T, true, NCH, eng_tail(ENG), QLDPC_PFC>(smem, Ly, m, tid, TB, sb);
     else
@@ -1056,10 +1291,13 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         mism = c_check_any<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha);
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
-        // (the tail family runs one workgroup per CU: nothing to take priority over)
-        constexpr int kPV = eng_tail(ENG) ? 0 : QLDPC_PRIO_V;
+        // (the 1024-thread tail family runs one workgroup per CU: nothing to take priority over)
+        constexpr int kPV = (eng_tail(ENG) && !eng_m2s(ENG)) ? 0 : QLDPC_PRIO_V;
         if (kPV) __builtin_amdgcn_s_setprio(kPV);
-        xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
+        if constexpr (eng_m2s(ENG))
+          xb = m_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
+        else
+          xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
         if (kPV) __builtin_amdgcn_s_setprio(0);
         unsigned long long t1 = 0;
         if (QLDPC_STAMPS) {
@@ -1074,7 +1312,9 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         // check state for iteration it + 1 (float: pre-scaled by its alpha)
         const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
         if (QLDPC_PRIO_C) __builtin_amdgcn_s_setprio(QLDPC_PRIO_C);
-        if constexpr (NCH > 0)
+        if constexpr (eng_m2s(ENG))
+          mism = m_check<T, false, NCH, eng_tail(ENG)>(smem, Ly, m, wbase, tid, TB, sb);
+        else if constexpr (NCH > 0)
           mism = r_check_c<T, false, NCH, eng_tail(ENG), QLDPC_PFC>(smem, Ly, m, tid, TB, sb);
         else
           mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha_next);
@@ -1179,7 +1419,7 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rmc_kernel(SMcArgs
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = A.chunk;
   const int fw = (CH + 31) / 32;
-  const RLayout Ly = r_layout(eng_base(ENG), A.vslots, A.mmax, (int)sizeof(T), eng_tail(ENG));
+  const RLayout Ly = r_layout(eng_base(ENG), A.vslots, A.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG));
   uint32_t* fm0 = reinterpret_cast<uint32_t*>(smem + Ly.total);
   uint32_t* fm1 = fm0 + ((fw + 3) & ~3);
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(fm1 + ((fw + 3) & ~3));
@@ -1236,7 +1476,7 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rdec_kernel(SDecAr
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = D.chunk;
-  const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T), eng_tail(ENG));
+  const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG));
   const long long nchunks = (D.B + CH - 1) / CH;
   __shared__ long long s_next;
   long long ch = blockIdx.x;

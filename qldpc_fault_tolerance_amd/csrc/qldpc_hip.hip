@@ -99,7 +99,12 @@ bool use_f64x(int engine, int precision, int dmax, int tb, int vpl, int ea_shift
 
 // Slot-family kernels of an engine (2, 3 or 4).
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
-                      int nch = 0, int tail = 0) {
+                      int nch = 0, int tail = 0, int m2s = 0) {
+  // fp64 m2-in-slot family (rows of 3 chunks + a tail slot, <= 256 threads, 3 workgroups per CU)
+  if (m2s) {
+    const bool ok = engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && nch == 3 && tail && tb <= 256;
+    return ok ? get_rvariant_f64_m2s(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
+  }
   // fp64 tail layout (rows of 4 chunks + a tail slot, dword-scaled addresses, 1024 threads)
   if (tail) {
     const bool ok = engine == 3 && dmax == 4 && ea_shift == 2 && nch == (precision == 64 ? 4 : 2) && tb > 512;
@@ -214,8 +219,8 @@ int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL, int pre
 // Engines 3 and 4 address their image with 16-bit byte offsets.
 // Engines 3 and 4 address their image with 16-bit byte offsets; engine 3 with
 // dword-scaled offsets (kernel id 13, ea_shift 2) reaches 256 KiB.
-bool r_fits(int eng, int vslots, int mmax, int tsize, int ea_shift = 0, int tail = 0) {
-  const RLayout L = r_layout(eng, vslots, mmax, tsize, tail);
+bool r_fits(int eng, int vslots, int mmax, int tsize, int ea_shift = 0, int tail = 0, int m2s = 0) {
+  const RLayout L = r_layout(eng, vslots, mmax, tsize, tail, m2s);
   return L.lred <= (65536u << ea_shift) && r_lds_bytes((int)L.total, kChunkMax) <= (size_t)kLdsMax;
 }
 
@@ -457,12 +462,16 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
 // in-row placement can make the stores conflict free too.  Pure host work, done
 // once per decoder; the arithmetic is untouched (labels only move storage).
 static std::vector<int> label_checks(const qldpc_graph* g, const std::vector<int32_t>& slot_var, int TB, int VPL,
-                                     int DM, int tsize, int* cost_before = nullptr, int* cost_after = nullptr) {
+                                     int DM, int tsize, int* cost_before = nullptr, int* cost_after = nullptr,
+                                     int m2s = 0) {
   const int m = g->m;
   std::vector<int> lab(m);
   for (int i = 0; i < m; ++i) lab[i] = i;
   if (m < 2) return lab;
-  const int NC = tsize == 4 ? 32 : 16;
+  // CS entries of 8 bytes (fp32 pairs; fp64 m2s words): ds_read_b64 gathers, 2 groups of 32 lanes,
+  // bank pair = entry mod 32.  16-byte fp64 pairs: ds_read_b128, bank quad = entry mod 16.
+  const bool cs8 = tsize == 4 || m2s;
+  const int NC = cs8 ? 32 : 16;
   static const int kB128[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
                                    {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
                                    {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
@@ -495,12 +504,13 @@ static std::vector<int> label_checks(const qldpc_graph* g, const std::vector<int
   for (int k = 0; k < VPL; ++k)
     for (int d = 0; d < DM; ++d)
       for (int w = 0; w * 64 < TB; ++w) {
-        if (tsize == 4) {
+        if (cs8) {
           for (int h = 0; h < 2; ++h) add_group(k, d, w, lanes32[h], 32, false);
         } else {
           for (int h = 0; h < 4; ++h) add_group(k, d, w, kB128[h], 16, false);
-          for (int h = 0; h < 4; ++h) add_group(k, d, w, lanes16[h], 16, true);
         }
+        if (tsize == 8)
+          for (int h = 0; h < 4; ++h) add_group(k, d, w, lanes16[h], 16, true);
       }
   const int ng = (int)gstore.size();
   if (ng == 0) return lab;
@@ -770,14 +780,38 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         bp->ea_shift = 2;
       }
     }
+    // fp64 "m2 in slot" family (bp_reg.h eng_m2s, kern_r_f64_m2s.hip): one-word check state, m2 in
+    // the argmin edge's V slot, rows of up to 7 edges as 3 chunks + a tail slot, <= 256 threads.
+    // The headline hgp_34_n1600 image drops from 65.0 KB to 52.3 KB: 3 workgroups per CU instead
+    // of 2.  The kernel keeps no dummy edges for real variables, so every column degree must be
+    // 3 or 4 with the degree-3 variables filling whole variable slots (host degree sort).
+    if (bp->engine == 3 && precision == 64 && DM == 4 && !bp->tail && g->max_row >= 1 && g->max_row <= 7 &&
+        env_int("QLDPC_M2S", 1) != 0 && env_int("QLDPC_DEGSORT", 1) != 0) {
+      int tb = 0, vpl = 0, n3 = 0, nother = 0;
+      for (int j = 0; j < g->n; ++j) {
+        const int d = (int)g->col_rows[j].size();
+        n3 += d == 3;
+        nother += d != 3 && d != 4;
+      }
+      bool uni = true;  // QLDPC_M2S_UNIL kernels hold one prior for every variable
+      for (int j = 1; j < g->n && QLDPC_M2S_UNIL; ++j) uni = uni && channel_probs[j] == channel_probs[0];
+      if (!nother && uni && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb <= 256 && vpl >= 4 &&
+          vpl <= 8 && (n3 % tb == 0 || n3 == g->n) && r_fits(3, (1 + g->m * 3) * 2, g->m, 8, 0, 1, 1)) {
+        bp->tail = 1;
+        bp->m2s = 1;
+        bp->nch = 3;
+        bp->ea_shift = 0;
+      }
+    }
     const int vslots_e3 = (1 + g->m * bp->nch) * (16 / tsize);
     if (bp->engine >= 3 && ((DM != 4 && !(bp->engine == 3 && (DM == 5 || DM == 6))) ||
                             choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL, pref, vmax) ||
-                            !r_fits(bp->engine, vslots_e3, g->m, tsize, bp->ea_shift, bp->tail) ||
+                            !r_fits(bp->engine, vslots_e3, g->m, tsize, bp->ea_shift, bp->tail, bp->m2s) ||
                             (precision == 64 && DM == 5 &&
                              !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch)))) {
       bp->ea_shift = 0;
       bp->tail = 0;
+      bp->m2s = 0;
       bp->engine = 2;  // graph outside the register engines' envelope
       bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
       if (DM == 5 || DM == 6) bp->DMAX = DM = 8;  // engine 2 kernels come in 4 and 8 slots
@@ -785,7 +819,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     const int vslots2 = (1 + g->m * bp->nch) * (16 / tsize);
     if (bp->engine >= 3) {
       bp->NS = 1;
-      bp->lds_bytes = (int)r_lds_bytes((int)r_layout(bp->engine, vslots2, g->m, tsize, bp->tail).total, kChunkMax);
+      bp->lds_bytes = (int)r_lds_bytes((int)r_layout(bp->engine, vslots2, g->m, tsize, bp->tail, bp->m2s).total, kChunkMax);
     } else {
       rc = choose_sgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL);
       if (rc) return fail(rc);
@@ -831,7 +865,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         bp->d3k = k + 1;
       }
     const int vbase_dw = (bp->engine == 3 && env_int("QLDPC_BANKOPT", 1) != 0)
-                             ? (int)(r_layout(3, vslots2, g->m, tsize).v / 4)
+                             ? (int)(r_layout(3, vslots2, g->m, tsize, bp->tail, bp->m2s).v / 4)
                              : -1;
     // fp64 engine-3 kernels are built with D3K = 0 only, except the <= 256-thread family
     if (precision != 32 && !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch) &&
@@ -841,7 +875,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     // fp64 (measured +3 % with the bank-aware fp64 v2c placement); fp32 gathers of the
     // structured codes are already near conflict-free (QLDPC_LABEL=1 forces it on)
     if (bp->engine == 3 && env_int("QLDPC_LABEL", precision == 64 ? 1 : 0) != 0) {
-      lab = label_checks(g, bp->slot_var, bp->TB, bp->VPL, DM, tsize, &bp->gather_conf[0], &bp->gather_conf[1]);
+      lab = label_checks(g, bp->slot_var, bp->TB, bp->VPL, DM, tsize, &bp->gather_conf[0], &bp->gather_conf[1], bp->m2s);
       std::vector<int32_t> inv(g->m);
       for (int i = 0; i < g->m; ++i) inv[lab[i]] = i;
       if ((rc = bp->rperm.alloc((size_t)std::max(1, g->m) * 4))) return fail(rc);
@@ -849,7 +883,8 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         return fail(set_err(QLDPC_EHIP, "upload check labels"));
     }
     build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab, bp->tail);
-    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch, bp->tail).dec_k;
+    kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch, bp->tail,
+                        bp->m2s).dec_k;
     if (bp->engine >= 3) {
       // row degrees by check label: engine 4 keeps them in F, engine 3 their parity (bp_reg.h, w domain)
       std::vector<uint8_t> deg(std::max(1, g->m));
@@ -888,6 +923,11 @@ int qldpc_bp_destroy(qldpc_bp* bp) {
 
 int qldpc_bp_set_channel_probs(qldpc_bp* bp, const double* channel_probs) {
   if (!bp || !channel_probs) return set_err(QLDPC_EINVAL, "NULL argument");
+  if (bp->m2s && QLDPC_M2S_UNIL)
+    for (int j = 1; j < bp->g->n; ++j)
+      if (channel_probs[j] != channel_probs[0])
+        return set_err(QLDPC_ENOTSUP, "this decoder's kernels hold one uniform prior: create a new decoder for "
+                                      "non-uniform channel_probs");
   bp->probs.assign(channel_probs, channel_probs + bp->g->n);
   return upload_llr(bp);
 }
@@ -902,6 +942,26 @@ int qldpc_bp_bank_stats(const qldpc_bp* bp, int32_t* before, int32_t* after) {
   if (!bp) return set_err(QLDPC_EINVAL, "NULL decoder");
   if (before) *before = bp->gather_conf[0];
   if (after) *after = bp->gather_conf[1];
+  return 0;
+}
+
+int qldpc_bp_kernel_id(const qldpc_bp* bp, int32_t* kernel_id, int32_t* row_chunks) {
+  if (!bp) return set_err(QLDPC_EINVAL, "NULL decoder");
+  int id = bp->engine;
+  if (bp->engine == 3) {
+    if (bp->m2s)
+      id = 11103;
+    else if (bp->tail)
+      id = 1013;
+    else if (use_f64w(bp->engine, bp->precision, bp->DMAX, bp->TB, bp->VPL, bp->ea_shift, bp->nch))
+      id = 103;
+    else if (use_f64x(bp->engine, bp->precision, bp->DMAX, bp->TB, bp->VPL, bp->ea_shift))
+      id = 303;
+    else if (bp->ea_shift == 2)
+      id = 13;
+  }
+  if (kernel_id) *kernel_id = id;
+  if (row_chunks) *row_chunks = bp->nch;
   return 0;
 }
 
@@ -1020,7 +1080,7 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
     SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch,
-                              bp->tail);
+                              bp->tail, bp->m2s);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;
@@ -1049,8 +1109,8 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
                     qldpc_mc** out) {
   if (!out || (!dec_x && !dec_z)) return set_err(QLDPC_EINVAL, "need at least one sector decoder");
   qldpc_bp* d0 = dec_x ? dec_x : dec_z;
-  const bool staged = (dec_x && dec_x->engine >= 5) || (dec_z && dec_z->engine >= 5) || (dec_x && dec_x->tail) ||
-                      (dec_z && dec_z->tail) ||
+  const bool staged = (dec_x && dec_x->engine >= 5) || (dec_z && dec_z->engine >= 5) ||
+                      (dec_x && dec_x->tail && !dec_x->m2s) || (dec_z && dec_z->tail && !dec_z->m2s) ||
                       env_int("QLDPC_MC_STAGED", 0) == 1;
   if (staged) {  // staged pipeline around decode_batch (staged.hip): any decoder pair
     if (dec_x && dec_z && (dec_x->g->n != dec_z->g->n || dec_x->g->device != dec_z->g->device))
@@ -1080,6 +1140,8 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
         dec_x->precision != dec_z->precision || dec_x->engine != dec_z->engine)
       return set_err(QLDPC_EINVAL, "sector decoders need identical geometry/precision (same vars_per_thread)");
     if (dec_x->g->device != dec_z->g->device) return set_err(QLDPC_EINVAL, "sector decoders on different devices");
+    if (dec_x->m2s != dec_z->m2s || dec_x->tail != dec_z->tail)
+      return set_err(QLDPC_EINVAL, "sector decoders use different LDS layouts (QLDPC_M2S)");
   }
   QLDPC_HIP(hipSetDevice(d0->g->device));
   auto* mc = new qldpc_mc();
@@ -1110,6 +1172,8 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   mc->nch = d0->nch;
   if (dec_x && dec_z && dec_x->nch != dec_z->nch) mc->nch = 0;
   mc->mmax = std::max(dec_x ? dec_x->g->m : 0, dec_z ? dec_z->g->m : 0);
+  mc->tail = d0->tail;
+  mc->m2s = d0->m2s;
   const void* kern;
   if (mc->engine == 1) {
     mc->lds_bytes = (int)lds_for(mc->precision, mc->mmax);
@@ -1120,15 +1184,17 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
       if (d) mc->vslots = std::max(mc->vslots, (1 + d->g->m * d->nch) * (16 / tsize));
     mc->img_bytes = (int)slot_img_bytes(mc->vslots, mc->mmax, tsize);
     if (mc->engine >= 3) {
-      if (!r_fits(mc->engine, mc->vslots, mc->mmax, tsize, mc->ea_shift))
+      if (!r_fits(mc->engine, mc->vslots, mc->mmax, tsize, mc->ea_shift, mc->tail, mc->m2s))
         return fail(set_err(QLDPC_ENOTSUP, "sector images exceed the register engines' 64 KiB addressing (QLDPC_ENGINE=2)"));
       mc->NS = 1;
-      mc->lds_bytes = (int)r_lds_bytes((int)r_layout(mc->engine, mc->vslots, mc->mmax, tsize).total, kChunkMax);
+      mc->lds_bytes =
+          (int)r_lds_bytes((int)r_layout(mc->engine, mc->vslots, mc->mmax, tsize, mc->tail, mc->m2s).total, kChunkMax);
     } else {
       mc->NS = choose_ns(mc->img_bytes);
       mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
     }
-    kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch).mc_k;
+    kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch,
+                        mc->tail, mc->m2s).mc_k;
   }
   if (mc->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB"));
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
@@ -1316,7 +1382,8 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
       }
       if (!a.fail) a.fail = static_cast<uint8_t*>(mc->c_fail.p);  // per-shot verdicts the OSD stage revises
     }
-    SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch);
+    SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch,
+                              mc->tail, mc->m2s);
     QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, st, a));
     if (bposd) {
       unsigned int nc[4] = {0, 0, 0, 0};

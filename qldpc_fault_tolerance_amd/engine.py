@@ -135,6 +135,10 @@ class DeviceBP:
         _native.check(_native.lib().qldpc_bp_bank_stats(self.handle, ctypes.byref(b0), ctypes.byref(b1)),
                       "bp_bank_stats")
         g["gather_conflicts"] = (b0.value, b1.value)
+        kid, nch = ctypes.c_int32(), ctypes.c_int32()
+        _native.check(_native.lib().qldpc_bp_kernel_id(self.handle, ctypes.byref(kid), ctypes.byref(nch)),
+                      "bp_kernel_id")
+        g["kernel_id"], g["row_chunks"] = kid.value, nch.value
         return g
 
     def decode_batch_device(self, synd_dev, corr_dev, iters_dev=None, conv_dev=None, stream=None):

@@ -65,8 +65,13 @@ def main():
             pp = ep / 2
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            tp = t0
             for s0 in range(0, S, a.chunk):
                 mc.launch(pp, pp, pp, a.seed, s0, min(a.chunk, S - s0), "Total", cnt)
+                if time.perf_counter() - tp > 30:  # progress line (keeps a long point visibly alive)
+                    torch.cuda.synchronize()
+                    tp = time.perf_counter()
+                    print(f"  {name} p={ep:.4f}: {s0 + min(a.chunk, S - s0)} / {S} shots, {tp - t0:.0f} s", flush=True)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             r = MCResult.from_words(cnt.cpu().numpy())
