@@ -55,7 +55,7 @@
 #endif
 // m2s family: one uniform prior in SGPRs instead of one per variable slot in VGPRs
 #ifndef QLDPC_M2S_UNIL
-#define QLDPC_M2S_UNIL 0
+#define QLDPC_M2S_UNIL 1
 #endif
 #include "bp_slot.h"
 

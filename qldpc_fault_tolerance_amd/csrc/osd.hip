@@ -388,6 +388,7 @@ struct OsdGpuArgs {
   int m_lds;  // 1: the matrix lives in LDS, aliasing the sort tables (copied out first), else in the HBM slice
   int bits_off;  // LDS byte offset of the used / syndrome bit-vectors
   int pbuf_off;  // register-row mode: LDS byte offset of the pivot-row broadcast buffer
+  int pnl_off;   // panel mode: LDS byte offset of the panel area (words, masks, pivot rows, indices)
   long long ws_words, iws_ints;
 };
 
@@ -421,7 +422,14 @@ __device__ inline u64 ord_key(double x) {
 // q.. in an LDS buffer and the rows that have the pivot bit xor them in registers, so a row
 // update costs no LDS writes (the word-major LDS / HBM image paid one 8-byte store per word and
 // row).  The reduced rows go to the HBM slice afterwards for the candidate bit-vectors.
-template <int LB, int WR = 0, int RPT = 1>
+// PNL (register-row mode): panel elimination.  Pivots are searched a 64-column panel (one row word)
+// at a time by ONE wave that holds every row's panel word and a 64-bit combination mask per row
+// (which of the panel's pivot rows, in their panel-start state, the row has absorbed): no barrier
+// per pivot.  Then the panel's pivot rows publish their remaining words once and every row xors in
+// the rows its mask names (uniform loop, broadcast LDS reads).  Same pivots (the lexicographic
+// minimum of (first set bit >= scan position, row) over unused rows, on up-to-date words) and the
+// same reduced rows as the per-pivot elimination; three barriers per panel instead of two per pivot.
+template <int LB, int WR = 0, int RPT = 1, int PNL = 0>
 __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
@@ -542,6 +550,137 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
       u64* pbuf = reinterpret_cast<u64*>(smem + A.pbuf_off);  // [WR] pivot row, [WR] its syndrome bit
       OSD_ST(1)
       int npiv = 0;   // uniform
+      if constexpr (PNL) {
+        static_assert(RPT == 1, "panel mode: one row per thread");
+        constexpr int SM = LB / 64;  // row slots per lane of the search wave (rows s * 64 + lane)
+        constexpr u64 kLo = 0xFFFFFFFFull, kHi = ~kLo;
+        uint32_t* pw = reinterpret_cast<uint32_t*>(smem + A.pnl_off);  // [m] panel half-word of every row
+        uint32_t* pmask = pw + m;                                     // [m] combination masks
+        u64* prow = reinterpret_cast<u64*>(smem + A.pnl_off + (((size_t)8 * m + 15) & ~(size_t)15));  // [32][WR+1]
+        int* pk = reinterpret_cast<int*>(prow + 32 * (WR + 1));       // [32] pivot rows of the panel
+        int* pidx = pk + 32;                                          // [m] panel index of a pivot row
+        __shared__ int s_P;
+        uint32_t usedm = 0;  // search wave: bit s = row s * 64 + lane is used (rows >= m: always)
+        if (tid < 64) {
+#pragma unroll
+          for (int s2 = 0; s2 < SM; ++s2)
+            if (s2 * 64 + tid >= m) usedm |= 1u << s2;
+        }
+        // panels of 32 columns (half a row word): 32-bit panel words and masks keep the search
+        // wave's state at 2 VGPRs per row slot.  Runtime panel index; row words are selected by
+        // compile-time index under uniform predicates (never indexed dynamically: they stay in VGPRs).
+        for (int qh = 0; qh < 2 * WR; ++qh) {
+          const int q = qh >> 1, h = qh & 1;
+          if (qh * 32 >= n || npiv >= rank) break;  // uniform
+          const int bend = n - qh * 32 < 32 ? n - qh * 32 : 32;
+          // 1. every row's panel half-word (up to date: all earlier panels applied)
+          if (tid < m) {
+            u64 wq = 0;
+#pragma unroll
+            for (int q2 = 0; q2 < WR; ++q2)
+              if (q2 == q) wq = row[0][q2];
+            pw[tid] = (uint32_t)(h ? wq >> 32 : wq);
+          }
+          __syncthreads();
+          // 2. the search wave: greedy pivots of this panel, masks and final half-words of every row
+          if (tid < 64) {
+            uint32_t wv[SM], cm[SM];
+#pragma unroll
+            for (int s2 = 0; s2 < SM; ++s2) {
+              wv[s2] = s2 * 64 + tid < m ? pw[s2 * 64 + tid] : 0u;
+              cm[s2] = 0u;
+            }
+            const uint32_t wmask = bend < 32 ? (1u << bend) - 1u : ~0u;
+            int P = 0, b = 0;
+            while (b < bend && npiv < rank) {  // uniform
+              const uint32_t lowm = (~0u << b) & wmask;
+              uint32_t key = 0x7FFFFFFFu;  // (first set bit << 11) | row
+#pragma unroll
+              for (int s2 = 0; s2 < SM; ++s2) {
+                const uint32_t mm = ((usedm >> s2) & 1u) ? 0u : (wv[s2] & lowm);
+                const uint32_t kj = mm ? ((uint32_t)(__ffs((int)mm) - 1) << 11) | (uint32_t)(s2 * 64 + tid) : 0x7FFFFFFFu;
+                key = kj < key ? kj : key;
+              }
+              key = wave_min_u32(key);
+              if (key == 0x7FFFFFFFu) break;  // no pivot left in this panel (uniform)
+              const int fb = (int)(key >> 11), r = (int)(key & 2047u), sr = r >> 6, lr = r & 63;
+              uint32_t pwv = 0, pmv = 0;
+#pragma unroll
+              for (int s2 = 0; s2 < SM; ++s2)
+                if (s2 == sr) {  // uniform
+                  pwv = wv[s2];
+                  pmv = cm[s2];
+                }
+              pwv = (uint32_t)__builtin_amdgcn_readlane((int)pwv, lr);
+              pmv = (uint32_t)__builtin_amdgcn_readlane((int)pmv, lr);
+              if (tid == lr) usedm |= 1u << sr;
+              if (tid == 0) {
+                pivrow[npiv] = r;
+                pivpos[npiv] = qh * 32 + fb;
+                pk[P] = r;
+                pidx[r] = P;
+              }
+              const uint32_t add = pmv | (1u << P);
+#pragma unroll
+              for (int s2 = 0; s2 < SM; ++s2) {
+                const bool hb = ((wv[s2] >> fb) & 1u) != 0 && s2 * 64 + tid != r;
+                wv[s2] ^= hb ? pwv : 0u;
+                cm[s2] ^= hb ? add : 0u;
+              }
+              ++P;
+              ++npiv;
+              b = fb + 1;
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < SM; ++s2)
+              if (s2 * 64 + tid < m) {
+                pw[s2 * 64 + tid] = wv[s2];
+                pmask[s2 * 64 + tid] = cm[s2];
+              }
+            if (tid == 0) {
+              s_P = P;
+              s_npiv = npiv;
+            }
+          }
+          __syncthreads();
+          const int P = s_P;
+          npiv = s_npiv;
+          // 3. the panel's pivot rows publish their panel-start words q.. and syndrome bit
+          if (tid < m) {
+            const int kx = pidx[tid];
+            if (kx >= 0 && kx < P && pk[kx] == tid) {  // (stale entries of earlier panels fail the check)
+              u64* dst = prow + kx * (WR + 1);
+#pragma unroll
+              for (int q2 = 0; q2 < WR; ++q2)
+                if (q2 >= q) dst[q2] = row[0][q2];
+              dst[WR] = sbit[0];
+            }
+          }
+          __syncthreads();
+          // 4. every row: the final panel half-word, then the named pivot rows into everything past
+          // the panel (the high half of word q when the panel is its low half, words q+1..)
+          if (tid < m) {
+            const uint32_t msk = pmask[tid];
+            u64 accq = 0;
+            for (int kx = 0; kx < P; ++kx) {  // uniform loop: one broadcast read per word
+              if ((msk >> kx) & 1u) {
+                const u64* src = prow + kx * (WR + 1);
+#pragma unroll
+                for (int q2 = 0; q2 < WR; ++q2) {
+                  if (q2 == q && h == 0) accq ^= src[q2];
+                  if (q2 > q) row[0][q2] ^= src[q2];
+                }
+                sbit[0] ^= (uint32_t)src[WR];
+              }
+            }
+            const u64 fw = (u64)pw[tid];
+#pragma unroll
+            for (int q2 = 0; q2 < WR; ++q2)
+              if (q2 == q) row[0][q2] = h ? ((row[0][q2] & kLo) | (fw << 32)) : (((row[0][q2] ^ accq) & kHi) | fw);
+          }
+          // (the next panel rewrites pw[tid] / prow only behind its first two barriers)
+        }
+      } else {
       int step3 = 0;  // search step mod 3: s_piv slot of the step (triple-buffered as above)
       int spar = 0;   // search step mod 2
 #pragma unroll
@@ -647,6 +786,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
           b = fb + 1;
         }
       }
+      }  // per-pivot elimination
       // reduced rows -> the HBM slice (word-major), syndrome bits -> sb
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
@@ -918,6 +1058,7 @@ struct qldpc_osd_gpu {
   int device = 0, grid = 0, W = 0, RW = 0, NP = 0, nh = 0, m_lds = 0, bits_off = 0;
   int wr = 0, pbuf_off = 0;  // register-row mode: compile-time words per row (0 = off), LDS pivot buffer
   int rr_tb = 0;             // register-row mode: threads per workgroup = m rounded up to waves
+  int pnl = 0, pnl_off = 0;  // register-row mode: panel elimination (QLDPC_OSD_PNL), its LDS area
   size_t lds = 0;
   long long ws_words = 0, iws_ints = 0;
   qldpc_rt::DevBuf rp, ci, ws, iws;
@@ -986,21 +1127,28 @@ constexpr int kOsdWR[] = {2, 4, 8, 12, 16, 20, 25};
 constexpr int osd_rpt(int) { return 1; }
 inline int osd_rr_threads(int wr) { return wr <= 16 ? 1024 : 768; }
 using OsdKern = void (*)(OsdGpuArgs);
-template <int WR>
+template <int WR, int PNL>
 OsdKern osd_rr_wide(int) {
-  return &osd_gpu_kernel<768, WR, 1>;
+  return &osd_gpu_kernel<768, WR, 1, PNL>;
 }
-OsdKern osd_rr_kernel(int wr) {
+template <int PNL>
+OsdKern osd_rr_kernel_t(int wr) {
   switch (wr) {
-    case 2: return &osd_gpu_kernel<1024, 2>;
-    case 4: return &osd_gpu_kernel<1024, 4>;
-    case 8: return &osd_gpu_kernel<1024, 8>;
-    case 12: return &osd_gpu_kernel<1024, 12>;
-    case 16: return &osd_gpu_kernel<1024, 16>;
-    case 20: return osd_rr_wide<20>(osd_rpt(wr));
-    case 25: return osd_rr_wide<25>(osd_rpt(wr));
+    case 2: return &osd_gpu_kernel<1024, 2, 1, PNL>;
+    case 4: return &osd_gpu_kernel<1024, 4, 1, PNL>;
+    case 8: return &osd_gpu_kernel<1024, 8, 1, PNL>;
+    case 12: return &osd_gpu_kernel<1024, 12, 1, PNL>;
+    case 16: return &osd_gpu_kernel<1024, 16, 1, PNL>;
+    case 20: return osd_rr_wide<20, PNL>(osd_rpt(wr));
+    case 25: return osd_rr_wide<25, PNL>(osd_rpt(wr));
     default: return nullptr;
   }
+}
+OsdKern osd_rr_kernel(int wr, int pnl) { return pnl ? osd_rr_kernel_t<1>(wr) : osd_rr_kernel_t<0>(wr); }
+// LDS bytes of the panel area (osd_gpu_kernel PNL): half-words + masks [m] (u32), pivot rows [32][WR+1],
+// pk [32], pidx [m]
+inline size_t osd_pnl_bytes(int m, int wr) {
+  return (((size_t)8 * m + 15) & ~(size_t)15) + (size_t)32 * (wr + 1) * 8 + 128 + (size_t)4 * m;
 }
 }  // namespace
 
@@ -1085,6 +1233,16 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   const size_t prows = QLDPC_OSD_1B ? 2 * (size_t)(osd_rr_threads(std::max(2, G->wr)) / 64) : 1;
   G->lds = G->wr ? (size_t)G->pbuf_off + prows * (size_t)(G->wr + 1) * 8 + (size_t)std::max(1, rank) * 4
                  : (size_t)G->bits_off + lbits;
+  // panel elimination (register-row mode), opt-in QLDPC_OSD_PNL=1: bit-exact, but the single search
+  // wave's per-pivot chain (one wave alone issues a VALU op every 4 cycles) is longer than the two
+  // barriers it saves: n1600 OSD-E(10) 6.66 vs 3.08 us per syndrome, BP+OSD 257k vs 490k shots/s
+  // (profiles/r03/bposd_pnl/)
+  const char* pnl_env = std::getenv("QLDPC_OSD_PNL");
+  if (G->wr && pnl_env && std::atoi(pnl_env) != 0) {
+    G->pnl = 1;
+    G->pnl_off = (int)((G->lds + 15) & ~(size_t)15);
+    G->lds = (size_t)G->pnl_off + osd_pnl_bytes(m, G->wr);
+  }
   G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW;
   G->iws_ints = 2ll * rank + 3ll * n;
   auto fail = [&](int code) {
@@ -1097,7 +1255,7 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)
     return fail(set_err(QLDPC_EHIP, "device CU count"));
   int nb = 0;
-  const void* kf = G->wr ? reinterpret_cast<const void*>(osd_rr_kernel(G->wr))
+  const void* kf = G->wr ? reinterpret_cast<const void*>(osd_rr_kernel(G->wr, G->pnl))
                   : G->m_lds ? reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreadsLds>)
                              : reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreads>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf,
@@ -1155,10 +1313,11 @@ int osd_gpu_decode_slots(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double
   a.m = osd->host.m; a.n = osd->host.n; a.W = osd->W; a.RW = osd->RW; a.rank = osd->host.rank;
   a.method = osd->host.method; a.order = osd->host.order; a.NP = osd->NP; a.m_lds = osd->m_lds; a.bits_off = osd->bits_off;
   a.pbuf_off = osd->pbuf_off;
+  a.pnl_off = osd->pnl_off;
   a.ws_words = osd->ws_words; a.iws_ints = osd->iws_ints;
   const int grid = (int)std::min<long long>(B, osd->grid);
   if (osd->wr)
-    hipLaunchKernelGGL(osd_rr_kernel(osd->wr), dim3(grid), dim3(osd->rr_tb), osd->lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(osd_rr_kernel(osd->wr, osd->pnl), dim3(grid), dim3(osd->rr_tb), osd->lds, (hipStream_t)stream, a);
   else if (osd->m_lds)
     hipLaunchKernelGGL(osd_gpu_kernel<kOsdThreadsLds>, dim3(grid), dim3(kOsdThreadsLds), osd->lds, (hipStream_t)stream, a);
   else

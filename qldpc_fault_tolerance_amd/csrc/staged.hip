@@ -569,7 +569,13 @@ int staged_mc_prepare(qldpc_mc* mc, const qldpc_graph* logical_x, const qldpc_gr
   // keeps its lanes refilled instead of waiting on the batch's slowest decode
   const bool hbm = (mc->dec[0] && mc->dec[0]->engine == 6) || (mc->dec[1] && mc->dec[1]->engine == 6);
   const char* eb = std::getenv("QLDPC_STAGED_BATCH");
-  long long B = (eb && *eb) ? std::max(64LL, std::atoll(eb) / 64 * 64) : (hbm ? kStagedBatch * 16 : kStagedBatch);
+  // HBM engine: 4M shots per batch (~32 decodes per resident lane and sector: the batch's tail, where
+  // lanes run out of syndromes and their partial-wave accesses still move whole lines, drops from 1/2
+  // of the traffic at 262k shots to a few %; LP L30 fp64 0.28 -> 0.45 of HBM, profiles/r03/e6/),
+  // bounded to ~8 GB of per-shot buffers
+  const long long hbm_b = std::max<long long>(kStagedBatch, std::min<long long>(kStagedBatch * 64,
+                                                                                 (8ll << 30) / std::max(1, n + d0->g->m)));
+  long long B = (eb && *eb) ? std::max(64LL, std::atoll(eb) / 64 * 64) : (hbm ? hbm_b / 64 * 64 : kStagedBatch);
   const size_t W = (size_t)(B / 64);
   int mm = 1, rc;
   for (int q = 0; q < 2; ++q) {

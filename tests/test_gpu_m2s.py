@@ -66,17 +66,26 @@ def test_m2s_decode_matches_oracle(gpu, oracle, sector, p):
 
 
 def test_m2s_adaptive_alpha_and_zero_priors_match_oracle(gpu, oracle):
+    """Adaptive alpha and all-zero priors on the m2s family; non-uniform priors take the two-word
+    family (the m2s kernels keep one prior in SGPRs: QLDPC_M2S_UNIL)."""
     code = codes.get_code("hgp_34_n1600")
     H = code.hz
     synd = _synd(H, 0.05, 256, seed=5)
     c, i, v = _dec(H, 0.05, 60, alpha=0.0).decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, 0.05, 60, "minimum_sum", 0.0, synd, 64)
     assert np.array_equal(c, oc.astype(np.int64)) and np.array_equal(i, oi) and np.array_equal(v, ov)
+    # every prior zero (p = 0.5): messages that are exactly +-0 on the one-prior m2s kernels
+    dec = _dec(H, 0.5, 12)
+    assert dec.geometry()["kernel_id"] == 11103
+    c, i, v = dec.decode_batch(synd)
+    oc, oi, ov = oracle.bp_decode_batch(H, 0.5, 12, "minimum_sum", 0.625, synd, 64)
+    assert np.array_equal(c, oc.astype(np.int64)) and np.array_equal(i, oi) and np.array_equal(v, ov)
+    # non-uniform priors (some zero): the m2s kernels hold one prior, so the two-word family serves
     rng = np.random.default_rng(3)
     probs = np.full(code.N, 0.04)
-    probs[rng.random(code.N) < 0.3] = 0.5  # zero prior LLRs: messages that are exactly +-0
+    probs[rng.random(code.N) < 0.3] = 0.5
     dec = _dec(H, probs, 40)
-    assert dec.geometry()["kernel_id"] == 11103
+    assert dec.geometry()["kernel_id"] == 103
     c, i, v = dec.decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, probs, 40, "minimum_sum", 0.625, synd, 64)
     assert np.array_equal(c, oc.astype(np.int64)) and np.array_equal(i, oi) and np.array_equal(v, ov)
