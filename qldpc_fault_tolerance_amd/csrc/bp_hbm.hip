@@ -9,9 +9,7 @@
 // (fp32) segment of an [edge][lane] array in HBM:
 //   V [E][64]   v2c, canonical bits (sign := v2c <= 0), row-major edge order
 //   C [E][64]   c2v, column-major edge order (rows ascending per column)
-//   X [n]       decisions, one 64-bit ballot word per variable (bit = lane; 8 KB per wave for
-//               n = 1020: L2-resident, instead of 64 bytes per edge read from HBM); syndromes are
-//               read straight from the [B][m] input
+//   X [n][64]   decisions (u8); syndromes are read straight from the [B][m] input
 // One flooding iteration = a check sweep (rows: read V, min / second min /
 // parity, write every edge's c2v = (-1)^sgn alpha min_{others}|v2c| into C at
 // its column-major position; the H x == s test of the previous iteration's
@@ -19,7 +17,7 @@
 // / backward sums in row order, write canonical v2c back into V, the decision
 // into X).  Per edge and iteration that is one read and one write of each of V
 // and C: 32 B (fp64) / 16 B (fp32) of HBM traffic, exactly SURVEY.md §8d's
-// algorithmic bytes (the decision words stay in L2).  No barrier, no LDS: waves
+// algorithmic bytes, plus 1 B of decision per edge.  No barrier, no LDS: waves
 // are independent; a lane whose decode ends takes the next syndrome from a device
 // queue at the next sweep boundary, so lanes of different iteration counts never
 // wait for each other.  The next row's / column's messages are loaded while the
@@ -98,7 +96,7 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
   unsigned char* wb = static_cast<unsigned char*>(A.ws) + (size_t)wave * A.ws_wave_bytes;
   U* __restrict__ V = reinterpret_cast<U*>(wb) + lane;
   U* __restrict__ C = reinterpret_cast<U*>(wb) + (size_t)A.E * 64 + lane;
-  unsigned long long* __restrict__ X = reinterpret_cast<unsigned long long*>(reinterpret_cast<U*>(wb) + (size_t)2 * A.E * 64);
+  uint8_t* __restrict__ X = reinterpret_cast<uint8_t*>(reinterpret_cast<U*>(wb) + (size_t)2 * A.E * 64) + lane;
   const T* __restrict__ L = static_cast<const T*>(llr);
   const int m = A.m, n = A.n;
   const bool adaptive = A.alpha == 0.0;
@@ -151,7 +149,7 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
               r.x[k] = 0;
             } else {
               r.v[k] = V[(size_t)(r.e0 + k) * 64];
-              r.x[k] = (uint8_t)((X[jv[k]] >> lane) & 1ull);  // same word for every lane: one fetch
+              r.x[k] = X[(size_t)jv[k] * 64];
             }
           }
         }
@@ -209,7 +207,7 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
     }
     if (__any(fin)) {
       if (fin) {
-        for (int j = 0; j < n; ++j) A.corr[shot * (long long)n + j] = (uint8_t)((X[j] >> lane) & 1ull);
+        for (int j = 0; j < n; ++j) A.corr[shot * (long long)n + j] = X[(size_t)j * 64];
         if (A.iters) A.iters[shot] = conv ? it : A.max_iter;
         if (A.conv) A.conv[shot] = (uint8_t)conv;
         shot = -1;
@@ -255,11 +253,8 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
           acc = acc + c[t];
         }
       }
-      // decisions of the wave's lanes as one ballot word (uniform control flow; lanes not running
-      // leave a 0 that nobody reads)
-      const unsigned long long xw = __ballot(run && acc <= (T)0);
-      if (lane == 0) X[j] = xw;
       if (run) {
+        X[(size_t)j * 64] = acc <= (T)0 ? 1 : 0;
         // backward sums: v2c_t = f_t + ((c_last + ...) + c_{t+1}); the redundant `0 + c`
         // and `f + 0` of ldpc's loop change at most the sign of a zero (erased by hcanon)
         T b = (T)0;
@@ -321,7 +316,7 @@ int hbm_prepare(qldpc_bp* bp) {
 
 size_t hbm_wave_bytes(const qldpc_bp* bp) {
   const size_t tsize = bp->precision == 32 ? 4 : 8;
-  const size_t b = (size_t)2 * bp->g->nnz * 64 * tsize + (size_t)bp->g->n * 8;
+  const size_t b = (size_t)2 * bp->g->nnz * 64 * tsize + (size_t)bp->g->n * 64;
   return (b + 255) & ~(size_t)255;
 }
 

@@ -77,7 +77,11 @@ constexpr int eng_tail(int E) { return (E / 1000) % 10; }
 // no longer holds the edge's own previous v2c (kept in VGPRs) is the argmin, and its value is m2.
 // The image shrinks by 8 bytes per check; with rows of 7 as 3 chunks + a tail slot the n1600 fp64
 // image is 52.3 KB, so 3 workgroups share a CU (168-VGPR budget).
-constexpr bool eng_m2s(int E) { return (E / 10000) % 10 != 0; }
+constexpr bool eng_m2s(int E) { return (E / 10000) % 10 == 1; }
+// + 20000 = byte F ("fb": the per-check flags F as one byte per check instead of a word, flips
+// xored into the containing word at the byte's shift): the fp32 space-time tail family for 512-thread
+// workgroups (engine id 21013), whose 79.6 KB image lets 2 decodes share a CU
+constexpr bool eng_fb(int E) { return (E / 10000) % 10 == 2; }
 // launch bounds: LB threads per workgroup at most; 256-thread fp64 kernels are
 // built for 2 workgroups per CU (2 waves per SIMD: up to 256 VGPRs, no spills)
 template <typename T, int ENG>
@@ -85,7 +89,7 @@ constexpr int lb_waves(int LB) {
   // engine 4 fp64 images (no CS array) fit 3 workgroups per CU: <= 168 VGPRs
   // (the fp64 512-thread family: 2 workgroups of 8 waves per CU, 128 VGPRs)
   return LB <= 256 ? (sizeof(T) == 8 ? ((eng_base(ENG) == 4 || eng_m2s(ENG)) ? 3 : 2) : 4)
-                   : (LB <= 512 && eng_kv64(ENG)) ? 4 : 1;
+                   : (LB <= 512 && (eng_kv64(ENG) || eng_fb(ENG))) ? 4 : 1;
 }
 __device__ inline unsigned long long qstamp() {
 #if QLDPC_STAMPS
@@ -109,12 +113,13 @@ struct RLayout {
 
 // [CS][V][tail: one slot per row label (tail layouts only)][F][sink][lred]
 // (m2s: CS entries of one message word instead of two)
-__host__ __device__ inline RLayout r_layout(int eng, int vslots, int mmax, int tsize, int tail = 0, int m2s = 0) {
+__host__ __device__ inline RLayout r_layout(int eng, int vslots, int mmax, int tsize, int tail = 0, int m2s = 0,
+                                            int fb = 0) {
   RLayout L;
   L.v = eng == 4 ? 0u : (uint32_t)a16((size_t)(mmax + 1) * (m2s ? 1 : 2) * tsize);
   L.t = L.v + (uint32_t)a16((size_t)vslots * tsize);
   L.f = L.t + (tail ? (uint32_t)a16((size_t)mmax * tsize) : 0u);
-  L.sink = L.f + (uint32_t)a16((size_t)(mmax + 1) * 4);
+  L.sink = L.f + (uint32_t)a16((size_t)(mmax + 1) * (fb ? 1 : 4));
   L.lred = L.sink + (eng == 4 ? 16u : 0u);
   L.total = L.lred + 48;
   return L;
@@ -323,25 +328,54 @@ __device__ inline uint32_t f_addr(uint32_t ea, const FMap& M) {
   if (eng_base(ENG) == 4) return M.fbase + 4u * (uint32_t)((int)((ea & 0xFFFFu) - M.rstart) >> M.rsh);
   return (ea_cs<ENG>(ea) >> (sizeof(T) == 4 ? 1 : 2)) + M.fbase;
 }
+// F entry access (engine 3): entry e (= check label + 1) at byte Ly.f + 4e, or Ly.f + e in byte-F
+// kernels, whose xors go to the containing word at the byte's shift (order-free, so still atomic
+// and commutative) and whose plain stores are byte stores (one owner per byte)
+template <int ENG>
+__device__ inline uint32_t f_off(const RLayout& Ly, int e) {
+  return Ly.f + (eng_fb(ENG) ? (uint32_t)e : 4u * (uint32_t)e);
+}
+template <int ENG>
+__device__ inline uint32_t f_ld(unsigned char* smem, uint32_t off) {
+  if constexpr (eng_fb(ENG)) return lds_at<uint8_t>(smem, off);
+  return lds_at<uint32_t>(smem, off);
+}
+template <int ENG>
+__device__ inline void f_st(unsigned char* smem, uint32_t off, uint32_t v) {
+  if constexpr (eng_fb(ENG))
+    lds_at<uint8_t>(smem, off) = (uint8_t)v;
+  else
+    lds_at<uint32_t>(smem, off) = v;
+}
+template <int ENG>
+__device__ inline void f_xor(unsigned char* smem, uint32_t off, uint32_t v) {
+  if constexpr (eng_fb(ENG))
+    atomicXor(&lds_at<uint32_t>(smem, off & ~3u), v << (8u * (off & 3u)));
+  else
+    atomicXor(&lds_at<uint32_t>(smem, off), v);
+}
+
 // F word offset of edge (k, t) (engine 3); split addresses are absolute: fbase is then
 // Ly.f - (LDS base >> 2)
 template <typename T, int DMAX, int VPL, int ENG>
 __device__ inline uint32_t r_fa(const RState<T, DMAX, VPL, ENG>& R, int k, int t, uint32_t fbase) {
   // CS entry (i + 1) of 2 words (fp32: 8 B, fp64: 16 B) or, m2s, one fp64 word (8 B) -> F word i + 1
+  // (byte-F kernels: fp32 CS entries of 8 B -> F byte i + 1)
+  if constexpr (eng_fb(ENG)) return (r_csa(R, k, t) >> 3) + fbase;
   return (r_csa(R, k, t) >> ((sizeof(T) == 4 || eng_m2s(ENG)) ? 1 : 2)) + fbase;
 }
 
 // Opaque redefinition of the edge words (no instruction): without it the
 // compiler hoists their derived CS / V / F addresses out of the iteration and
 // shot loops, tripling the VGPRs per edge and spilling.
-// m2s kernels (D3K > 0 passed) keep no edge words for the unused 4th edge of degree-3 slots.
+// m2s and byte-F kernels (D3K > 0 passed) keep no edge words for the unused 4th edge of degree-3 slots.
 template <typename T, int DMAX, int VPL, int ENG, int D3K = 0>
 __device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
 #pragma unroll
   for (int k = 0; k < VPL; ++k)
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
-      if (eng_m2s(ENG) && k < D3K && t >= 3) continue;
+      if ((eng_m2s(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;
       asm volatile("" : "+v"(R.ea[k][t]));
       if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) asm volatile("" : "+v"(R.ev[k][t]));
     }
@@ -445,11 +479,11 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
 #elif QLDPC_FLIP_BRANCHFREE
   // diagnostic variant: every edge xors (x != xprev) into its check's F word, no branch
 #pragma unroll
-  for (int t = 0; t < ND; ++t) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), (uint32_t)(x != xprev));
+  for (int t = 0; t < ND; ++t) f_xor<ENG>(smem, r_fa(R, k, t, fdelta), (uint32_t)(x != xprev));
 #else
   if (x != xprev) {
 #pragma unroll
-    for (int t = 0; t < ND; ++t) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), 1u);
+    for (int t = 0; t < ND; ++t) f_xor<ENG>(smem, r_fa(R, k, t, fdelta), 1u);
   }
 #endif
   return x;
@@ -495,7 +529,7 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   constexpr int N3 = DMAX > 3 ? 3 : DMAX;  // low-degree slots use 3 edge slots
   constexpr int PF0 = QLDPC_PF >= 1 ? QLDPC_PF : (RState<T, DMAX, VPL, ENG>::kSplit ? 2 : 1);
   constexpr int PF = PF0 < VPL ? PF0 : VPL;
-  r_launder(R);
+  r_launder<T, DMAX, VPL, ENG, D3K>(R);
   uint32_t xbits = 0;
   // gather ring: variable k's CS entries (and, without kKeepV, own v2c) live in slot k % PF
   typename CSEntry<T>::type pb[PF][DMAX];
@@ -528,7 +562,7 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
       const int nd = k < D3K ? N3 : DMAX;
 #pragma unroll
       for (int t = 0; t < DMAX; ++t)
-        if (t < nd) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), 1u);
+        if (t < nd) f_xor<ENG>(smem, r_fa(R, k, t, fdelta), 1u);
     }
   }
 #endif
@@ -619,7 +653,7 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
 // non-negative, non-NaN doubles the float order is the bit order and the
 // results are inputs unchanged, i.e. the integer min / second min of |v2c| bits
 // (three instructions per edge instead of three 64-bit compares + six selects).
-template <typename T, bool FIRST, int NCH, int TAIL = 0, int PFC = 1>
+template <typename T, bool FIRST, int NCH, int TAIL = 0, int PFC = 1, int ENG = 3>
 __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, int tid, int TB, uint32_t& sbits) {
   using U = typename FT<T>::U;
   using VT = typename V16<T>::type;
@@ -654,7 +688,7 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
 #pragma unroll
       for (int c = 0; c < NCH; ++c) v[c] = *reinterpret_cast<const VT*>(row + coff[c]);
       if (TAIL) tv = lds_at<T>(smem, Ly.t + (uint32_t)r * (uint32_t)sizeof(T));
-      fv = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(r + 1));
+      fv = f_ld<ENG>(smem, f_off<ENG>(Ly, r + 1));
     }
   };
   VT cur[NCH], mid[NCH];
@@ -675,7 +709,7 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
     if (FIRST) {
       s = ((fcur >> 1) ^ (fcur >> 2)) & 1u;  // as r_check: syndrome ^ row-degree parity
       sbits |= s << q;
-      lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1)) = (fcur & 4u) | ((fcur >> 2) & 1u);
+      f_st<ENG>(smem, f_off<ENG>(Ly, i + 1), (fcur & 4u) | ((fcur >> 2) & 1u));
     } else {
       s = (sbits >> q) & 1u;
       mism |= (int)((fcur ^ s) & 1u);
@@ -1084,11 +1118,11 @@ __device__ inline void r_fill(const SSector& S, unsigned char* smem, const RLayo
   (void)vslots;
   const int nchunks = (int)((Ly.f - Ly.v) / 16u);  // V rows and (tail layouts) the tail slots
   for (int i = tid; i < nchunks; i += TB) V4[i] = (eng_base(ENG) == 4 && i == 0) ? V16<T>::splat((T)0) : s;
-  uint32_t* F = reinterpret_cast<uint32_t*>(smem + Ly.f);
   // engine 4: row degree in the high half; engine 3: row-degree parity in bit 2 (w domain)
   for (int i = tid; i <= mmax; i += TB)
-    F[i] = (i >= 1 && i <= S.m) ? (eng_base(ENG) == 4 ? ((uint32_t)S.rdeg[i - 1] << 16) : (((uint32_t)S.rdeg[i - 1] & 1u) << 2))
-                                : 0u;
+    f_st<ENG>(smem, f_off<ENG>(Ly, i),
+              (i >= 1 && i <= S.m) ? (eng_base(ENG) == 4 ? ((uint32_t)S.rdeg[i - 1] << 16) : (((uint32_t)S.rdeg[i - 1] & 1u) << 2))
+                                   : 0u);
   uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);
   if (tid < 10) lred[tid] = 0;  // lred[0..7], flags[0..1]
   if (eng_base(ENG) == 3 && tid == 0) {
@@ -1166,7 +1200,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         const U cl = FT<T>::bits(r_prior(R, k));  // w domain: the prior as is
 #pragma unroll
         for (int t = 0; t < DMAX; ++t) {
-          if (eng_m2s(ENG) && k < D3K && t >= 3) continue;  // (m2s: no dummy 4th edge kept)
+          if ((eng_m2s(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;  // (no dummy 4th edge kept)
           lds_st<U, SP>(smem, r_va(R, k, t), cl);
           if (KV) R.ov[KV ? k : 0][KV ? t : 0] = cl;
         }
@@ -1198,8 +1232,11 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
             if (e) {
 #pragma unroll
               for (int t = 0; t < DMAX; ++t) {
-                if (eng_m2s(ENG) && k < D3K && t >= 3) continue;
-                atomicXor(&lds_at<uint32_t>(smem, eng_base(ENG) == 4 ? f_addr<T, ENG>(R.ea[k][t], M) : r_fa(R, k, t, M.fbase)), 2u);
+                if ((eng_m2s(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;
+                if constexpr (eng_base(ENG) == 4)
+                  atomicXor(&lds_at<uint32_t>(smem, f_addr<T, ENG>(R.ea[k][t], M)), 2u);
+                else
+                  f_xor<ENG>(smem, r_fa(R, k, t, M.fbase), 2u);
               }
             }
           }
@@ -1207,9 +1244,10 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       } else {
         const uint8_t* srow = D->synd + (c0 + sh) * (long long)m;
         for (int i = tidl; i < m; i += TB) {  // i = check label (engine 3: S.rperm maps it to the check)
-          uint32_t& F = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
+          const uint32_t fo = f_off<ENG>(Ly, i + 1);
+          const uint32_t F = f_ld<ENG>(smem, fo);
           const int oi = S.rperm ? S.rperm[i] : i;
-          F = (eng_base(ENG) == 4 ? (F & 0xFFFF0000u) : (F & 4u)) | ((uint32_t)(srow[oi] & 1u) << 1);
+          f_st<ENG>(smem, fo, (eng_base(ENG) == 4 ? (F & 0xFFFF0000u) : (F & 4u)) | ((uint32_t)(srow[oi] & 1u) << 1));
         }
       }
     }
@@ -1255,7 +1293,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     else if constexpr (eng_m2s(ENG))
       m_check<T, true, NCH, eng_tail(ENG)>(smem, Ly, m, wbase, tid, TB, sb);
     else if constexpr (NCH > 0)
-      r_check_c<T, true, NCH, eng_tail(ENG), QLDPC_PFC>(smem, Ly, m, tid, TB, sb);
+      r_check_c<T, true, NCH, eng_tail(ENG), QLDPC_PFC, ENG>(smem, Ly, m, tid, TB, sb);
     else
       r_check<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     __syncthreads();
@@ -1292,7 +1330,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
         // (the 1024-thread tail family runs one workgroup per CU: nothing to take priority over)
-        constexpr int kPV = (eng_tail(ENG) && !eng_m2s(ENG)) ? 0 : QLDPC_PRIO_V;
+        constexpr int kPV = (eng_tail(ENG) && !eng_m2s(ENG) && !eng_fb(ENG)) ? 0 : QLDPC_PRIO_V;
         if (kPV) __builtin_amdgcn_s_setprio(kPV);
         if constexpr (eng_m2s(ENG))
           xb = m_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
@@ -1315,7 +1353,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         if constexpr (eng_m2s(ENG))
           mism = m_check<T, false, NCH, eng_tail(ENG)>(smem, Ly, m, wbase, tid, TB, sb);
         else if constexpr (NCH > 0)
-          mism = r_check_c<T, false, NCH, eng_tail(ENG), QLDPC_PFC>(smem, Ly, m, tid, TB, sb);
+          mism = r_check_c<T, false, NCH, eng_tail(ENG), QLDPC_PFC, ENG>(smem, Ly, m, tid, TB, sb);
         else
           mism = r_check<T, false>(smem, Ly, m, nch, tid, TB, sb, alpha_next);
         if (QLDPC_PRIO_C) __builtin_amdgcn_s_setprio(0);
@@ -1347,7 +1385,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         int qq = 0;
         for (int i = tidl; i < m; i += TB, ++qq)  // sb holds syndrome ^ row-degree parity (F bit 2)
           cs[S.rperm ? S.rperm[i] : i] =
-              (uint8_t)(((sb >> qq) ^ (lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1)) >> 2)) & 1u);
+              (uint8_t)(((sb >> qq) ^ (f_ld<ENG>(smem, f_off<ENG>(Ly, i + 1)) >> 2)) & 1u);
         uint8_t* ce = A->c_err[q] + cslot * (long long)n;
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
@@ -1419,7 +1457,7 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rmc_kernel(SMcArgs
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = A.chunk;
   const int fw = (CH + 31) / 32;
-  const RLayout Ly = r_layout(eng_base(ENG), A.vslots, A.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG));
+  const RLayout Ly = r_layout(eng_base(ENG), A.vslots, A.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG), eng_fb(ENG));
   uint32_t* fm0 = reinterpret_cast<uint32_t*>(smem + Ly.total);
   uint32_t* fm1 = fm0 + ((fw + 3) & ~3);
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(fm1 + ((fw + 3) & ~3));
@@ -1476,7 +1514,7 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rdec_kernel(SDecAr
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = D.chunk;
-  const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG));
+  const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG), eng_fb(ENG));
   const long long nchunks = (D.B + CH - 1) / CH;
   __shared__ long long s_next;
   long long ch = blockIdx.x;

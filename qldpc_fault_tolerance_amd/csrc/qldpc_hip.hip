@@ -99,7 +99,12 @@ bool use_f64x(int engine, int precision, int dmax, int tb, int vpl, int ea_shift
 
 // Slot-family kernels of an engine (2, 3 or 4).
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
-                      int nch = 0, int tail = 0, int m2s = 0) {
+                      int nch = 0, int tail = 0, int m2s = 0, int fb = 0) {
+  // fp32 space-time family with byte F words (rows of 2 chunks + a tail slot, 512 threads, 2 per CU)
+  if (fb) {
+    const bool ok = engine == 3 && precision == 32 && dmax == 4 && ea_shift == 2 && nch == 2 && tail && tb == 512;
+    return ok ? get_rvariant_f32_stfb(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
+  }
   // fp64 m2-in-slot family (rows of 3 chunks + a tail slot, <= 256 threads, 3 workgroups per CU)
   if (m2s) {
     const bool ok = engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && nch == 3 && tail && tb <= 256;
@@ -219,8 +224,8 @@ int choose_rgeometry(int n, int m, int requested_vpl, int& TB, int& VPL, int pre
 // Engines 3 and 4 address their image with 16-bit byte offsets.
 // Engines 3 and 4 address their image with 16-bit byte offsets; engine 3 with
 // dword-scaled offsets (kernel id 13, ea_shift 2) reaches 256 KiB.
-bool r_fits(int eng, int vslots, int mmax, int tsize, int ea_shift = 0, int tail = 0, int m2s = 0) {
-  const RLayout L = r_layout(eng, vslots, mmax, tsize, tail, m2s);
+bool r_fits(int eng, int vslots, int mmax, int tsize, int ea_shift = 0, int tail = 0, int m2s = 0, int fb = 0) {
+  const RLayout L = r_layout(eng, vslots, mmax, tsize, tail, m2s, fb);
   return L.lred <= (65536u << ea_shift) && r_lds_bytes((int)L.total, kChunkMax) <= (size_t)kLdsMax;
 }
 
@@ -381,7 +386,7 @@ static int upload_llr(qldpc_bp* bp) {
 // decode path maps syndromes through the inverse permutation (bp->rperm).
 static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
                              const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1,
-                             const std::vector<int>& lab = {}, int tail = 0) {
+                             const std::vector<int>& lab = {}, int tail = 0, int m2s = 0) {
   const int nv = 16 / tsize;  // messages per 16-byte chunk
   const int rw = nch * nv;
   const int rwt = rw + (tail ? 1 : 0);  // tail layouts: logical slot rw = the row's tail slot
@@ -408,7 +413,39 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
   // slot s on bank pair s mod 16 (MI355X_MICROARCH.md §LDS)
   const int sg = tsize == 4 ? 32 : 16, nb = tsize == 4 ? 32 : 16;
   const int vbase_u = vbase_dw < 0 ? 0 : (tsize == 4 ? vbase_dw : vbase_dw / 2);
-  if (vbase_dw >= 0 && rwt <= 32) {
+  if (vbase_dw >= 0 && rwt <= 32 && m2s) {
+    // m2s (fp64): the variable phase also READS each edge's V slot (ds_read_b64: 2 groups of 32
+    // lanes, 8-byte slot s on bank pair s mod 32), besides storing it (ds_write_b64: 4 groups of 16
+    // contiguous lanes, bank pair s mod 16).  Place per 32-lane group: distinct s mod 32 over the
+    // group first, distinct s mod 16 within each 16-lane half second.
+    std::vector<uint32_t> used(g->m, 0u);
+    for (int k = 0; k < VPL; ++k)
+      for (int d = 0; d < DM; ++d)
+        for (int h0 = 0; h0 < TB; h0 += 32) {
+          int c32[32] = {0}, c16[2][16] = {{0}};
+          for (int t = h0; t < h0 + 32 && t < TB; ++t) {
+            const int j = slot_var[(size_t)k * TB + t];
+            if (j < 0 || d >= (int)g->col_rows[j].size()) continue;
+            const int i = g->col_rows[j][d];
+            const int hf = (t - h0) >> 4;
+            int best = -1, bc = 1 << 30;
+            for (int ls = 0; ls < rwt; ++ls) {
+              if ((used[i] >> ls) & 1u) continue;
+              const int sl = vbase_u + phys(i, ls);
+              const int c = 4 * c32[sl % 32] + c16[hf][sl % 16];
+              if (c < bc) {
+                bc = c;
+                best = ls;
+              }
+            }
+            used[i] |= 1u << best;
+            const int sl = vbase_u + phys(i, best);
+            c32[sl % 32]++;
+            c16[hf][sl % 16]++;
+            lslot[edge_of(i, j)] = best;
+          }
+        }
+  } else if (vbase_dw >= 0 && rwt <= 32) {
     std::vector<uint32_t> used(g->m, 0u);
     for (int k = 0; k < VPL; ++k)
       for (int d = 0; d < DM; ++d)
@@ -773,8 +810,20 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       const int nch_t = 8 * tsize / 16;
       const int vst = (1 + g->m * nch_t) * (16 / tsize);
       int tb = 0, vpl = 0;
-      if (r_fits(3, vst, g->m, tsize, 2, 1) && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb > 512 &&
-          vpl >= 4 && vpl <= 8) {
+      // fp32: byte F words shrink the image below half a CU (config 5: 85.1 -> 79.6 KB), so two
+      // 512-thread decodes share a CU (bp_reg.h eng_fb; QLDPC_E3_FB=0 keeps one 1024-thread decode)
+      const int vpl_fb = (g->n + 511) / 512;
+      if (precision == 32 && vars_per_thread <= 0 && env_int("QLDPC_TB", 0) <= 0 && env_int("QLDPC_E3_FB", 1) != 0 &&
+          vpl_fb >= 9 && vpl_fb <= 12 && (g->m + 511) / 512 <= 32 && r_fits(3, vst, g->m, tsize, 2, 1, 0, 1) &&
+          2 * r_lds_bytes((int)r_layout(3, vst, g->m, tsize, 1, 0, 1).total, kChunkMax) <= (size_t)kLdsMax) {
+        bp->tail = 1;
+        bp->fb = 1;
+        bp->nch = nch_t;
+        bp->ea_shift = 2;
+        bp->TB = 512;
+        bp->VPL = vpl_fb;
+      } else if (r_fits(3, vst, g->m, tsize, 2, 1) && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) &&
+                 tb > 512 && vpl >= 4 && vpl <= 8) {
         bp->tail = 1;
         bp->nch = nch_t;
         bp->ea_shift = 2;
@@ -805,13 +854,14 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     }
     const int vslots_e3 = (1 + g->m * bp->nch) * (16 / tsize);
     if (bp->engine >= 3 && ((DM != 4 && !(bp->engine == 3 && (DM == 5 || DM == 6))) ||
-                            choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL, pref, vmax) ||
-                            !r_fits(bp->engine, vslots_e3, g->m, tsize, bp->ea_shift, bp->tail, bp->m2s) ||
+                            (!bp->fb && choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL, pref, vmax)) ||
+                            !r_fits(bp->engine, vslots_e3, g->m, tsize, bp->ea_shift, bp->tail, bp->m2s, bp->fb) ||
                             (precision == 64 && DM == 5 &&
                              !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch)))) {
       bp->ea_shift = 0;
       bp->tail = 0;
       bp->m2s = 0;
+      bp->fb = 0;
       bp->engine = 2;  // graph outside the register engines' envelope
       bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
       if (DM == 5 || DM == 6) bp->DMAX = DM = 8;  // engine 2 kernels come in 4 and 8 slots
@@ -819,7 +869,8 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     const int vslots2 = (1 + g->m * bp->nch) * (16 / tsize);
     if (bp->engine >= 3) {
       bp->NS = 1;
-      bp->lds_bytes = (int)r_lds_bytes((int)r_layout(bp->engine, vslots2, g->m, tsize, bp->tail, bp->m2s).total, kChunkMax);
+      bp->lds_bytes =
+          (int)r_lds_bytes((int)r_layout(bp->engine, vslots2, g->m, tsize, bp->tail, bp->m2s, bp->fb).total, kChunkMax);
     } else {
       rc = choose_sgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL);
       if (rc) return fail(rc);
@@ -882,9 +933,10 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       if (g->m && hipMemcpy(bp->rperm.p, inv.data(), (size_t)g->m * 4, hipMemcpyHostToDevice) != hipSuccess)
         return fail(set_err(QLDPC_EHIP, "upload check labels"));
     }
-    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab, bp->tail);
+    build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab, bp->tail,
+                     bp->m2s && env_int("QLDPC_M2S_PLACE", 1) != 0);
     kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch, bp->tail,
-                        bp->m2s).dec_k;
+                        bp->m2s, bp->fb).dec_k;
     if (bp->engine >= 3) {
       // row degrees by check label: engine 4 keeps them in F, engine 3 their parity (bp_reg.h, w domain)
       std::vector<uint8_t> deg(std::max(1, g->m));
@@ -951,6 +1003,8 @@ int qldpc_bp_kernel_id(const qldpc_bp* bp, int32_t* kernel_id, int32_t* row_chun
   if (bp->engine == 3) {
     if (bp->m2s)
       id = 11103;
+    else if (bp->fb)
+      id = 21013;
     else if (bp->tail)
       id = 1013;
     else if (use_f64w(bp->engine, bp->precision, bp->DMAX, bp->TB, bp->VPL, bp->ea_shift, bp->nch))
@@ -1080,7 +1134,7 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
     SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch,
-                              bp->tail, bp->m2s);
+                              bp->tail, bp->m2s, bp->fb);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;
@@ -1140,7 +1194,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
         dec_x->precision != dec_z->precision || dec_x->engine != dec_z->engine)
       return set_err(QLDPC_EINVAL, "sector decoders need identical geometry/precision (same vars_per_thread)");
     if (dec_x->g->device != dec_z->g->device) return set_err(QLDPC_EINVAL, "sector decoders on different devices");
-    if (dec_x->m2s != dec_z->m2s || dec_x->tail != dec_z->tail)
+    if (dec_x->m2s != dec_z->m2s || dec_x->tail != dec_z->tail || dec_x->fb != dec_z->fb)
       return set_err(QLDPC_EINVAL, "sector decoders use different LDS layouts (QLDPC_M2S)");
   }
   QLDPC_HIP(hipSetDevice(d0->g->device));
@@ -1174,6 +1228,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   mc->mmax = std::max(dec_x ? dec_x->g->m : 0, dec_z ? dec_z->g->m : 0);
   mc->tail = d0->tail;
   mc->m2s = d0->m2s;
+  mc->fb = d0->fb;
   const void* kern;
   if (mc->engine == 1) {
     mc->lds_bytes = (int)lds_for(mc->precision, mc->mmax);
@@ -1184,17 +1239,17 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
       if (d) mc->vslots = std::max(mc->vslots, (1 + d->g->m * d->nch) * (16 / tsize));
     mc->img_bytes = (int)slot_img_bytes(mc->vslots, mc->mmax, tsize);
     if (mc->engine >= 3) {
-      if (!r_fits(mc->engine, mc->vslots, mc->mmax, tsize, mc->ea_shift, mc->tail, mc->m2s))
+      if (!r_fits(mc->engine, mc->vslots, mc->mmax, tsize, mc->ea_shift, mc->tail, mc->m2s, mc->fb))
         return fail(set_err(QLDPC_ENOTSUP, "sector images exceed the register engines' 64 KiB addressing (QLDPC_ENGINE=2)"));
       mc->NS = 1;
       mc->lds_bytes =
-          (int)r_lds_bytes((int)r_layout(mc->engine, mc->vslots, mc->mmax, tsize, mc->tail, mc->m2s).total, kChunkMax);
+          (int)r_lds_bytes((int)r_layout(mc->engine, mc->vslots, mc->mmax, tsize, mc->tail, mc->m2s, mc->fb).total, kChunkMax);
     } else {
       mc->NS = choose_ns(mc->img_bytes);
       mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
     }
     kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch,
-                        mc->tail, mc->m2s).mc_k;
+                        mc->tail, mc->m2s, mc->fb).mc_k;
   }
   if (mc->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB"));
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
@@ -1383,7 +1438,7 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
       if (!a.fail) a.fail = static_cast<uint8_t*>(mc->c_fail.p);  // per-shot verdicts the OSD stage revises
     }
     SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch,
-                              mc->tail, mc->m2s);
+                              mc->tail, mc->m2s, mc->fb);
     QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, st, a));
     if (bposd) {
       unsigned int nc[4] = {0, 0, 0, 0};

@@ -74,6 +74,7 @@ struct qldpc_bp {
   int ea_shift = 0;  // engine 3: 2 = dword-scaled LDS addresses in the edge words (images > 64 KiB)
   int tail = 0;      // engine 3: 1 = rows of nch chunks + one tail slot per row (bp_reg.h eng_tail)
   int m2s = 0;       // engine 3: 1 = one-word check state, m2 in the argmin slot (bp_reg.h eng_m2s)
+  int fb = 0;        // engine 3: 1 = byte F words (fp32 space-time family, 512 threads; bp_reg.h eng_fb)
   // engine 5 (product-sum, bp_ps.hip): CSR / CSC on the device, optional HBM message workspace
   qldpc_rt::DevBuf ps_rp, ps_ci, ps_cp, ps_ce, ps_ws;
   long long ps_grid = 0;
@@ -92,7 +93,7 @@ struct qldpc_mc {
   int d3k = 0;  // engine 3: compile-time degree-3 slot count of the kernel (min over sectors)
   int nch = 0;  // 16-byte chunks per check row when both sectors agree (else 0)
   int ea_shift = 0;
-  int tail = 0, m2s = 0;  // engine 3 layout flags shared by both sectors (m2s family only)
+  int tail = 0, m2s = 0, fb = 0;  // engine 3 layout flags shared by both sectors
   // staged pipeline (staged.hip): product-sum decoders, or QLDPC_MC_STAGED=1
   bool staged = false;
   long long sbatch = 0;

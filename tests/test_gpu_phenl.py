@@ -98,7 +98,10 @@ def test_phenl_n1225_space_time_graph(gpu, oracle):
     code = codes.get_code("hgp_34_n1225_q3")
     p = 0.01
     ph = _phenl(code, p, p, 3, precision=32)
-    assert ph.decoders[0].geometry()["engine"] == 3  # register engine with dword-scaled LDS addresses
+    g = ph.decoders[0].geometry()
+    # register engine, tail layout with byte F words: two 512-thread decodes per CU (engine id 21013)
+    assert (g["engine"], g["kernel_id"], g["threads"], g["vars_per_thread"]) == (3, 21013, 512, 11), g
+    assert g["blocks_per_cu"] == 2 and 2 * g["lds_bytes"] <= 160 * 1024, g
     S, R = 96, 3
     res = ph.run(p / 2, p / 2, p / 2, p, 11, 0, S, R, per_shot=True)
     ref = oracle.phenl_run(code, p / 2, p / 2, p / 2, p, 11, 0, S, R, 3, "Total", p_data=p, p_synd=p,
@@ -185,3 +188,35 @@ def test_firstmin_decoder_matches_reference_fixture(gpu):
     out = fm.decode_batch(g["firstmin_synd"])
     assert np.array_equal(out.astype(np.uint8), g["firstmin_corr"])
     assert np.array_equal(fm.decode(g["firstmin_synd"][3]).astype(np.uint8), g["firstmin_corr"][3])
+
+
+@pytest.mark.parametrize("p", [0.01, 0.06])
+def test_st_fp32_byte_f_family_decode_matches_oracle(gpu, oracle, p):
+    """The fp32 space-time decoder of config 5 on the byte-F family (512 threads x 11 variables,
+    2 decodes per CU) against the oracle's float32 restatement and the 1024-thread family
+    (QLDPC_E3_FB=0), on syndromes of i.i.d. errors (p = 0.06: every decode runs to max_iter)."""
+    import os
+
+    from qldpc_fault_tolerance_amd.engine import DeviceBP
+
+    code = codes.get_code("hgp_34_n1225_q3")
+    H = codes.space_time_csr(code.hz, 3)
+    n, m = H.n, H.m
+    pr = np.full(n, p)
+    mi = int(code.N / 10)
+    rng = np.random.default_rng(int(p * 1000))
+    e = (rng.random((160, n)) < p).astype(np.uint8)
+    synd = H.matvec(e).astype(np.uint8)
+    dec = DeviceBP(H, pr, max_iter=mi, precision=32)
+    assert dec.geometry()["kernel_id"] == 21013
+    c, i, v = dec.decode_batch(synd)
+    oc, oi, ov = oracle.bp_decode_batch(H, pr, mi, "minimum_sum", 0.625, synd, 32)
+    assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64))
+    os.environ["QLDPC_E3_FB"] = "0"
+    try:
+        d1 = DeviceBP(H, pr, max_iter=mi, precision=32)
+    finally:
+        del os.environ["QLDPC_E3_FB"]
+    assert d1.geometry()["kernel_id"] == 1013
+    c1, i1, v1 = d1.decode_batch(synd)
+    assert np.array_equal(c, c1) and np.array_equal(i, i1) and np.array_equal(v, v1)
