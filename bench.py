@@ -91,7 +91,11 @@ def cpu_baseline(code, eval_p, max_iter, logical, budget_s):
     dt = time.perf_counter() - t0
     return {"value": S2 / dt, "unit": "shots/s", "cores": cores, "kind": "port",
             "sample": f"{S2} shots of the same workload (shots 0..{S2 - 1}, same seed), oracle/qldpc_oracle.c "
-                      f"fp64 with {cores} OpenMP threads, {dt:.1f} s; LER={r['failures'] / S2:.4g}"}
+                      f"fp64 with {cores} OpenMP threads, {dt:.1f} s; LER={r['failures'] / S2:.4g}",
+            "note": "ORACLE PORT, not the reference: the reference's own CPU path (Python + the third-party ldpc "
+                    "package, absent from this image and not installable offline) cannot run here; this is this "
+                    "repository's C restatement of ldpc 0.1.x min-sum + the _single_run shot loop, compiled with "
+                    "gcc -O3 and OpenMP (SURVEY.md 8d)"}
 
 
 def kernel_name(dec):

@@ -923,9 +923,11 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         !use_f64x(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift) && !bp->tail)
       bp->d3k = 0;
     std::vector<int> lab;
-    // fp64 (measured +3 % with the bank-aware fp64 v2c placement); fp32 gathers of the
-    // structured codes are already near conflict-free (QLDPC_LABEL=1 forces it on)
-    if (bp->engine == 3 && env_int("QLDPC_LABEL", precision == 64 ? 1 : 0) != 0) {
+    // fp64 two-word families (measured +3 % with the bank-aware fp64 v2c placement); fp32 gathers of
+    // the structured codes are already near conflict-free, and the m2s family runs 2.5 % faster on
+    // the identity labels (1.188 M vs 1.159 M shots/s, profiles/r03/m2s_ab/ab_label.txt): off there
+    // (QLDPC_LABEL=1 forces it on)
+    if (bp->engine == 3 && env_int("QLDPC_LABEL", precision == 64 && !bp->m2s ? 1 : 0) != 0) {
       lab = label_checks(g, bp->slot_var, bp->TB, bp->VPL, DM, tsize, &bp->gather_conf[0], &bp->gather_conf[1], bp->m2s);
       std::vector<int32_t> inv(g->m);
       for (int i = 0; i < g->m; ++i) inv[lab[i]] = i;
