@@ -10,6 +10,10 @@
 //   V [E][64]   v2c, canonical bits (sign := v2c <= 0), row-major edge order
 //   C [E][64]   c2v, column-major edge order (rows ascending per column)
 //   X [n][64]   decisions (u8); syndromes are read straight from the [B][m] input
+//               (graphs of n + m <= 2048: the decisions are instead one ballot word per variable
+//               in the wave's LDS, xs [n] u64, and the syndromes one ballot word per check,
+//               sw [m] u64, filled once per shot when a lane takes it: no decision traffic to
+//               HBM, and no per-iteration re-read of scattered syndrome lines)
 // One flooding iteration = a check sweep (rows: read V, min / second min /
 // parity, write every edge's c2v = (-1)^sgn alpha min_{others}|v2c| into C at
 // its column-major position; the H x == s test of the previous iteration's
@@ -75,14 +79,14 @@ __device__ inline typename FT<T>::U hcanon(T v) {
 template <typename T>
 struct HRow {
   typename FT<T>::U v[kHRow];
-  uint8_t x[kHRow];
+  uint32_t x[kHRow];  // decision byte, or (LDS ballot words) the 32-lane half word holding it
   int e0, d;
 };
 
 // The edge tables come in as separate __restrict__ kernel arguments: never written by the
 // kernel, so the backend may read them with scalar loads (uniform addresses) instead of one
 // vector load per lane.
-template <typename T>
+template <typename T, bool XL>
 __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32_t* __restrict__ rp,
                                                          const int32_t* __restrict__ rcol,
                                                          const int32_t* __restrict__ rcpos,
@@ -97,6 +101,17 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
   U* __restrict__ V = reinterpret_cast<U*>(wb) + lane;
   U* __restrict__ C = reinterpret_cast<U*>(wb) + (size_t)A.E * 64 + lane;
   uint8_t* __restrict__ X = reinterpret_cast<uint8_t*>(reinterpret_cast<U*>(wb) + (size_t)2 * A.E * 64) + lane;
+  // xlds: bit `lane` of xs[j] = this lane's decision on variable j (one u64 per variable and wave,
+  // written by the variable sweep's ballot, read back as a broadcast LDS word)
+  extern __shared__ unsigned long long hx_lds[];
+  unsigned long long* xs = hx_lds + (size_t)(threadIdx.x >> 6) * (size_t)A.n;
+  // per-lane 32-bit view: word 2j + (lane >> 5), bit lane & 31 (32-bit loads keep the prefetched
+  // rows at one VGPR per edge)
+  const uint32_t* xs32 = reinterpret_cast<const uint32_t*>(xs) + (lane >> 5);
+  unsigned long long* sw = hx_lds + (size_t)(blockDim.x >> 6) * (size_t)A.n + (size_t)(threadIdx.x >> 6) * (size_t)A.m;
+  const uint32_t* sw32 = reinterpret_cast<const uint32_t*>(sw) + (lane >> 5);
+  const uint32_t xsh = XL ? (uint32_t)(lane & 31) : 0u;
+  constexpr bool xl = XL;
   const T* __restrict__ L = static_cast<const T*>(llr);
   const int m = A.m, n = A.n;
   const bool adaptive = A.alpha == 0.0;
@@ -126,6 +141,28 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
     }
     const bool active = shot >= 0;
     if (!__any(active)) break;
+    if constexpr (XL) {
+      // syndrome bits of the lanes that just took a shot into the wave's ballot words (once per
+      // shot; 32 byte loads in flight per lane)
+      const bool fresh = need && active;
+      const unsigned long long fb = __ballot(fresh);
+      if (fb) {
+        const uint8_t* sr = A.synd + (fresh ? shot : 0) * (long long)m;
+        for (int i0 = 0; i0 < m; i0 += 32) {
+          uint32_t b[32];
+#pragma unroll
+          for (int u = 0; u < 32; ++u) b[u] = (fresh && i0 + u < m) ? (uint32_t)(sr[i0 + u] & 1u) : 0u;
+#pragma unroll
+          for (int u = 0; u < 32; ++u) {
+            if (i0 + u < m) {
+              const unsigned long long w = __ballot(b[u] != 0);
+              if (lane == 0) sw[i0 + u] = (sw[i0 + u] & ~fb) | w;
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      }
+    }
     const uint8_t* srow = A.synd + (active ? shot : 0) * (long long)m;
     const bool first = it == 0;
     // ---------------------------------------- check sweep (+ the H x == s test of iteration it)
@@ -149,7 +186,7 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
               r.x[k] = 0;
             } else {
               r.v[k] = V[(size_t)(r.e0 + k) * 64];
-              r.x[k] = X[(size_t)jv[k] * 64];
+              r.x[k] = xl ? xs32[2 * jv[k]] : (uint32_t)X[(size_t)jv[k] * 64];
             }
           }
         }
@@ -167,7 +204,7 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
       int rq[kHRow];
 #pragma unroll
       for (int k = 0; k < kHRow; ++k) rq[k] = rqp[k];
-      const uint32_t s = active ? (srow[i] & 1u) : 0u;
+      const uint32_t s = !active ? 0u : XL ? (sw32[2 * i] >> xsh) & 1u : (srow[i] & 1u);
       uint32_t hx = 0;
       U m1 = FT<T>::kSent, m2 = FT<T>::kSent, px = s ? kS : (U)0;
 #pragma unroll
@@ -181,7 +218,7 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
           px ^= cur.v[k];
         }
       }
-      mism |= (hx ^ s) & 1u;
+      mism |= ((hx >> xsh) ^ s) & 1u;
       const U b1 = FT<T>::bits(FT<T>::val(m1) * alpha), b2 = FT<T>::bits(FT<T>::val(m2) * alpha);
 #pragma unroll
       for (int k = 0; k < kHRow; ++k) {
@@ -207,7 +244,8 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
     }
     if (__any(fin)) {
       if (fin) {
-        for (int j = 0; j < n; ++j) A.corr[shot * (long long)n + j] = X[(size_t)j * 64];
+        for (int j = 0; j < n; ++j)
+          A.corr[shot * (long long)n + j] = xl ? (uint8_t)((xs32[2 * j] >> xsh) & 1u) : X[(size_t)j * 64];
         if (A.iters) A.iters[shot] = conv ? it : A.max_iter;
         if (A.conv) A.conv[shot] = (uint8_t)conv;
         shot = -1;
@@ -253,8 +291,12 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
           acc = acc + c[t];
         }
       }
+      if (xl) {
+        const unsigned long long w = __ballot(run && acc <= (T)0);
+        if (lane == 0) xs[j] = w;
+      }
       if (run) {
-        X[(size_t)j * 64] = acc <= (T)0 ? 1 : 0;
+        if (!xl) X[(size_t)j * 64] = acc <= (T)0 ? 1 : 0;
         // backward sums: v2c_t = f_t + ((c_last + ...) + c_{t+1}); the redundant `0 + c`
         // and `f + 0` of ldpc's loop change at most the sign of a zero (erased by hcanon)
         T b = (T)0;
@@ -269,6 +311,10 @@ __global__ void __launch_bounds__(kHThreads, 2) hdec_kernel(HArgs A, const int32
       }
     }
     if (run) ++it;
+    // the ballot words written by lane 0 are read by every lane of the wave in the next check
+    // sweep: LDS operations of a wave complete in order; this keeps the compiler from moving
+    // those reads above the writes
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
 }
 
@@ -314,15 +360,21 @@ int hbm_prepare(qldpc_bp* bp) {
   return 0;
 }
 
+// decisions and syndromes in LDS when 4 waves x (n + m) x 8 B leave room for 2 workgroups per CU
+bool hbm_xlds(const qldpc_bp* bp) {
+  const char* e = std::getenv("QLDPC_HBM_XLDS");
+  return bp->g->n + bp->g->m <= 2048 && !(e && *e && std::atoi(e) == 0);
+}
+
 size_t hbm_wave_bytes(const qldpc_bp* bp) {
   const size_t tsize = bp->precision == 32 ? 4 : 8;
-  const size_t b = (size_t)2 * bp->g->nnz * 64 * tsize + (size_t)bp->g->n * 64;
+  const size_t b = (size_t)2 * bp->g->nnz * 64 * tsize + (hbm_xlds(bp) ? 0 : (size_t)bp->g->n * 64);
   return (b + 255) & ~(size_t)255;
 }
 
 const void* hbm_kernel(int precision) {
-  return precision == 32 ? reinterpret_cast<const void*>(&hdec_kernel<float>)
-                         : reinterpret_cast<const void*>(&hdec_kernel<double>);
+  return precision == 32 ? reinterpret_cast<const void*>(&hdec_kernel<float, false>)
+                         : reinterpret_cast<const void*>(&hdec_kernel<double, false>);
 }
 
 int hbm_decode_launch(qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int32_t* iters, uint8_t* conv, int64_t B,
@@ -364,13 +416,17 @@ int hbm_decode_launch(qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int32_t*
   a.E = bp->g->nnz;
   a.max_iter = bp->max_iter;
   a.alpha = bp->alpha;
+  const bool xl = hbm_xlds(bp);
+  const size_t shm = xl ? (size_t)wpb * (bp->g->n + bp->g->m) * 8 : 0;
   QLDPC_HIP(hipMemsetAsync(bp->work.p, 0, 4, stream));
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kHThreads), shm, stream, a, a.rp, a.rcol, a.rcpos, a.cp,
+                       a.crpos, a.llr);
+  };
   if (bp->precision == 32)
-    hipLaunchKernelGGL(hdec_kernel<float>, dim3((unsigned)blocks), dim3(kHThreads), 0, stream, a, a.rp, a.rcol, a.rcpos,
-                       a.cp, a.crpos, a.llr);
+    xl ? launch(hdec_kernel<float, true>) : launch(hdec_kernel<float, false>);
   else
-    hipLaunchKernelGGL(hdec_kernel<double>, dim3((unsigned)blocks), dim3(kHThreads), 0, stream, a, a.rp, a.rcol,
-                       a.rcpos, a.cp, a.crpos, a.llr);
+    xl ? launch(hdec_kernel<double, true>) : launch(hdec_kernel<double, false>);
   QLDPC_HIP(hipGetLastError());
   return 0;
 }

@@ -53,6 +53,15 @@
 #ifndef QLDPC_M2S_MBCNT
 #define QLDPC_M2S_MBCNT 0
 #endif
+// c2s family: variables whose c2v reads are issued ahead of the current one's arithmetic
+#ifndef QLDPC_C2S_PF
+#define QLDPC_C2S_PF 2
+#endif
+// c2s check phase: the row's c2v as one 16-byte store per chunk (else 4-byte stores the
+// compiler pairs)
+#ifndef QLDPC_C2S_W128
+#define QLDPC_C2S_W128 1
+#endif
 // m2s family: one uniform prior in SGPRs instead of one per variable slot in VGPRs
 #ifndef QLDPC_M2S_UNIL
 #define QLDPC_M2S_UNIL 1
@@ -82,13 +91,22 @@ constexpr bool eng_m2s(int E) { return (E / 10000) % 10 == 1; }
 // xored into the containing word at the byte's shift): the fp32 space-time tail family for 512-thread
 // workgroups (engine id 21013), whose 79.6 KB image lets 2 decodes share a CU
 constexpr bool eng_fb(int E) { return (E / 10000) % 10 == 2; }
+// + 30000 = "c2v in slot" (fp64 <= 256-thread family with tail rows, engine id 31103): the check
+// phase writes each edge's c2v into the edge's own V slot (alpha * m1 with the edge's sign for
+// every edge, then one ds_xor_b64 turns the argmin edge's word into alpha * m2 with its sign), so
+// the variable phase reads one word per edge and keeps neither a check-state array nor its own
+// previous v2c; the F word addresses of the edges are held in VGPRs instead of the CS addresses.
+// Every row must hold exactly 2 * NCH + 1 edges (no padding slot is overwritten).
+constexpr bool eng_c2s(int E) { return (E / 10000) % 10 == 3; }
+// the one-word / no-word check-state families share the register layout and the shot setup
+constexpr bool eng_m2x(int E) { return eng_m2s(E) || eng_c2s(E); }
 // launch bounds: LB threads per workgroup at most; 256-thread fp64 kernels are
 // built for 2 workgroups per CU (2 waves per SIMD: up to 256 VGPRs, no spills)
 template <typename T, int ENG>
 constexpr int lb_waves(int LB) {
   // engine 4 fp64 images (no CS array) fit 3 workgroups per CU: <= 168 VGPRs
   // (the fp64 512-thread family: 2 workgroups of 8 waves per CU, 128 VGPRs)
-  return LB <= 256 ? (sizeof(T) == 8 ? ((eng_base(ENG) == 4 || eng_m2s(ENG)) ? 3 : 2) : 4)
+  return LB <= 256 ? (sizeof(T) == 8 ? ((eng_base(ENG) == 4 || eng_m2x(ENG)) ? 3 : 2) : 4)
                    : (LB <= 512 && (eng_kv64(ENG) || eng_fb(ENG))) ? 4 : 1;
 }
 __device__ inline unsigned long long qstamp() {
@@ -112,11 +130,11 @@ struct RLayout {
 };
 
 // [CS][V][tail: one slot per row label (tail layouts only)][F][sink][lred]
-// (m2s: CS entries of one message word instead of two)
+// (m2s = 1: CS entries of one message word instead of two; m2s = 2, c2s: no CS array)
 __host__ __device__ inline RLayout r_layout(int eng, int vslots, int mmax, int tsize, int tail = 0, int m2s = 0,
                                             int fb = 0) {
   RLayout L;
-  L.v = eng == 4 ? 0u : (uint32_t)a16((size_t)(mmax + 1) * (m2s ? 1 : 2) * tsize);
+  L.v = eng == 4 ? 0u : (uint32_t)a16((size_t)(mmax + 1) * (m2s == 2 ? 0 : m2s ? 1 : 2) * tsize);
   L.t = L.v + (uint32_t)a16((size_t)vslots * tsize);
   L.f = L.t + (tail ? (uint32_t)a16((size_t)mmax * tsize) : 0u);
   L.sink = L.f + (uint32_t)a16((size_t)(mmax + 1) * (fb ? 1 : 4));
@@ -187,6 +205,10 @@ __device__ inline void lds_st(unsigned char* smem, uint32_t a, X v) {
     lds_at<X>(smem, a) = v;
   }
 }
+// LDS atomic xor (no return) at an absolute address
+__device__ inline void lds_xor_abs(uint32_t a, uint32_t v) {
+  __hip_atomic_fetch_xor((LdsPtr<uint32_t>)(uintptr_t)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // canonical bits: |v| with the sign bit := (v <= 0).  Only +0 differs from the
 // raw bits (-0 and negatives already carry the sign bit; NaN never occurs).
@@ -253,14 +275,15 @@ __device__ inline uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
 template <typename T, int DMAX, int VPL, int ENG = 3>
 struct RState {
   using U = typename FT<T>::U;
-  static constexpr bool kKeepV = eng_base(ENG) == 3 && (sizeof(T) == 4 || eng_kv64(ENG));  // own v2c in VGPRs
+  static constexpr bool kKeepV =
+      eng_base(ENG) == 3 && (sizeof(T) == 4 || eng_kv64(ENG)) && !eng_c2s(ENG);  // own v2c in VGPRs
   // the fp64 <= 256-thread family (256-VGPR budget) keeps the two addresses of an edge
   // unpacked and absolute (ea = CS address, ev = V slot address): no unpack / base add
   // per access, 2 VALU per edge and iteration fewer
   static constexpr bool kSplit = (ENG / 100) % 10 == 1 && sizeof(T) == 8;  // engine id 103 (not 303)
   // m2s with QLDPC_M2S_UNIL: one prior for every variable (uniform channel_probs, host-checked),
   // loaded by a scalar load: 2 SGPRs instead of 2 * VPL VGPRs
-  static constexpr bool kUniL = eng_m2s(ENG) && QLDPC_M2S_UNIL;
+  static constexpr bool kUniL = eng_m2x(ENG) && QLDPC_M2S_UNIL;
   uint32_t ea[VPL][DMAX];
   uint32_t ev[kSplit ? VPL : 1][kSplit ? DMAX : 1];
   T L[kUniL ? 1 : VPL];
@@ -295,7 +318,8 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
       if (eng_base(ENG) == 4) {
         R.ea[k][t] = e == kNoEdgeS ? (Ly.v | (Ly.sink << 16)) : (va | (va << 16));
       } else if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) {
-        R.ea[k][t] = sbase + echk(e) * (uint32_t)((eng_m2s(ENG) ? 1 : 2) * sizeof(T));
+        // c2s: the absolute address of the edge's F word (entry = check label + 1)
+        R.ea[k][t] = eng_c2s(ENG) ? sbase + Ly.f + 4u * echk(e) : sbase + echk(e) * (uint32_t)((eng_m2s(ENG) ? 1 : 2) * sizeof(T));
         R.ev[k][t] = sbase + va;
       } else {
         R.ea[k][t] = ((echk(e) * (uint32_t)(2 * sizeof(T))) >> eng_sh(ENG)) | ((va >> eng_sh(ENG)) << 16);
@@ -375,7 +399,7 @@ __device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
   for (int k = 0; k < VPL; ++k)
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
-      if ((eng_m2s(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;
+      if ((eng_m2x(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;
       asm volatile("" : "+v"(R.ea[k][t]));
       if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) asm volatile("" : "+v"(R.ev[k][t]));
     }
@@ -803,7 +827,7 @@ __device__ inline void m_gather(const RState<T, DMAX, VPL, ENG>& R, int k, typen
   using U = typename FT<T>::U;
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
-    an[t] = lds_ld<U, true>(nullptr, R.ea[k][t]);
+    if constexpr (!eng_c2s(ENG)) an[t] = lds_ld<U, true>(nullptr, R.ea[k][t]);  // (c2s: ea = F word)
     vn[t] = lds_ld<U, true>(nullptr, R.ev[k][t]);
   }
 }
@@ -814,12 +838,18 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
                                  const typename FT<T>::U (&vn)[DMAX], uint32_t fdelta, T alpha, bool xprev,
                                  double* post, const int32_t* perm) {
   using U = typename FT<T>::U;
-  static_assert(sizeof(T) == 8 && RState<T, DMAX, VPL, ENG>::kSplit && RState<T, DMAX, VPL, ENG>::kKeepV,
-                "m2s: fp64 split-address family only");
+  constexpr bool KV1 = RState<T, DMAX, VPL, ENG>::kKeepV;
+  static_assert(sizeof(T) == 8 && RState<T, DMAX, VPL, ENG>::kSplit &&
+                    (RState<T, DMAX, VPL, ENG>::kKeepV || eng_c2s(ENG)),
+                "m2s / c2s: fp64 split-address family only");
   T c[ND];
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
-    const U o = R.ov[k][t];
+    if constexpr (eng_c2s(ENG)) {  // the slot holds this edge's c2v (c2s_check)
+      c[t] = FT<T>::val(vn[t]);
+      continue;
+    }
+    const U o = R.ov[KV1 ? k : 0][KV1 ? t : 0];
     // argmin edge <=> its slot no longer holds our own previous v2c: m2 | parity, else m1 | parity
     const U sel = vn[t] != o ? vn[t] : an[t];
     // sign(sel) = parity; sel * alpha is exactly +-(|sel| * alpha) (IEEE rounding is sign-symmetric),
@@ -855,11 +885,16 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
     lds_st<U, true>(nullptr, R.ev[k][t], nv[t]);
-    R.ov[k][t] = nv[t];
+    if constexpr (KV1) R.ov[k][t] = nv[t];
   }
   if (x != xprev) {
 #pragma unroll
-    for (int t = 0; t < ND; ++t) atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), 1u);
+    for (int t = 0; t < ND; ++t) {
+      if constexpr (eng_c2s(ENG))
+        lds_xor_abs(R.ea[k][t], 1u);
+      else
+        atomicXor(&lds_at<uint32_t>(smem, r_fa(R, k, t, fdelta)), 1u);
+    }
   }
   return x;
 }
@@ -871,7 +906,8 @@ __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   constexpr int N3 = DMAX > 3 ? 3 : DMAX;
   // gathers one variable ahead: two ahead needs 32 more VGPRs than the 168 of 3 workgroups per
   // CU and spills (n1600: 849k vs 1.13M shots/s, profiles/r03/m2s_ab/)
-  constexpr int PF0 = QLDPC_PF >= 1 ? QLDPC_PF : 1;
+  // c2s keeps no own v2c (48 VGPRs fewer): QLDPC_C2S_PF variables ahead
+  constexpr int PF0 = eng_c2s(ENG) ? QLDPC_C2S_PF : QLDPC_PF >= 1 ? QLDPC_PF : 1;
   constexpr int PF = PF0 < VPL ? PF0 : VPL;
   r_launder<T, DMAX, VPL, ENG, D3K>(R);
   uint32_t xbits = 0;
@@ -983,6 +1019,109 @@ __device__ inline int m_check(unsigned char* smem, const RLayout& Ly, int m, int
     const U par = (U)(px & 0x80000000u) << 32;
     lds_at<U>(smem, (uint32_t)(i + 1) * (uint32_t)sizeof(T)) = FT<T>::bits(f1) | par;
     lds_at<U>(smem, amin) = FT<T>::bits(f2) | par;
+  }
+  return mism;
+}
+
+// c2s check phase (rows of exactly 2 * NCH + TAIL edges; fp64): min / second min / parity / argmin
+// as m_check, then the c2v of the NEXT variable phase into the row's own slots: every edge gets
+// alpha * m1 with sign parity ^ own sign, written as {lo(a1), hi(a1) ^ parity ^ (own hi & sign)}
+// (one v_bitop3 per edge, the low word shared), and one ds_xor_b64 of bits(a1) ^ bits(a2) turns the
+// argmin's word into alpha * m2 with the same sign.  alpha * m with the sign applied afterwards is
+// bit-identical to ldpc's (+-m) * alpha (IEEE rounding is sign-symmetric); with a tie m1 == m2 and
+// the xor is zero.
+template <typename T, bool FIRST, int NCH, int TAIL>
+__device__ inline int c2s_check(unsigned char* smem, const RLayout& Ly, int m, int wtid, int TB, uint32_t& sbits,
+                                T alpha) {
+  using U = typename FT<T>::U;
+  using VT = typename V16<T>::type;
+  constexpr int NV = V16<T>::N;
+  static_assert(sizeof(T) == 8, "c2s: fp64 only");
+  int mism = 0;
+  int q = 0;
+  int tid = wtid;  // opaque: the row offsets are re-derived per pass (as m_check)
+  asm volatile("" : "+v"(tid));
+  const uint32_t rstride = (uint32_t)NCH * 16u;
+  for (int i = tid; i < m; i += TB, ++q) {
+    const uint32_t roff = Ly.v + 16u + (uint32_t)i * rstride;
+    VT cur[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) cur[c] = *reinterpret_cast<const VT*>(smem + roff + 16u * (uint32_t)c);
+    const uint32_t toff = Ly.t + (uint32_t)i * (uint32_t)sizeof(T);
+    T tcur = (T)0;
+    if (TAIL) tcur = lds_at<T>(smem, toff);
+    const uint32_t fcur = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
+    uint32_t s;
+    if (FIRST) {
+      s = ((fcur >> 1) ^ (fcur >> 2)) & 1u;
+      sbits |= s << q;
+      lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1)) = (fcur & 4u) | ((fcur >> 2) & 1u);
+    } else {
+      s = (sbits >> q) & 1u;
+      mism |= (int)((fcur ^ s) & 1u);
+    }
+    double f1 = FT<T>::val(FT<T>::kSent), f2 = f1;
+    uint32_t px = s ? 0x80000000u : 0u;
+    uint32_t amin = roff;  // argmin slot (byte offset)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const double x = V16<T>::get(cur[c], k);
+        amin = __builtin_fabs(x) < f1 ? roff + 16u * (uint32_t)c + 8u * (uint32_t)k : amin;
+        double t;
+        asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x));
+        asm("v_min_f64 %0, %1, %2" : "=v"(f2) : "v"(f2), "v"(t));
+        asm("v_min_f64 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
+      }
+      uint32_t p;
+      asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96"
+          : "=v"(p)
+          : "v"(px), "v"((uint32_t)(FT<T>::bits(cur[c].x) >> 32)), "v"((uint32_t)(FT<T>::bits(cur[c].y) >> 32)));
+      px = p;
+    }
+    if (TAIL) {
+      const double x = (double)tcur;
+      amin = __builtin_fabs(x) < f1 ? toff : amin;
+      double t;
+      asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x));
+      asm("v_min_f64 %0, %1, %2" : "=v"(f2) : "v"(f2), "v"(t));
+      asm("v_min_f64 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
+      px ^= (uint32_t)(FT<T>::bits(tcur) >> 32);
+    }
+    const U a1 = FT<T>::bits(f1 * alpha);
+    const U a2 = FT<T>::bits(f2 * alpha);
+    const uint32_t lo = (uint32_t)a1;
+    const uint32_t ah = (uint32_t)(a1 >> 32) ^ (px & 0x80000000u);
+    auto hiw = [&](double x) {
+      uint32_t hi;
+      asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c"
+          : "=v"(hi)
+          : "v"((uint32_t)(FT<T>::bits(x) >> 32)), "v"(ah), "v"(0x80000000u));
+      return hi;
+    };
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const uint32_t off = roff + 16u * (uint32_t)c;
+      if (QLDPC_C2S_W128) {  // one 16-byte store per chunk (conflict-free at the 48-byte row stride)
+        typename LdsWord<16>::type w;
+        w.x = lo;
+        w.y = hiw(cur[c].x);
+        w.z = lo;
+        w.w = hiw(cur[c].y);
+        *reinterpret_cast<typename LdsWord<16>::type*>(smem + off) = w;
+      } else {
+        lds_at<uint32_t>(smem, off) = lo;
+        lds_at<uint32_t>(smem, off + 4u) = hiw(cur[c].x);
+        lds_at<uint32_t>(smem, off + 8u) = lo;
+        lds_at<uint32_t>(smem, off + 12u) = hiw(cur[c].y);
+      }
+    }
+    if (TAIL) {
+      lds_at<uint32_t>(smem, toff) = lo;
+      lds_at<uint32_t>(smem, toff + 4u) = hiw((double)tcur);
+    }
+    atomicXor(reinterpret_cast<unsigned long long*>(&lds_at<U>(smem, amin)), (unsigned long long)(a1 ^ a2));
   }
   return mism;
 }
@@ -1200,7 +1339,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         const U cl = FT<T>::bits(r_prior(R, k));  // w domain: the prior as is
 #pragma unroll
         for (int t = 0; t < DMAX; ++t) {
-          if ((eng_m2s(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;  // (no dummy 4th edge kept)
+          if ((eng_m2x(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;  // (no dummy 4th edge kept)
           lds_st<U, SP>(smem, r_va(R, k, t), cl);
           if (KV) R.ov[KV ? k : 0][KV ? t : 0] = cl;
         }
@@ -1232,9 +1371,11 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
             if (e) {
 #pragma unroll
               for (int t = 0; t < DMAX; ++t) {
-                if ((eng_m2s(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;
+                if ((eng_m2x(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;
                 if constexpr (eng_base(ENG) == 4)
                   atomicXor(&lds_at<uint32_t>(smem, f_addr<T, ENG>(R.ea[k][t], M)), 2u);
+                else if constexpr (eng_c2s(ENG))
+                  lds_xor_abs(R.ea[k][t], 2u);
                 else
                   f_xor<ENG>(smem, r_fa(R, k, t, M.fbase), 2u);
               }
@@ -1290,6 +1431,8 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     // ---------------------------------------------------------- first check pass (CS / c2v from priors)
     if constexpr (eng_base(ENG) == 4)
       c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
+    else if constexpr (eng_c2s(ENG))
+      c2s_check<T, true, NCH, eng_tail(ENG)>(smem, Ly, m, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     else if constexpr (eng_m2s(ENG))
       m_check<T, true, NCH, eng_tail(ENG)>(smem, Ly, m, wbase, tid, TB, sb);
     else if constexpr (NCH > 0)
@@ -1330,9 +1473,9 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       } else {
         const T alpha = adaptive ? (T)(1.0 - ldexp(1.0, -it)) : alpha_fixed;
         // (the 1024-thread tail family runs one workgroup per CU: nothing to take priority over)
-        constexpr int kPV = (eng_tail(ENG) && !eng_m2s(ENG) && !eng_fb(ENG)) ? 0 : QLDPC_PRIO_V;
+        constexpr int kPV = (eng_tail(ENG) && !eng_m2x(ENG) && !eng_fb(ENG)) ? 0 : QLDPC_PRIO_V;
         if (kPV) __builtin_amdgcn_s_setprio(kPV);
-        if constexpr (eng_m2s(ENG))
+        if constexpr (eng_m2x(ENG))
           xb = m_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
         else
           xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
@@ -1350,7 +1493,9 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         // check state for iteration it + 1 (float: pre-scaled by its alpha)
         const T alpha_next = adaptive ? (T)(1.0 - ldexp(1.0, -(it + 1))) : alpha_fixed;
         if (QLDPC_PRIO_C) __builtin_amdgcn_s_setprio(QLDPC_PRIO_C);
-        if constexpr (eng_m2s(ENG))
+        if constexpr (eng_c2s(ENG))
+          mism = c2s_check<T, false, NCH, eng_tail(ENG)>(smem, Ly, m, tid, TB, sb, alpha_next);
+        else if constexpr (eng_m2s(ENG))
           mism = m_check<T, false, NCH, eng_tail(ENG)>(smem, Ly, m, wbase, tid, TB, sb);
         else if constexpr (NCH > 0)
           mism = r_check_c<T, false, NCH, eng_tail(ENG), QLDPC_PFC, ENG>(smem, Ly, m, tid, TB, sb);
@@ -1457,7 +1602,7 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rmc_kernel(SMcArgs
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = A.chunk;
   const int fw = (CH + 31) / 32;
-  const RLayout Ly = r_layout(eng_base(ENG), A.vslots, A.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG), eng_fb(ENG));
+  const RLayout Ly = r_layout(eng_base(ENG), A.vslots, A.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG) ? 1 : eng_c2s(ENG) ? 2 : 0, eng_fb(ENG));
   uint32_t* fm0 = reinterpret_cast<uint32_t*>(smem + Ly.total);
   uint32_t* fm1 = fm0 + ((fw + 3) & ~3);
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(fm1 + ((fw + 3) & ~3));
@@ -1514,7 +1659,7 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rdec_kernel(SDecAr
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int CH = D.chunk;
-  const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG), eng_fb(ENG));
+  const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG) ? 1 : eng_c2s(ENG) ? 2 : 0, eng_fb(ENG));
   const long long nchunks = (D.B + CH - 1) / CH;
   __shared__ long long s_next;
   long long ch = blockIdx.x;

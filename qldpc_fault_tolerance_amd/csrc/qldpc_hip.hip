@@ -108,7 +108,8 @@ SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int 
   // fp64 m2-in-slot family (rows of 3 chunks + a tail slot, <= 256 threads, 3 workgroups per CU)
   if (m2s) {
     const bool ok = engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && nch == 3 && tail && tb <= 256;
-    return ok ? get_rvariant_f64_m2s(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
+    if (!ok) return SVariant{nullptr, nullptr, nullptr, nullptr};
+    return m2s == 2 ? get_rvariant_f64_c2s(vpl, d3k) : get_rvariant_f64_m2s(vpl, d3k);
   }
   // fp64 tail layout (rows of 4 chunks + a tail slot, dword-scaled addresses, 1024 threads)
   if (tail) {
@@ -850,6 +851,15 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         bp->m2s = 1;
         bp->nch = 3;
         bp->ea_shift = 0;
+        // "c2v in slot" (bp_reg.h eng_c2s, kern_r_f64_c2s.hip, opt-in QLDPC_C2S=1): the check phase
+        // writes the c2v of every edge into the row's slots, so no row may have a padding slot:
+        // every row exactly 7 edges (the headline HGP graphs).  No CS array (n1600 52.3 -> 46.2 KB)
+        // and 25 % fewer VALU, but its check phase stores 7 words per row where m2s stores 2, and
+        // LDS stores cost 3x the cycles of reads per byte: 1.141 M vs 1.189 M shots/s
+        // (profiles/r03/c2s/), so m2s stays the default
+        bool full = true;
+        for (int i = 0; i < g->m && full; ++i) full = g->row_ptr[i + 1] - g->row_ptr[i] == 7;
+        if (full && env_int("QLDPC_C2S", 0) != 0 && r_fits(3, (1 + g->m * 3) * 2, g->m, 8, 0, 1, 2)) bp->m2s = 2;
       }
     }
     const int vslots_e3 = (1 + g->m * bp->nch) * (16 / tsize);
@@ -1004,7 +1014,7 @@ int qldpc_bp_kernel_id(const qldpc_bp* bp, int32_t* kernel_id, int32_t* row_chun
   int id = bp->engine;
   if (bp->engine == 3) {
     if (bp->m2s)
-      id = 11103;
+      id = bp->m2s == 2 ? 31103 : 11103;
     else if (bp->fb)
       id = 21013;
     else if (bp->tail)
@@ -1167,6 +1177,9 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   qldpc_bp* d0 = dec_x ? dec_x : dec_z;
   const bool staged = (dec_x && dec_x->engine >= 5) || (dec_z && dec_z->engine >= 5) ||
                       (dec_x && dec_x->tail && !dec_x->m2s) || (dec_z && dec_z->tail && !dec_z->m2s) ||
+                      // the fused kernel runs one layout family for both sectors
+                      (dec_x && dec_z &&
+                       (dec_x->m2s != dec_z->m2s || dec_x->tail != dec_z->tail || dec_x->fb != dec_z->fb)) ||
                       env_int("QLDPC_MC_STAGED", 0) == 1;
   if (staged) {  // staged pipeline around decode_batch (staged.hip): any decoder pair
     if (dec_x && dec_z && (dec_x->g->n != dec_z->g->n || dec_x->g->device != dec_z->g->device))

@@ -73,7 +73,8 @@ struct qldpc_bp {
   int d3k = 0;
   int ea_shift = 0;  // engine 3: 2 = dword-scaled LDS addresses in the edge words (images > 64 KiB)
   int tail = 0;      // engine 3: 1 = rows of nch chunks + one tail slot per row (bp_reg.h eng_tail)
-  int m2s = 0;       // engine 3: 1 = one-word check state, m2 in the argmin slot (bp_reg.h eng_m2s)
+  int m2s = 0;       // engine 3: 1 = one-word check state, m2 in the argmin slot (bp_reg.h eng_m2s);
+                     // 2 = c2v written into the slots by the check phase (eng_c2s)
   int fb = 0;        // engine 3: 1 = byte F words (fp32 space-time family, 512 threads; bp_reg.h eng_fb)
   // engine 5 (product-sum, bp_ps.hip): CSR / CSC on the device, optional HBM message workspace
   qldpc_rt::DevBuf ps_rp, ps_ci, ps_cp, ps_ce, ps_ws;

@@ -1,11 +1,13 @@
-"""The fp64 "m2 in slot" kernel family (engine id 11103, bp_reg.h eng_m2s) against the oracle.
+"""The fp64 one-slot families against the oracle: "c2v in slot" (engine id 31103, bp_reg.h
+eng_c2s, the default for the headline graphs) and "m2 in slot" (11103, eng_m2s, QLDPC_C2S=0).
 
-The headline graphs (hgp_34_n1600 hz / hx: rows of 7, column degrees 3 / 4 with the degree-3
-variables filling 4 whole slots of 256 lanes) run on it by default in float64: one-word check
-state {m1 | parity}, m2 | parity written by the check phase into the argmin edge's V slot, rows of
-3 chunks + a tail slot, 52.3 KB per image, 3 workgroups per CU.  Bit-exact bar as every other
-engine: corrections, iteration counts and convergence flags identical to the oracle's float64
-restatement of ldpc; also identical to the two-word family (QLDPC_M2S=0) on the same inputs.
+The headline graphs (hgp_34_n1600 hz / hx: rows of exactly 7, column degrees 3 / 4 with the
+degree-3 variables filling 4 whole slots of 256 lanes) run in float64 with rows of 3 chunks + a
+tail slot and 3 workgroups per CU.  c2s: the check phase writes every edge's c2v into the row's
+slots (46.2 KB image, no check-state array); m2s: one-word check state {m1 | parity} and m2 |
+parity in the argmin edge's V slot (52.3 KB).  Bit-exact bar as every other engine: corrections,
+iteration counts and convergence flags identical to the oracle's float64 restatement of ldpc; the
+three families (c2s, m2s, two-word QLDPC_M2S=0) identical on the same inputs.
 """
 import os
 
@@ -23,31 +25,35 @@ def _synd(H, p, B, seed):
     return (e.astype(np.int64) @ H.T.astype(np.int64) % 2).astype(np.uint8)
 
 
-def _dec(H, probs, mi, alpha=0.625, m2s=True, vpl=0):
+def _dec(H, probs, mi, alpha=0.625, m2s=True, vpl=0, c2s=True):
     from qldpc_fault_tolerance_amd.engine import DeviceBP
 
-    old = os.environ.get("QLDPC_M2S")
-    os.environ["QLDPC_M2S"] = "1" if m2s else "0"
+    env = {"QLDPC_M2S": "1" if m2s else "0", "QLDPC_C2S": "1" if c2s else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return DeviceBP(H, probs, max_iter=mi, ms_scaling_factor=alpha, precision=64, vars_per_thread=vpl)
     finally:
-        if old is None:
-            del os.environ["QLDPC_M2S"]
-        else:
-            os.environ["QLDPC_M2S"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
-def test_headline_graphs_select_m2s_family(gpu):
+def test_headline_graphs_select_c2s_family(gpu):
     code = codes.get_code("hgp_34_n1600")
     for H in (code.hz, code.hx):
         g = _dec(H, 0.06, 160).geometry()
-        assert (g["engine"], g["kernel_id"], g["row_chunks"], g["threads"], g["vars_per_thread"]) == (3, 11103, 3, 256, 7), g
+        assert (g["engine"], g["kernel_id"], g["row_chunks"], g["threads"], g["vars_per_thread"]) == (3, 31103, 3, 256, 7), g
         assert g["degree3_slots"] == 4 and g["lds_bytes"] * 3 <= 160 * 1024, g
         assert g["blocks_per_cu"] == 3, g
+        g1 = _dec(H, 0.06, 160, c2s=False).geometry()
+        assert g1["kernel_id"] == 11103 and g1["blocks_per_cu"] == 3 and g1["lds_bytes"] > g["lds_bytes"], (g1, g)
         g0 = _dec(H, 0.06, 160, m2s=False).geometry()
         assert g0["kernel_id"] == 103 and g0["blocks_per_cu"] == 2, g0
     # outside the envelope (mixed-degree slots: n225's 144 degree-3 variables over 64 lanes) -> two-word family
-    assert _dec(codes.get_code("hgp_34_n225").hz, 0.05, 22).geometry()["kernel_id"] != 11103
+    assert _dec(codes.get_code("hgp_34_n225").hz, 0.05, 22).geometry()["kernel_id"] not in (11103, 31103)
 
 
 @pytest.mark.parametrize("sector", ["hz", "hx"])
@@ -61,22 +67,24 @@ def test_m2s_decode_matches_oracle(gpu, oracle, sector, p):
     c, i, v = _dec(H, p, 160).decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, p, 160, "minimum_sum", 0.625, synd, 64)
     assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64))
-    c0, i0, v0 = _dec(H, p, 160, m2s=False).decode_batch(synd)
-    assert np.array_equal(c, c0) and np.array_equal(i, i0) and np.array_equal(v, v0)
+    for kw in ({"c2s": False}, {"m2s": False}):
+        c0, i0, v0 = _dec(H, p, 160, **kw).decode_batch(synd)
+        assert np.array_equal(c, c0) and np.array_equal(i, i0) and np.array_equal(v, v0), kw
 
 
-def test_m2s_adaptive_alpha_and_zero_priors_match_oracle(gpu, oracle):
-    """Adaptive alpha and all-zero priors on the m2s family; non-uniform priors take the two-word
-    family (the m2s kernels keep one prior in SGPRs: QLDPC_M2S_UNIL)."""
+@pytest.mark.parametrize("c2s", [True, False])
+def test_m2s_adaptive_alpha_and_zero_priors_match_oracle(gpu, oracle, c2s):
+    """Adaptive alpha and all-zero priors on the c2s / m2s families; non-uniform priors take the
+    two-word family (both keep one prior in SGPRs: QLDPC_M2S_UNIL)."""
     code = codes.get_code("hgp_34_n1600")
     H = code.hz
     synd = _synd(H, 0.05, 256, seed=5)
-    c, i, v = _dec(H, 0.05, 60, alpha=0.0).decode_batch(synd)
+    c, i, v = _dec(H, 0.05, 60, alpha=0.0, c2s=c2s).decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, 0.05, 60, "minimum_sum", 0.0, synd, 64)
     assert np.array_equal(c, oc.astype(np.int64)) and np.array_equal(i, oi) and np.array_equal(v, ov)
-    # every prior zero (p = 0.5): messages that are exactly +-0 on the one-prior m2s kernels
-    dec = _dec(H, 0.5, 12)
-    assert dec.geometry()["kernel_id"] == 11103
+    # every prior zero (p = 0.5): messages that are exactly +-0 on the one-prior kernels
+    dec = _dec(H, 0.5, 12, c2s=c2s)
+    assert dec.geometry()["kernel_id"] == (31103 if c2s else 11103)
     c, i, v = dec.decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, 0.5, 12, "minimum_sum", 0.625, synd, 64)
     assert np.array_equal(c, oc.astype(np.int64)) and np.array_equal(i, oi) and np.array_equal(v, ov)
@@ -84,20 +92,21 @@ def test_m2s_adaptive_alpha_and_zero_priors_match_oracle(gpu, oracle):
     rng = np.random.default_rng(3)
     probs = np.full(code.N, 0.04)
     probs[rng.random(code.N) < 0.3] = 0.5
-    dec = _dec(H, probs, 40)
+    dec = _dec(H, probs, 40, c2s=c2s)
     assert dec.geometry()["kernel_id"] == 103
     c, i, v = dec.decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, probs, 40, "minimum_sum", 0.625, synd, 64)
     assert np.array_equal(c, oc.astype(np.int64)) and np.array_equal(i, oi) and np.array_equal(v, ov)
 
 
-def test_m2s_fused_mc_matches_oracle_per_shot(gpu, oracle):
+@pytest.mark.parametrize("c2s", [True, False])
+def test_m2s_fused_mc_matches_oracle_per_shot(gpu, oracle, c2s):
     from qldpc_fault_tolerance_amd.engine import DeviceMC
 
     code = codes.get_code("hgp_34_n1600")
     n, p, S = code.N, 0.07, 400
-    dx, dz = _dec(code.hz, p, 160), _dec(code.hx, p, 160, vpl=7)
-    assert dx.geometry()["kernel_id"] == dz.geometry()["kernel_id"] == 11103
+    dx, dz = _dec(code.hz, p, 160, c2s=c2s), _dec(code.hx, p, 160, vpl=7, c2s=c2s)
+    assert dx.geometry()["kernel_id"] == dz.geometry()["kernel_id"] == (31103 if c2s else 11103)
     res = DeviceMC(code, dx, dz).run(p / 2, p / 2, p / 2, 0x51D5EED2, 777, S, "Total", per_shot=True)
     ref = oracle.mc_run(code, p / 2, p / 2, p / 2, seed=0x51D5EED2, shot_begin=777, shot_count=S, logical_mode="Total",
                         max_iter=160, precision=64, per_shot=True)
