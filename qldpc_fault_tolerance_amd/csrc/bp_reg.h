@@ -57,6 +57,14 @@
 #ifndef QLDPC_C2S_PF
 #define QLDPC_C2S_PF 2
 #endif
+// fp32 c2v in 4 VALU per edge (r_var_one); the check phases then store m2 | parity
+#ifndef QLDPC_F32_C2V4
+#define QLDPC_F32_C2V4 1
+#endif
+// dword-scaled packed edge words (space-time families) hold absolute dword indices (SDWA unpack)
+#ifndef QLDPC_ABS_SH2
+#define QLDPC_ABS_SH2 1
+#endif
 // c2s check phase: the row's c2v as one 16-byte store per chunk (else 4-byte stores the
 // compiler pairs)
 #ifndef QLDPC_C2S_W128
@@ -98,6 +106,14 @@ constexpr bool eng_fb(int E) { return (E / 10000) % 10 == 2; }
 // previous v2c; the F word addresses of the edges are held in VGPRs instead of the CS addresses.
 // Every row must hold exactly 2 * NCH + 1 edges (no padding slot is overwritten).
 constexpr bool eng_c2s(int E) { return (E / 10000) % 10 == 3; }
+// + 100000 * D2K (byte-F family): slots k < D2K hold variables of column degree <= 2 (the
+// space-time graphs' measurement variables, host-sorted first): no third edge slot kept
+constexpr int eng_d2k(int E) { return (E / 100000) % 10; }
+// edge slot t of variable slot k is compile-time absent (m2s / c2s / byte-F kernels)
+template <int ENG, int D3K>
+__device__ constexpr bool no_edge(int k, int t) {
+  return (eng_m2s(ENG) || eng_c2s(ENG) || eng_fb(ENG)) && ((k < D3K && t >= 3) || (k < eng_d2k(ENG) && t >= 2));
+}
 // the one-word / no-word check-state families share the register layout and the shot setup
 constexpr bool eng_m2x(int E) { return eng_m2s(E) || eng_c2s(E); }
 // launch bounds: LB threads per workgroup at most; 256-thread fp64 kernels are
@@ -281,6 +297,10 @@ struct RState {
   // unpacked and absolute (ea = CS address, ev = V slot address): no unpack / base add
   // per access, 2 VALU per edge and iteration fewer
   static constexpr bool kSplit = (ENG / 100) % 10 == 1 && sizeof(T) == 8;  // engine id 103 (not 303)
+  // absolute LDS addresses: split words, or (dword-scaled packed words: the space-time families
+  // 13 / 1013 / 21013) absolute dword indices, unpacked by one SDWA shift per access and used
+  // without a base add
+  static constexpr bool kAbs = kSplit || (eng_sh(ENG) == 2 && QLDPC_ABS_SH2);
   // m2s with QLDPC_M2S_UNIL: one prior for every variable (uniform channel_probs, host-checked),
   // loaded by a scalar load: 2 SGPRs instead of 2 * VPL VGPRs
   static constexpr bool kUniL = eng_m2x(ENG) && QLDPC_M2S_UNIL;
@@ -289,11 +309,25 @@ struct RState {
   T L[kUniL ? 1 : VPL];
   U ov[kKeepV ? VPL : 1][kKeepV ? DMAX : 1];
 };
-// CS / V slot address of edge (k, t): absolute when split, else offsets from smem
+// 4 * (16-bit half h of w) in one VALU (SDWA word select feeding the shift)
+template <int H, int SH>
+__device__ inline uint32_t sdwa_shl(uint32_t w) {
+  uint32_t r;
+  if constexpr (H == 0)
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+        : "=v"(r) : "v"(w), "i"(SH));
+  else
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+        : "=v"(r) : "v"(w), "i"(SH));
+  return r;
+}
+// CS / V slot address of edge (k, t): absolute when split or kAbs, else offsets from smem
 template <typename T, int DMAX, int VPL, int ENG>
 __device__ inline uint32_t r_csa(const RState<T, DMAX, VPL, ENG>& R, int k, int t) {
   if constexpr (RState<T, DMAX, VPL, ENG>::kSplit)
     return R.ea[k][t];
+  else if constexpr (RState<T, DMAX, VPL, ENG>::kAbs)
+    return sdwa_shl<0, 2>(R.ea[k][t]);
   else
     return ea_cs<ENG>(R.ea[k][t]);
 }
@@ -301,6 +335,8 @@ template <typename T, int DMAX, int VPL, int ENG>
 __device__ inline uint32_t r_va(const RState<T, DMAX, VPL, ENG>& R, int k, int t) {
   if constexpr (RState<T, DMAX, VPL, ENG>::kSplit)
     return R.ev[k][t];
+  else if constexpr (RState<T, DMAX, VPL, ENG>::kAbs)
+    return sdwa_shl<1, 2>(R.ea[k][t]);
   else
     return ea_v<ENG>(R.ea[k][t]);
 }
@@ -321,6 +357,8 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
         // c2s: the absolute address of the edge's F word (entry = check label + 1)
         R.ea[k][t] = eng_c2s(ENG) ? sbase + Ly.f + 4u * echk(e) : sbase + echk(e) * (uint32_t)((eng_m2s(ENG) ? 1 : 2) * sizeof(T));
         R.ev[k][t] = sbase + va;
+      } else if constexpr (RState<T, DMAX, VPL, ENG>::kAbs) {  // absolute dword indices
+        R.ea[k][t] = ((sbase + echk(e) * (uint32_t)(2 * sizeof(T))) >> 2) | (((sbase + va) >> 2) << 16);
       } else {
         R.ea[k][t] = ((echk(e) * (uint32_t)(2 * sizeof(T))) >> eng_sh(ENG)) | ((va >> eng_sh(ENG)) << 16);
       }
@@ -385,6 +423,13 @@ template <typename T, int DMAX, int VPL, int ENG>
 __device__ inline uint32_t r_fa(const RState<T, DMAX, VPL, ENG>& R, int k, int t, uint32_t fbase) {
   // CS entry (i + 1) of 2 words (fp32: 8 B, fp64: 16 B) or, m2s, one fp64 word (8 B) -> F word i + 1
   // (byte-F kernels: fp32 CS entries of 8 B -> F byte i + 1)
+  if constexpr (RState<T, DMAX, VPL, ENG>::kAbs && !RState<T, DMAX, VPL, ENG>::kSplit) {
+    // absolute dword index w = csa / 4 in the low half: csa >> 3 = w >> 1, csa >> 1 = 2 w, csa >> 2 = w
+    const uint32_t w = R.ea[k][t];
+    if constexpr (eng_fb(ENG)) return __builtin_amdgcn_ubfe(w, 1, 15) + fbase;
+    if constexpr (sizeof(T) == 4) return sdwa_shl<0, 1>(w) + fbase;
+    return (w & 0xFFFFu) + fbase;
+  }
   if constexpr (eng_fb(ENG)) return (r_csa(R, k, t) >> 3) + fbase;
   return (r_csa(R, k, t) >> ((sizeof(T) == 4 || eng_m2s(ENG)) ? 1 : 2)) + fbase;
 }
@@ -399,7 +444,7 @@ __device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
   for (int k = 0; k < VPL; ++k)
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
-      if ((eng_m2x(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;
+      if (no_edge<ENG, D3K>(k, t)) continue;
       asm volatile("" : "+v"(R.ea[k][t]));
       if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) asm volatile("" : "+v"(R.ev[k][t]));
     }
@@ -415,7 +460,7 @@ __device__ inline void r_gather(unsigned char* smem, const RState<T, DMAX, VPL, 
                                 typename CSEntry<T>::type (&pn)[DMAX],
                                 typename FT<T>::U (&on)[DMAX]) {
   constexpr bool KV = RState<T, DMAX, VPL, ENG>::kKeepV;
-  constexpr bool SP = RState<T, DMAX, VPL, ENG>::kSplit;
+  constexpr bool SP = RState<T, DMAX, VPL, ENG>::kAbs;
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
     pn[t] = lds_ld<typename CSEntry<T>::type, SP>(smem, r_csa(R, k, t));
@@ -443,7 +488,23 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     // |d| == 0 is tested with v_cmp_class (+-0 only): one instruction instead of
     // mask + compare (bit patterns of any class, denormals and NaNs included).
     U sel;
-    if constexpr (sizeof(T) == 4) {
+    if constexpr (sizeof(T) == 4 && QLDPC_F32_C2V4) {
+      // 4 VALU: |own| == |m1| by v_cmp_eq_f32 on the absolute values (the magnitude-bits test of
+      // the class form: denormals compare exactly, no flush; NaN never occurs), select m1 | parity
+      // or m2 | parity (the check phase stores both with the parity), and the own sign rides on
+      // alpha: (alpha ^ own sign) * sel has sign parity ^ own and magnitude |sel| * alpha
+      // (sign-symmetric rounding), the value of the class form bit for bit, zeros included
+      (void)d;
+      asm("v_cmp_eq_f32 vcc, |%1|, |%2|\n\ts_nop 1\n\tv_cndmask_b32 %0, %3, %4, vcc"
+          : "=v"(sel)
+          : "v"(a), "v"(o[t]), "v"(a), "v"(pr[t].b)
+          : "vcc");
+      uint32_t as;
+      asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c"
+          : "=v"(as)
+          : "v"((uint32_t)o[t]), "v"(FT<T>::bits(alpha)), "v"(0x80000000u));
+      c[t] = FT<T>::val(sel) * FT<T>::val(as);
+    } else if constexpr (sizeof(T) == 4) {
       // v_cmp_class (+-0) feeding v_cndmask; LLVM would rewrite the class test as
       // mask + integer compare.  s_nop 1: the VALU-writes-VCC -> VALU-reads-VCC
       // hazard the compiler itself pads on gfx950.
@@ -495,7 +556,7 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   }
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
-    lds_st<U, RState<T, DMAX, VPL, ENG>::kSplit>(smem, r_va(R, k, t), nv[t]);
+    lds_st<U, RState<T, DMAX, VPL, ENG>::kAbs>(smem, r_va(R, k, t), nv[t]);
     if (KV) R.ov[KV ? k : 0][KV ? t : 0] = nv[t];
   }
 #if QLDPC_FLIPLATE
@@ -538,7 +599,9 @@ template <typename T, int DMAX, int VPL, int D3K, int ENG>
 __device__ inline void r_gather_k(unsigned char* smem, const RState<T, DMAX, VPL, ENG>& R, int k,
                                   typename CSEntry<T>::type (&pn)[DMAX], typename FT<T>::U (&on)[DMAX]) {
   constexpr int N3 = DMAX > 3 ? 3 : DMAX;
-  if (k < D3K)
+  if (k < eng_d2k(ENG))
+    r_gather<T, DMAX, VPL, 2, ENG>(smem, R, k, pn, on);
+  else if (k < D3K)
     r_gather<T, DMAX, VPL, N3, ENG>(smem, R, k, pn, on);
   else
     r_gather<T, DMAX, VPL, DMAX, ENG>(smem, R, k, pn, on);
@@ -574,8 +637,9 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     if (k == VPL - 1 && !last_live) break;  // every lane of this wave holds padding
     const bool xp = ((xprev >> k) & 1u) != 0;
     const int32_t* pk = perm ? perm + k * TB : nullptr;
-    const bool x = k < D3K ? r_var_one<T, DMAX, VPL, N3, ENG>(smem, R, k, pr, o, fdelta, alpha, xp, post, pk)
-                           : r_var_one<T, DMAX, VPL, DMAX, ENG>(smem, R, k, pr, o, fdelta, alpha, xp, post, pk);
+    const bool x = k < eng_d2k(ENG) ? r_var_one<T, DMAX, VPL, 2, ENG>(smem, R, k, pr, o, fdelta, alpha, xp, post, pk)
+                   : k < D3K        ? r_var_one<T, DMAX, VPL, N3, ENG>(smem, R, k, pr, o, fdelta, alpha, xp, post, pk)
+                                    : r_var_one<T, DMAX, VPL, DMAX, ENG>(smem, R, k, pr, o, fdelta, alpha, xp, post, pk);
     xbits |= (x ? 1u : 0u) << k;
   }
 #if QLDPC_FLIPLATE
@@ -583,7 +647,7 @@ __device__ inline uint32_t r_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     if ((fl >> k) & 1u) {
-      const int nd = k < D3K ? N3 : DMAX;
+      const int nd = k < eng_d2k(ENG) ? 2 : k < D3K ? N3 : DMAX;
 #pragma unroll
       for (int t = 0; t < DMAX; ++t)
         if (t < nd) f_xor<ENG>(smem, r_fa(R, k, t, fdelta), 1u);
@@ -664,7 +728,7 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
     (void)alpha_next;
     typename CSEntry<T>::type st;
     st.a = m1 | (px & kS);
-    st.b = m2;
+    st.b = m2 | ((sizeof(T) == 4 && QLDPC_F32_C2V4) ? (px & kS) : (U)0);  // fp32: m2 | parity too
     lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
   }
   return mism;
@@ -791,7 +855,7 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
         px ^= (uint32_t)FT<T>::bits(tcur);
       }
       st.a = FT<T>::bits(f1) | (px & kS);
-      st.b = FT<T>::bits(f2);
+      st.b = FT<T>::bits(f2) | (QLDPC_F32_C2V4 ? (px & kS) : 0u);  // m2 | parity (r_var_one's 4-VALU c2v)
     }
     lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
     if (PFC == 2) {
@@ -1310,7 +1374,9 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   M.fbase = eng_base(ENG) == 4 ? Ly.f + 4u : Ly.f;
   M.rstart = Ly.v + 16u;
   M.rsh = 4 + __builtin_ctz((unsigned)nch);
-  if (SP) M.fbase = Ly.f - (sbase >> (eng_m2s(ENG) ? 1 : 2));  // split: absolute CS addresses (16-byte aligned base)
+  // absolute CS addresses (split or kAbs; 16-byte aligned base): fbase absorbs the base
+  constexpr bool AB = RState<T, DMAX, VPL, ENG>::kAbs;
+  if (AB) M.fbase = Ly.f - (sbase >> (eng_fb(ENG) ? 3 : (sizeof(T) == 4 || eng_m2s(ENG)) ? 1 : 2));
   const uint32_t fdelta = eng_base(ENG) == 4 ? Ly.f : M.fbase;
   // waves whose lanes all hold padding variables skip the last variable (engine 4)
   const bool last_live = uni((VPL - 1) * TB + (tid & ~63) < n ? 1 : 0) != 0;
@@ -1339,8 +1405,8 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         const U cl = FT<T>::bits(r_prior(R, k));  // w domain: the prior as is
 #pragma unroll
         for (int t = 0; t < DMAX; ++t) {
-          if ((eng_m2x(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;  // (no dummy 4th edge kept)
-          lds_st<U, SP>(smem, r_va(R, k, t), cl);
+          if (no_edge<ENG, D3K>(k, t)) continue;  // (no dummy edge kept)
+          lds_st<U, AB>(smem, r_va(R, k, t), cl);
           if (KV) R.ov[KV ? k : 0][KV ? t : 0] = cl;
         }
       }
@@ -1371,7 +1437,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
             if (e) {
 #pragma unroll
               for (int t = 0; t < DMAX; ++t) {
-                if ((eng_m2x(ENG) || eng_fb(ENG)) && k < D3K && t >= 3) continue;
+                if (no_edge<ENG, D3K>(k, t)) continue;
                 if constexpr (eng_base(ENG) == 4)
                   atomicXor(&lds_at<uint32_t>(smem, f_addr<T, ENG>(R.ea[k][t], M)), 2u);
                 else if constexpr (eng_c2s(ENG))

@@ -99,11 +99,11 @@ bool use_f64x(int engine, int precision, int dmax, int tb, int vpl, int ea_shift
 
 // Slot-family kernels of an engine (2, 3 or 4).
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
-                      int nch = 0, int tail = 0, int m2s = 0, int fb = 0) {
+                      int nch = 0, int tail = 0, int m2s = 0, int fb = 0, int d2k = 0) {
   // fp32 space-time family with byte F words (rows of 2 chunks + a tail slot, 512 threads, 2 per CU)
   if (fb) {
     const bool ok = engine == 3 && precision == 32 && dmax == 4 && ea_shift == 2 && nch == 2 && tail && tb == 512;
-    return ok ? get_rvariant_f32_stfb(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
+    return ok ? get_rvariant_f32_stfb(vpl, d3k, d2k) : SVariant{nullptr, nullptr, nullptr, nullptr};
   }
   // fp64 m2-in-slot family (rows of 3 chunks + a tail slot, <= 256 threads, 3 workgroups per CU)
   if (m2s) {
@@ -909,9 +909,16 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     std::vector<int32_t> order;
     order.reserve(g->n);
     const bool sort3 = bp->engine == 3 && DM >= 4 && env_int("QLDPC_DEGSORT", 1) != 0;
-    for (int pass = 0; pass < (sort3 ? 2 : 1); ++pass)
+    // byte-F kernels also keep degree <= 2 variables (the space-time measurement columns) in
+    // compile-time 2-edge slots: those go first
+    const bool sort2 = sort3 && bp->fb && env_int("QLDPC_D2K", 1) != 0;
+    auto cls = [&](int j) {
+      const int d = (int)g->col_rows[j].size();
+      return sort2 ? (d <= 2 ? 0 : d <= 3 ? 1 : 2) : (d <= 3 ? 0 : 1);
+    };
+    for (int pass = 0; pass < (sort2 ? 3 : sort3 ? 2 : 1); ++pass)
       for (int j = 0; j < g->n; ++j)
-        if (!sort3 || ((int)g->col_rows[j].size() <= 3) == (pass == 0)) order.push_back(j);
+        if (!sort3 || cls(j) == pass) order.push_back(j);
     bp->slot_var.assign((size_t)VPL * TB, -1);
     for (int j = 0; j < g->n; ++j) bp->slot_var[j] = order[j];
     bp->d3k = 0;
@@ -924,6 +931,17 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         }
         if (!ok) break;
         bp->d3k = k + 1;
+      }
+    bp->d2k = 0;
+    if (sort2)
+      for (int k = 0; k < VPL; ++k) {
+        bool ok = true;
+        for (int t = 0; t < TB && ok; ++t) {
+          const int j = bp->slot_var[(size_t)k * TB + t];
+          ok = j < 0 || (int)g->col_rows[j].size() <= 2;
+        }
+        if (!ok) break;
+        bp->d2k = k + 1;
       }
     const int vbase_dw = (bp->engine == 3 && env_int("QLDPC_BANKOPT", 1) != 0)
                              ? (int)(r_layout(3, vslots2, g->m, tsize, bp->tail, bp->m2s).v / 4)
@@ -948,7 +966,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab, bp->tail,
                      bp->m2s && env_int("QLDPC_M2S_PLACE", 1) != 0);
     kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch, bp->tail,
-                        bp->m2s, bp->fb).dec_k;
+                        bp->m2s, bp->fb, bp->d2k).dec_k;
     if (bp->engine >= 3) {
       // row degrees by check label: engine 4 keeps them in F, engine 3 their parity (bp_reg.h, w domain)
       std::vector<uint8_t> deg(std::max(1, g->m));
@@ -1016,7 +1034,7 @@ int qldpc_bp_kernel_id(const qldpc_bp* bp, int32_t* kernel_id, int32_t* row_chun
     if (bp->m2s)
       id = bp->m2s == 2 ? 31103 : 11103;
     else if (bp->fb)
-      id = 21013;
+      id = 21013 + ((bp->d3k >= 8 && bp->d2k > 0) ? 100000 * std::min(bp->d2k, 4) : 0);  // + D2K digit
     else if (bp->tail)
       id = 1013;
     else if (use_f64w(bp->engine, bp->precision, bp->DMAX, bp->TB, bp->VPL, bp->ea_shift, bp->nch))
@@ -1146,7 +1164,7 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
     SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch,
-                              bp->tail, bp->m2s, bp->fb);
+                              bp->tail, bp->m2s, bp->fb, bp->d2k);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;

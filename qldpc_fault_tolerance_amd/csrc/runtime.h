@@ -71,6 +71,7 @@ struct qldpc_bp {
   qldpc_rt::DevBuf rperm;  // engine 3: original check of each check label (label_checks)
   int gather_conf[2] = {0, 0};  // engine 3: extra gather cycles per pass before / after labelling
   int d3k = 0;
+  int d2k = 0;  // byte-F family: compile-time degree-2 slot count (slots of the measurement variables)
   int ea_shift = 0;  // engine 3: 2 = dword-scaled LDS addresses in the edge words (images > 64 KiB)
   int tail = 0;      // engine 3: 1 = rows of nch chunks + one tail slot per row (bp_reg.h eng_tail)
   int m2s = 0;       // engine 3: 1 = one-word check state, m2 in the argmin slot (bp_reg.h eng_m2s);

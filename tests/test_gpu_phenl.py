@@ -99,8 +99,9 @@ def test_phenl_n1225_space_time_graph(gpu, oracle):
     p = 0.01
     ph = _phenl(code, p, p, 3, precision=32)
     g = ph.decoders[0].geometry()
-    # register engine, tail layout with byte F words: two 512-thread decodes per CU (engine id 21013)
-    assert (g["engine"], g["kernel_id"], g["threads"], g["vars_per_thread"]) == (3, 21013, 512, 11), g
+    # register engine, tail layout with byte F words: two 512-thread decodes per CU (engine id 21013),
+    # the 1764 degree-2 measurement variables in 3 compile-time 2-edge slots (+ 100000 * D2K)
+    assert (g["engine"], g["kernel_id"], g["threads"], g["vars_per_thread"]) == (3, 321013, 512, 11), g
     assert g["blocks_per_cu"] == 2 and 2 * g["lds_bytes"] <= 160 * 1024, g
     S, R = 96, 3
     res = ph.run(p / 2, p / 2, p / 2, p, 11, 0, S, R, per_shot=True)
@@ -208,15 +209,17 @@ def test_st_fp32_byte_f_family_decode_matches_oracle(gpu, oracle, p):
     e = (rng.random((160, n)) < p).astype(np.uint8)
     synd = H.matvec(e).astype(np.uint8)
     dec = DeviceBP(H, pr, max_iter=mi, precision=32)
-    assert dec.geometry()["kernel_id"] == 21013
+    assert dec.geometry()["kernel_id"] == 321013
     c, i, v = dec.decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, pr, mi, "minimum_sum", 0.625, synd, 32)
     assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64))
-    os.environ["QLDPC_E3_FB"] = "0"
-    try:
-        d1 = DeviceBP(H, pr, max_iter=mi, precision=32)
-    finally:
-        del os.environ["QLDPC_E3_FB"]
-    assert d1.geometry()["kernel_id"] == 1013
-    c1, i1, v1 = d1.decode_batch(synd)
-    assert np.array_equal(c, c1) and np.array_equal(i, i1) and np.array_equal(v, v1)
+    # the same family without the degree-2 slots, and the 1024-thread family
+    for env, kid in (("QLDPC_D2K", 21013), ("QLDPC_E3_FB", 1013)):
+        os.environ[env] = "0"
+        try:
+            d1 = DeviceBP(H, pr, max_iter=mi, precision=32)
+        finally:
+            del os.environ[env]
+        assert d1.geometry()["kernel_id"] == kid
+        c1, i1, v1 = d1.decode_batch(synd)
+        assert np.array_equal(c, c1) and np.array_equal(i, i1) and np.array_equal(v, v1), env

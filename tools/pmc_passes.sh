@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 PMC passes (one counter group per run, as gfx950 requires) over one
 # fused MC launch.  Run ON the GPU box:  tools/pmc_passes.sh <outdir> [prof_one args...]
+# (PROF_SCRIPT=prof_st.py: one space-time decode_batch launch instead)
 #   outdir is relative to the repo root; results: <outdir>/p<N>/p_counter_collection.csv
 set -u
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -21,6 +22,6 @@ for pass in "${PASSES[@]}"; do
   n=$((n + 1))
   # shellcheck disable=SC2086
   timeout -s KILL 90 rocprofv3 --pmc $pass --output-format csv -d "$OUT/p$n" -o p -- \
-    python3 "$R/tools/prof_one.py" "$@" > "$OUT/p$n.log" 2>&1 || { echo "pass $n failed"; exit 1; }
+    python3 "$R/tools/${PROF_SCRIPT:-prof_one.py}" "$@" > "$OUT/p$n.log" 2>&1 || { echo "pass $n failed"; exit 1; }
 done
 echo "pmc passes done: $OUT"
