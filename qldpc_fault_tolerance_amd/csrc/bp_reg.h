@@ -61,6 +61,10 @@
 #ifndef QLDPC_F32_C2V4
 #define QLDPC_F32_C2V4 1
 #endif
+// fp64 c2v in 5 VALU per edge (r_var_one, two-word families); the check phases store m2 | parity
+#ifndef QLDPC_F64_C2V5
+#define QLDPC_F64_C2V5 1
+#endif
 // dword-scaled packed edge words (space-time families) hold absolute dword indices (SDWA unpack)
 #ifndef QLDPC_ABS_SH2
 #define QLDPC_ABS_SH2 1
@@ -514,6 +518,23 @@ __device__ inline bool r_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
           : "vcc");
       sel &= ~kS;
       c[t] = FT<T>::val(FT<T>::bits(FT<T>::val(sel) * alpha) ^ (d & kS));
+    } else if constexpr (QLDPC_F64_C2V5) {
+      // double in 5 VALU (the class form takes 7: the 64-bit xor is 2): |own| == |m1| by
+      // v_cmp_eq_f64 on absolute values, two cndmasks select m1 | parity or m2 | parity, and the
+      // own sign rides on alpha's high word: (alpha ^ own sign) * sel, the same bits
+      (void)d;
+      uint32_t slo, shi;
+      asm("v_cmp_eq_f64 vcc, |%2|, |%3|\n\ts_nop 1\n\tv_cndmask_b32 %0, %4, %5, vcc\n\tv_cndmask_b32 %1, %6, %7, vcc"
+          : "=&v"(slo), "=&v"(shi)
+          : "v"(FT<T>::val(a)), "v"(FT<T>::val(o[t])), "v"((uint32_t)a), "v"((uint32_t)pr[t].b),
+            "v"((uint32_t)(a >> 32)), "v"((uint32_t)(pr[t].b >> 32))
+          : "vcc");
+      const U ab = FT<T>::bits(alpha);
+      uint32_t ahs;
+      asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c"
+          : "=v"(ahs)
+          : "v"((uint32_t)(o[t] >> 32)), "v"((uint32_t)(ab >> 32)), "v"(0x80000000u));
+      c[t] = FT<T>::val(((U)shi << 32) | slo) * FT<T>::val(((U)ahs << 32) | (uint32_t)ab);
     } else {
       // double: the same class test on the 64-bit pair and two cndmasks; |sel| folds
       // into v_mul_f64's source modifier; sign = hi(product) ^ (hi(d) & sign bit) in
@@ -728,7 +749,7 @@ __device__ inline int r_check(unsigned char* smem, const RLayout& Ly, int m, int
     (void)alpha_next;
     typename CSEntry<T>::type st;
     st.a = m1 | (px & kS);
-    st.b = m2 | ((sizeof(T) == 4 && QLDPC_F32_C2V4) ? (px & kS) : (U)0);  // fp32: m2 | parity too
+    st.b = m2 | ((sizeof(T) == 4 ? QLDPC_F32_C2V4 : QLDPC_F64_C2V5) ? (px & kS) : (U)0);  // m2 | parity too
     lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
   }
   return mism;
@@ -831,7 +852,7 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
         px ^= (uint32_t)(FT<T>::bits(tcur) >> 32);
       }
       st.a = FT<T>::bits(f1) | ((U)(px & 0x80000000u) << 32);
-      st.b = FT<T>::bits(f2);
+      st.b = FT<T>::bits(f2) | (QLDPC_F64_C2V5 ? ((U)(px & 0x80000000u) << 32) : (U)0);  // m2 | parity
     } else {
       float f1 = FT<T>::val(FT<T>::kSent), f2 = f1;
       uint32_t px = s ? kS : 0u;
