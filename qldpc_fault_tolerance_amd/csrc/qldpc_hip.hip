@@ -115,7 +115,7 @@ SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int 
   if (tail) {
     const bool ok = engine == 3 && dmax == 4 && ea_shift == 2 && nch == (precision == 64 ? 4 : 2) && tb > 512;
     if (!ok) return SVariant{nullptr, nullptr, nullptr, nullptr};
-    return precision == 64 ? get_rvariant_f64_st(vpl, d3k) : get_rvariant_f32_st(vpl, d3k);
+    return precision == 64 ? get_rvariant_f64_st(vpl, d3k, d2k) : get_rvariant_f32_st(vpl, d3k);
   }
   if (use_f64w(engine, precision, dmax, tb, vpl, ea_shift, nch))
     return dmax == 5 ? get_rvariant_f64_w_d5(vpl, d3k, nch) : get_rvariant_f64_w(vpl, d3k, nch);
@@ -911,7 +911,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     const bool sort3 = bp->engine == 3 && DM >= 4 && env_int("QLDPC_DEGSORT", 1) != 0;
     // byte-F kernels also keep degree <= 2 variables (the space-time measurement columns) in
     // compile-time 2-edge slots: those go first
-    const bool sort2 = sort3 && bp->fb && env_int("QLDPC_D2K", 1) != 0;
+    const bool sort2 = sort3 && (bp->fb || (bp->tail && !bp->m2s && precision == 64)) && env_int("QLDPC_D2K", 1) != 0;
     auto cls = [&](int j) {
       const int d = (int)g->col_rows[j].size();
       return sort2 ? (d <= 2 ? 0 : d <= 3 ? 1 : 2) : (d <= 3 ? 0 : 1);
@@ -1036,7 +1036,7 @@ int qldpc_bp_kernel_id(const qldpc_bp* bp, int32_t* kernel_id, int32_t* row_chun
     else if (bp->fb)
       id = 21013 + ((bp->d3k >= 8 && bp->d2k > 0) ? 100000 * std::min(bp->d2k, 4) : 0);  // + D2K digit
     else if (bp->tail)
-      id = 1013;
+      id = 1013 + ((bp->precision == 64 && bp->VPL == 6 && bp->d2k >= 1 && bp->d3k >= 1) ? 100000 : 0);
     else if (use_f64w(bp->engine, bp->precision, bp->DMAX, bp->TB, bp->VPL, bp->ea_shift, bp->nch))
       id = 103;
     else if (use_f64x(bp->engine, bp->precision, bp->DMAX, bp->TB, bp->VPL, bp->ea_shift))

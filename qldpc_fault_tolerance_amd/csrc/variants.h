@@ -48,7 +48,7 @@ SVariant get_rvariant_f64_w3(int vpl, int d3k);
 SVariant get_rvariant_f64_w_d5(int vpl, int d3k, int nch);  // kern_r_f64_d5.hip: column degree 5
 SVariant get_rvariant_f64_x(int vpl, int d3k);  // kern_r_f64_x.hip: 257-512 threads, 128 VGPRs (opt-in)
 SVariant get_rvariant_f64_w4(int vpl, int d3k);
-SVariant get_rvariant_f64_st(int vpl, int d3k);  // kern_r_f64_st*.hip: tail layout, 1024 threads (engine id 1013)
+SVariant get_rvariant_f64_st(int vpl, int d3k, int d2k = 0);  // kern_r_f64_st*.hip: tail layout, 1024 threads (engine id 1013)
 SVariant get_rvariant_f64_st_hi(int vpl, int d3k);
 SVariant get_rvariant_f32_st(int vpl, int d3k);  // kern_r_f32_st.hip: tail layout in float (engine id 1013)
 SVariant get_rvariant_f64_m2s(int vpl, int d3k);  // kern_r_f64_m2s.hip: m2 in the argmin slot, rows of 3 chunks + tail (engine id 11103)

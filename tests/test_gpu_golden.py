@@ -99,6 +99,8 @@ def test_config5_space_time_replayed_on_gpu_fp64(gpu):
         assert geo["engine"] == (6 if hbm else 3), geo
         if not hbm:
             assert geo["lds_bytes"] > 64 * 1024 and geo["threads"] == 1024, geo  # the tail-layout family
+            # 6 variables per thread, the first slot's 1024 degree-2 measurement variables on 2 edge slots
+            assert geo["kernel_id"] == 101013, geo
         d2 = [DeviceBP(code.csr(k), p * np.ones(n), max_iter=mi, precision=64) for k in ("hz", "hx")]
         ph = DevicePhenl(code, st[0], st[1], d2[0], d2[1], num_rep=3)
         u = uniforms(int(g["st1225_seed0"][0]), S, ph.uniforms_per_sample(3))
