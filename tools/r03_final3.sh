@@ -4,8 +4,12 @@
 # 0.005), the BP+OSD line at p = 0.04 with its kernel trace.
 set -u
 R=$(cd "$(dirname "$0")/.." && pwd)
-TAG=r03_final3 bash "$R/tools/r03_final.sh" || exit 1
 O=$R/gpurun_out/r03_final3
+if [ "${PART:-1}" = 1 ]; then
+  TAG=r03_final3 bash "$R/tools/r03_final.sh" || exit 1
+  exit 0
+fi
+mkdir -p "$O"
 cd "$R" || exit 1
 for cfg in "32 0.06 bp" "64 0.06 bp" "64 0.02 bp" "64 0.005 bp" "32 0.005 bp"; do
   set -- $cfg
