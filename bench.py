@@ -106,7 +106,7 @@ def kernel_name(dec):
         # decisions and syndromes as LDS ballot words for n + m <= 2048 (bp_hbm.hip hbm_xlds)
         xl = dec.graph.n + dec.graph.m <= 2048 and os.environ.get("QLDPC_HBM_XLDS", "1") != "0"
         return f"(anonymous namespace)::hdec_kernel<{t}, {'true' if xl else 'false'}> (engine 6, staged shot loop)"
-    if g.get("kernel_id") in (11103, 31103):  # fp64 one-slot families (rows of 3 chunks + a tail slot, 256 threads)
+    if g.get("kernel_id") in (11103, 31103, 40103):  # fp64 one-slot families (256 threads, NCH 3)
         return f"qldpc::rmc_kernel<double, 4, {g['vars_per_thread']}, {g['kernel_id']}, {g['degree3_slots']}, 256, 3>"
     mc = dec.graph.info()["max_col_deg"]
     dmax = 4 if mc <= 4 else (mc if g["engine"] == 3 and (mc <= 6 if dec.precision == 32 else mc == 5) else 8)

@@ -98,7 +98,17 @@ constexpr int eng_tail(int E) { return (E / 1000) % 10; }
 // no longer holds the edge's own previous v2c (kept in VGPRs) is the argmin, and its value is m2.
 // The image shrinks by 8 bytes per check; with rows of 7 as 3 chunks + a tail slot the n1600 fp64
 // image is 52.3 KB, so 3 workgroups share a CU (168-VGPR budget).
-constexpr bool eng_m2s(int E) { return (E / 10000) % 10 == 1; }
+constexpr bool eng_m2s(int E) { return (E / 10000) % 10 == 1 || (E / 10000) % 10 == 4; }
+// + 40000 = m2s with variable-major v2c slots ("m2v", engine id 40103): edge (k, d) of lane t owns
+// V slot (ecnt(k) + d) * LB + t (the last variable slot: ecnt * LB + d * NL + t), so the variable
+// phase reads and writes its slots lane-linearly (conflict-free, one base VGPR and immediate
+// offsets), and the check phase gathers its row's 7 slots from a per-thread register table
+constexpr bool eng_m2v(int E) { return (E / 10000) % 10 == 4; }
+// edge slots of variable slots 0..k-1 (degree-3 slots k < D3K keep 3)
+template <int D3K>
+__host__ __device__ constexpr int m2v_ecnt(int k) { return 3 * (k < D3K ? k : D3K) + 4 * (k > D3K ? k - D3K : 0); }
+// rows per thread the m2v check phase keeps in its register table (host-enforced m <= 4 * TB)
+constexpr int kM2vRows = 4;
 // + 20000 = byte F ("fb": the per-check flags F as one byte per check instead of a word, flips
 // xored into the containing word at the byte's shift): the fp32 space-time tail family for 512-thread
 // workgroups (engine id 21013), whose 79.6 KB image lets 2 decodes share a CU
@@ -308,11 +318,32 @@ struct RState {
   // m2s with QLDPC_M2S_UNIL: one prior for every variable (uniform channel_probs, host-checked),
   // loaded by a scalar load: 2 SGPRs instead of 2 * VPL VGPRs
   static constexpr bool kUniL = eng_m2x(ENG) && QLDPC_M2S_UNIL;
+  static constexpr bool kM2v = eng_m2v(ENG);
   uint32_t ea[VPL][DMAX];
-  uint32_t ev[kSplit ? VPL : 1][kSplit ? DMAX : 1];
+  uint32_t ev[kSplit && !kM2v ? VPL : 1][kSplit && !kM2v ? DMAX : 1];
   T L[kUniL ? 1 : VPL];
   U ov[kKeepV ? VPL : 1][kKeepV ? DMAX : 1];
+  // m2v: lane base of the V slots and the last variable slot's per-edge addresses
+  uint32_t vlane;
+  uint32_t vl[kM2v ? DMAX : 1];
 };
+// m2v row table of one thread: row q (check tid + q * TB) = 7 16-bit slot offsets from the V base,
+// two per word; loaded from global memory before the barrier that precedes each check phase
+// (registers live across that barrier only)
+struct M2vRows {
+  uint4 w[kM2vRows];
+};
+__device__ inline void m2v_rows_load(const SSector& S, int tid, int TB, int m, M2vRows& r) {
+#pragma unroll
+  for (int q = 0; q < kM2vRows; ++q)
+    if (q * TB < m) r.w[q] = reinterpret_cast<const uint4*>(S.rows)[(size_t)q * TB + tid];
+}
+// m2v: absolute V slot address of edge (k, t) (immediate offsets from the lane base)
+template <typename T, int DMAX, int VPL, int ENG, int D3K, int LB>
+__device__ inline uint32_t m2v_va(const RState<T, DMAX, VPL, ENG>& R, int k, int t) {
+  if (k < VPL - 1) return R.vlane + (uint32_t)((m2v_ecnt<D3K>(k) + t) * LB * 8);
+  return R.vl[RState<T, DMAX, VPL, ENG>::kM2v ? t : 0];
+}
 // 4 * (16-bit half h of w) in one VALU (SDWA word select feeding the shift)
 template <int H, int SH>
 __device__ inline uint32_t sdwa_shl(uint32_t w) {
@@ -360,7 +391,7 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
       } else if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) {
         // c2s: the absolute address of the edge's F word (entry = check label + 1)
         R.ea[k][t] = eng_c2s(ENG) ? sbase + Ly.f + 4u * echk(e) : sbase + echk(e) * (uint32_t)((eng_m2s(ENG) ? 1 : 2) * sizeof(T));
-        R.ev[k][t] = sbase + va;
+        if constexpr (!RState<T, DMAX, VPL, ENG>::kM2v) R.ev[k][t] = sbase + va;
       } else if constexpr (RState<T, DMAX, VPL, ENG>::kAbs) {  // absolute dword indices
         R.ea[k][t] = ((sbase + echk(e) * (uint32_t)(2 * sizeof(T))) >> 2) | (((sbase + va) >> 2) << 16);
       } else {
@@ -375,6 +406,14 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
   // uniform prior (slot 0 of lane 0 holds a real variable); padding lanes take it too (their
   // results are never read)
   if constexpr (RState<T, DMAX, VPL, ENG>::kUniL) R.L[0] = w_prior<T>(llr[0]);
+  if constexpr (RState<T, DMAX, VPL, ENG>::kM2v) {
+    // lane base (LDS addresses are < 64 KiB: the mask makes the sign bit known, so the per-edge
+    // offsets fold into the DS instructions' offset fields); the last variable slot strides S.vnl
+    R.vlane = (sbase + Ly.v + 8u * (uint32_t)tid) & 0xFFFFu;
+    const uint32_t last = (uint32_t)S.vlast * 8u;  // byte offset of the last slot's first edge
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) R.vl[t] = R.vlane + last + (uint32_t)t * (uint32_t)S.vnl * 8u;
+  }
 }
 template <typename T, int DMAX, int VPL, int ENG>
 __device__ inline T r_prior(const RState<T, DMAX, VPL, ENG>& R, int k) {
@@ -450,7 +489,8 @@ __device__ inline void r_launder(RState<T, DMAX, VPL, ENG>& R) {
     for (int t = 0; t < DMAX; ++t) {
       if (no_edge<ENG, D3K>(k, t)) continue;
       asm volatile("" : "+v"(R.ea[k][t]));
-      if constexpr (RState<T, DMAX, VPL, ENG>::kSplit) asm volatile("" : "+v"(R.ev[k][t]));
+      if constexpr (RState<T, DMAX, VPL, ENG>::kSplit && !RState<T, DMAX, VPL, ENG>::kM2v)
+        asm volatile("" : "+v"(R.ev[k][t]));
     }
 }
 
@@ -906,18 +946,21 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
 // v2c" marks the argmin and c2v = alpha * m2, else alpha * m1.  Same values as ldpc's "m2 if
 // |own| == m1 else m1": with a tie m1 == m2; a slot equal to the own word by chance has
 // m2 == m1 and the own sign == parity, i.e. the same c2v either way.
-template <typename T, int DMAX, int VPL, int ND, int ENG>
+template <typename T, int DMAX, int VPL, int ND, int ENG, int D3K = 0, int LB = 256>
 __device__ inline void m_gather(const RState<T, DMAX, VPL, ENG>& R, int k, typename FT<T>::U (&an)[DMAX],
                                 typename FT<T>::U (&vn)[DMAX]) {
   using U = typename FT<T>::U;
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
     if constexpr (!eng_c2s(ENG)) an[t] = lds_ld<U, true>(nullptr, R.ea[k][t]);  // (c2s: ea = F word)
-    vn[t] = lds_ld<U, true>(nullptr, R.ev[k][t]);
+    if constexpr (eng_m2v(ENG))
+      vn[t] = lds_ld<U, true>(nullptr, m2v_va<T, DMAX, VPL, ENG, D3K, LB>(R, k, t));
+    else
+      vn[t] = lds_ld<U, true>(nullptr, R.ev[k][t]);
   }
 }
 
-template <typename T, int DMAX, int VPL, int ND, int ENG>
+template <typename T, int DMAX, int VPL, int ND, int ENG, int D3K = 0, int LB = 256>
 __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, int k,
                                  const typename FT<T>::U (&an)[DMAX],
                                  const typename FT<T>::U (&vn)[DMAX], uint32_t fdelta, T alpha, bool xprev,
@@ -969,7 +1012,10 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   }
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
-    lds_st<U, true>(nullptr, R.ev[k][t], nv[t]);
+    if constexpr (eng_m2v(ENG))
+      lds_st<U, true>(nullptr, m2v_va<T, DMAX, VPL, ENG, D3K, LB>(R, k, t), nv[t]);
+    else
+      lds_st<U, true>(nullptr, R.ev[k][t], nv[t]);
     if constexpr (KV1) R.ov[k][t] = nv[t];
   }
   if (x != xprev) {
@@ -984,7 +1030,7 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   return x;
 }
 
-template <typename T, int DMAX, int VPL, int D3K, int ENG>
+template <typename T, int DMAX, int VPL, int D3K, int ENG, int LB = 256>
 __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, uint32_t fdelta, T alpha, uint32_t xprev,
                                  bool last_live, double* post = nullptr, const int32_t* perm = nullptr, int TB = 0) {
   using U = typename FT<T>::U;
@@ -999,9 +1045,9 @@ __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   U ab[PF][DMAX], vb[PF][DMAX];
   auto gk = [&](int k, U (&an)[DMAX], U (&vn)[DMAX]) {
     if (k < D3K)
-      m_gather<T, DMAX, VPL, N3, ENG>(R, k, an, vn);
+      m_gather<T, DMAX, VPL, N3, ENG, D3K, LB>(R, k, an, vn);
     else
-      m_gather<T, DMAX, VPL, DMAX, ENG>(R, k, an, vn);
+      m_gather<T, DMAX, VPL, DMAX, ENG, D3K, LB>(R, k, an, vn);
   };
 #pragma unroll
   for (int k = 0; k < PF; ++k) gk(k, ab[k], vb[k]);
@@ -1017,8 +1063,8 @@ __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     if (k == VPL - 1 && !last_live) break;
     const bool xp = ((xprev >> k) & 1u) != 0;
     const int32_t* pk = perm ? perm + k * TB : nullptr;
-    const bool x = k < D3K ? m_var_one<T, DMAX, VPL, N3, ENG>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk)
-                           : m_var_one<T, DMAX, VPL, DMAX, ENG>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk);
+    const bool x = k < D3K ? m_var_one<T, DMAX, VPL, N3, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk)
+                           : m_var_one<T, DMAX, VPL, DMAX, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk);
     xbits |= (x ? 1u : 0u) << k;
   }
   return xbits;
@@ -1104,6 +1150,65 @@ __device__ inline int m_check(unsigned char* smem, const RLayout& Ly, int m, int
     const U par = (U)(px & 0x80000000u) << 32;
     lds_at<U>(smem, (uint32_t)(i + 1) * (uint32_t)sizeof(T)) = FT<T>::bits(f1) | par;
     lds_at<U>(smem, amin) = FT<T>::bits(f2) | par;
+  }
+  return mism;
+}
+
+// m2v check phase (fp64): row q of this thread (check i = tid + q * TB) gathers its 7 V slots
+// through the register table (scattered ds_read_b64), then min / second min / parity / argmin as
+// m_check: CS[i+1] = m1 | parity, V[argmin] = m2 | parity.  Rows of fewer edges point their unused
+// entries at a slot that holds the sentinel forever (never the argmin: no edge is below it).
+template <typename T, bool FIRST>
+__device__ inline int m2v_check(unsigned char* smem, const RLayout& Ly, int m, int tid, int TB, uint32_t& sbits,
+                                const M2vRows& RW, uint32_t vbase) {
+  using U = typename FT<T>::U;
+  static_assert(sizeof(T) == 8, "m2v: fp64 only");
+  int mism = 0;
+#pragma unroll
+  for (int q = 0; q < kM2vRows; ++q) {
+    const int i = tid + q * TB;
+    if (i >= m) break;
+    const uint32_t wd[4] = {RW.w[q].x, RW.w[q].y, RW.w[q].z, RW.w[q].w};
+    uint32_t a[7];
+#pragma unroll
+    for (int e = 0; e < 7; ++e) a[e] = vbase + ((e & 1) ? (wd[e >> 1] >> 16) : (wd[e >> 1] & 0xFFFFu));
+    double x[7];
+#pragma unroll
+    for (int e = 0; e < 7; ++e) x[e] = FT<T>::val(lds_ld<U, true>(nullptr, a[e]));
+    const uint32_t fo = Ly.f + 4u * (uint32_t)(i + 1);
+    const uint32_t fcur = lds_at<uint32_t>(smem, fo);
+    uint32_t s;
+    if (FIRST) {
+      s = ((fcur >> 1) ^ (fcur >> 2)) & 1u;
+      sbits |= s << q;
+      lds_at<uint32_t>(smem, fo) = (fcur & 4u) | ((fcur >> 2) & 1u);
+    } else {
+      s = (sbits >> q) & 1u;
+      mism |= (int)((fcur ^ s) & 1u);
+    }
+    double f1 = FT<T>::val(FT<T>::kSent), f2 = f1;
+    uint32_t px = s ? 0x80000000u : 0u;
+    uint32_t amin = a[0];
+#pragma unroll
+    for (int e = 0; e < 7; ++e) {
+      amin = __builtin_fabs(x[e]) < f1 ? a[e] : amin;
+      double t;
+      asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x[e]));
+      asm("v_min_f64 %0, %1, %2" : "=v"(f2) : "v"(f2), "v"(t));
+      asm("v_min_f64 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x[e]));
+    }
+#pragma unroll
+    for (int e = 0; e + 1 < 7; e += 2) {
+      uint32_t p;
+      asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96"
+          : "=v"(p)
+          : "v"(px), "v"((uint32_t)(FT<T>::bits(x[e]) >> 32)), "v"((uint32_t)(FT<T>::bits(x[e + 1]) >> 32)));
+      px = p;
+    }
+    px ^= (uint32_t)(FT<T>::bits(x[6]) >> 32);
+    const U par = (U)(px & 0x80000000u) << 32;
+    lds_at<U>(smem, (uint32_t)(i + 1) * (uint32_t)sizeof(T)) = FT<T>::bits(f1) | par;
+    lds_st<U, true>(nullptr, amin, FT<T>::bits(f2) | par);
   }
   return mism;
 }
@@ -1427,7 +1532,14 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
 #pragma unroll
         for (int t = 0; t < DMAX; ++t) {
           if (no_edge<ENG, D3K>(k, t)) continue;  // (no dummy edge kept)
-          lds_st<U, AB>(smem, r_va(R, k, t), cl);
+          if constexpr (eng_m2v(ENG)) {  // (m2v: 256-thread workgroups, host-enforced)
+            // lanes past the last variable slot's S.vnl own no slots there (their lane-linear
+            // addresses would run into the next edge's slots and past the V region)
+            if (k == VPL - 1 && tidl >= S.vnl) continue;
+            lds_st<U, true>(smem, m2v_va<T, DMAX, VPL, ENG, D3K, 256>(R, k, t), cl);
+          }
+          else
+            lds_st<U, AB>(smem, r_va(R, k, t), cl);
           if (KV) R.ov[KV ? k : 0][KV ? t : 0] = cl;
         }
       }
@@ -1484,6 +1596,9 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       st_acc[4] += t - st_a;
       st_a = t;
     }
+    M2vRows rwv;  // m2v: this thread's rows, loaded ahead of each check phase's barrier
+    if constexpr (eng_m2v(ENG))
+      if (have) m2v_rows_load(S, tid, TB, m, rwv);
     __syncthreads();
     // ---------------------------------------------------------- finish the previous decode
     if (pshot >= 0) {
@@ -1520,6 +1635,8 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       c_check_any<T, true>(smem, Ly, m, nch, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
     else if constexpr (eng_c2s(ENG))
       c2s_check<T, true, NCH, eng_tail(ENG)>(smem, Ly, m, tid, TB, sb, adaptive ? (T)0.5 : alpha_fixed);
+    else if constexpr (eng_m2v(ENG))
+      m2v_check<T, true>(smem, Ly, m, tid, TB, sb, rwv, sbase + Ly.v);
     else if constexpr (eng_m2s(ENG))
       m_check<T, true, NCH, eng_tail(ENG)>(smem, Ly, m, wbase, tid, TB, sb);
     else if constexpr (NCH > 0)
@@ -1567,6 +1684,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         else
           xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
         if (kPV) __builtin_amdgcn_s_setprio(0);
+        if constexpr (eng_m2v(ENG)) m2v_rows_load(S, tid, TB, m, rwv);
         unsigned long long t1 = 0;
         if (QLDPC_STAMPS) {
           t1 = qstamp();
@@ -1582,6 +1700,8 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         if (QLDPC_PRIO_C) __builtin_amdgcn_s_setprio(QLDPC_PRIO_C);
         if constexpr (eng_c2s(ENG))
           mism = c2s_check<T, false, NCH, eng_tail(ENG)>(smem, Ly, m, tid, TB, sb, alpha_next);
+        else if constexpr (eng_m2v(ENG))
+          mism = m2v_check<T, false>(smem, Ly, m, tid, TB, sb, rwv, sbase + Ly.v);
         else if constexpr (eng_m2s(ENG))
           mism = m_check<T, false, NCH, eng_tail(ENG)>(smem, Ly, m, wbase, tid, TB, sb);
         else if constexpr (NCH > 0)

@@ -49,6 +49,10 @@ struct SSector {
   int m, n, kw, max_iter, nch, vpl; // nch = 16-byte chunks per row; vpl = variables per thread
   int d3k;                          // engine 3: slots k < d3k hold variables of degree <= 3 only
   double alpha;                     // 0 => 1 - 2^-iter
+  // m2v (variable-major V slots): the check phase's row table [kM2vRows][4][TB] (two 16-bit slot
+  // byte offsets from the V base per word), the last variable slot's first V slot and per-edge stride
+  const uint32_t* rows;
+  int vlast, vnl;
 };
 
 struct SMcArgs {
@@ -488,6 +492,9 @@ __device__ inline SSector pick_ssector(const SMcArgs& A, int qi) {
   S.nch = b ? A.sec[1].nch : A.sec[0].nch;
   S.vpl = b ? A.sec[1].vpl : A.sec[0].vpl;
   S.alpha = b ? A.sec[1].alpha : A.sec[0].alpha;
+  S.rows = b ? A.sec[1].rows : A.sec[0].rows;
+  S.vlast = b ? A.sec[1].vlast : A.sec[0].vlast;
+  S.vnl = b ? A.sec[1].vnl : A.sec[0].vnl;
   return S;
 }
 

@@ -108,6 +108,9 @@ SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int 
   // fp64 m2-in-slot family (rows of 3 chunks + a tail slot, <= 256 threads, 3 workgroups per CU)
   if (m2s) {
     const bool ok = engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && nch == 3 && tail && tb <= 256;
+    if (m2s == 3)  // variable-major V slots: no tail array, 256 threads
+      return (engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && tb == 256) ? get_rvariant_f64_m2v(vpl, d3k)
+                                                                                          : SVariant{nullptr, nullptr, nullptr, nullptr};
     if (!ok) return SVariant{nullptr, nullptr, nullptr, nullptr};
     return m2s == 2 ? get_rvariant_f64_c2s(vpl, d3k) : get_rvariant_f64_m2s(vpl, d3k);
   }
@@ -744,7 +747,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
   if (bp->engine == 3 && precision == 64 && colmax == 5 && env_int("QLDPC_E3_D56", 1) != 0) bp->DMAX = 5;
   bp->probs.assign(channel_probs, channel_probs + g->n);
   auto fail = [&](int code) {
-    for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->rperm, &bp->work, &bp->h_rp, &bp->h_rcol,
+    for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->rowtab, &bp->perm, &bp->rperm, &bp->work, &bp->h_rp, &bp->h_rcol,
                       &bp->h_rcpos, &bp->h_cp, &bp->h_crpos, &bp->h_ws})
       d->release();
     delete bp;
@@ -860,9 +863,24 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         bool full = true;
         for (int i = 0; i < g->m && full; ++i) full = g->row_ptr[i + 1] - g->row_ptr[i] == 7;
         if (full && env_int("QLDPC_C2S", 0) != 0 && r_fits(3, (1 + g->m * 3) * 2, g->m, 8, 0, 1, 2)) bp->m2s = 2;
+        // variable-major V slots (bp_reg.h eng_m2v, kern_r_f64_m2v.hip): edge (k, d) of lane t at
+        // slot (ecnt(k) + d) * 256 + t, the last variable slot at ecnt * 256 + d * NL + t, then one
+        // sentinel slot; the check phase's rows come from a register table (m <= 4 * 256)
+        const int d3 = n3 == g->n ? vpl : n3 / 256;
+        const int nlast = g->n - (vpl - 1) * 256, NL = (nlast + 63) & ~63;
+        const int ecl = 3 * std::min(vpl - 1, d3) + 4 * std::max(0, vpl - 1 - d3);
+        const int vm = ecl * 256 + (vpl - 1 < d3 ? 3 : 4) * NL + 1;
+        if (bp->m2s == 1 && tb == 256 && g->m <= 4 * 256 && vm * 8 < 65536 && env_int("QLDPC_M2V", 0) != 0 &&
+            r_fits(3, vm, g->m, 8, 0, 0, 1)) {
+          bp->m2s = 3;
+          bp->tail = 0;
+          bp->vslots_m2v = vm;
+          bp->m2v_vlast = ecl * 256;
+          bp->m2v_nl = NL;
+        }
       }
     }
-    const int vslots_e3 = (1 + g->m * bp->nch) * (16 / tsize);
+    const int vslots_e3 = bp->vslots_m2v ? bp->vslots_m2v : (1 + g->m * bp->nch) * (16 / tsize);
     if (bp->engine >= 3 && ((DM != 4 && !(bp->engine == 3 && (DM == 5 || DM == 6))) ||
                             (!bp->fb && choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL, pref, vmax)) ||
                             !r_fits(bp->engine, vslots_e3, g->m, tsize, bp->ea_shift, bp->tail, bp->m2s, bp->fb) ||
@@ -876,7 +894,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
       if (DM == 5 || DM == 6) bp->DMAX = DM = 8;  // engine 2 kernels come in 4 and 8 slots
     }
-    const int vslots2 = (1 + g->m * bp->nch) * (16 / tsize);
+    const int vslots2 = bp->vslots_m2v ? bp->vslots_m2v : (1 + g->m * bp->nch) * (16 / tsize);
     if (bp->engine >= 3) {
       bp->NS = 1;
       bp->lds_bytes =
@@ -964,7 +982,89 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         return fail(set_err(QLDPC_EHIP, "upload check labels"));
     }
     build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab, bp->tail,
-                     bp->m2s && env_int("QLDPC_M2S_PLACE", 1) != 0);
+                     bp->m2s == 1 && env_int("QLDPC_M2S_PLACE", 1) != 0);
+    if (bp->m2s == 3) {
+      // m2v row table (bp_reg.h M2vRows): row i = q * TB + t -> uint4 (q * TB + t): the byte offsets
+      // from the V base of its edges' variable-major slots, two 16-bit offsets per word, the unused
+      // entries at the sentinel slot
+      const int TBm = bp->TB, VPLm = bp->VPL, d3 = std::min(bp->d3k, VPLm);
+      auto ecnt = [&](int k) { return 3 * std::min(k, d3) + 4 * std::max(0, k - d3); };
+      if (ecnt(VPLm - 1) * TBm != bp->m2v_vlast) return fail(set_err(QLDPC_ENOTSUP, "m2v layout mismatch"));
+      const uint32_t sent = (uint32_t)(bp->vslots_m2v - 1) * 8u;
+      std::vector<std::vector<uint32_t>> roff(g->m);
+      for (int k = 0; k < VPLm; ++k)
+        for (int t = 0; t < TBm; ++t) {
+          const int j = bp->slot_var[(size_t)k * TBm + t];
+          if (j < 0) continue;
+          const auto& rows = g->col_rows[j];
+          for (int d = 0; d < (int)rows.size(); ++d) {
+            const int vs = k < VPLm - 1 ? (ecnt(k) + d) * TBm + t : bp->m2v_vlast + d * bp->m2v_nl + t;
+            roff[rows[d]].push_back((uint32_t)vs * 8u);
+          }
+        }
+      for (int i = 0; i < g->m; ++i) {
+        if (roff[i].size() > 7) return fail(set_err(QLDPC_ENOTSUP, "m2v row wider than 7"));
+        while (roff[i].size() < 8) roff[i].push_back(sent);
+      }
+      // The check phase gathers entry e of its rows with one ds_read_b64 per e: 32-lane groups,
+      // bank pair = slot mod 32 (MI355X_MICROARCH.md §LDS).  The order of a row's entries is
+      // free: per group of 32 rows, a seeded local search swaps two entries of a row whenever that
+      // does not raise Σ_e Σ_bank count² (the sentinel broadcasts: not counted).  Host work only.
+      if (env_int("QLDPC_M2V_ORDER", 1) != 0) {
+        uint64_t rs = 0x9E3779B97F4A7C15ull;
+        auto rnd = [&]() { rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17; return rs; };
+        for (int q = 0; q < 4; ++q)
+          for (int g0 = 0; g0 < TBm; g0 += 32) {
+            std::vector<int> rr;
+            for (int l = 0; l < 32; ++l)
+              if (q * TBm + g0 + l < g->m) rr.push_back(q * TBm + g0 + l);
+            if (rr.size() < 2) continue;
+            int cnt[7][32] = {{0}};
+            auto bk = [&](uint32_t o) { return (int)((o / 8u) % 32u); };
+            for (int i : rr)
+              for (int e = 0; e < 7; ++e)
+                if (roff[i][e] != sent) cnt[e][bk(roff[i][e])]++;
+            for (int it = 0; it < 4000; ++it) {
+              const int i = rr[rnd() % rr.size()], a = (int)(rnd() % 7), b = (int)(rnd() % 7);
+              const uint32_t oa = roff[i][a], ob = roff[i][b];
+              if (a == b || oa == ob) continue;
+              auto term = [&](int e, uint32_t o, int dlt) {  // change of count^2 when o enters (+1) / leaves (-1) e
+                if (o == sent) return 0;
+                const int c = cnt[e][bk(o)];
+                return dlt > 0 ? 2 * c + 1 : -(2 * c - 1);
+              };
+              int d = term(a, oa, -1);
+              if (oa != sent) cnt[a][bk(oa)]--;
+              d += term(b, ob, -1);
+              if (ob != sent) cnt[b][bk(ob)]--;
+              d += term(a, ob, +1);
+              if (ob != sent) cnt[a][bk(ob)]++;
+              d += term(b, oa, +1);
+              if (oa != sent) cnt[b][bk(oa)]++;
+              if (d <= 0) {
+                roff[i][a] = ob;
+                roff[i][b] = oa;
+              } else {  // undo
+                if (ob != sent) cnt[a][bk(ob)]--;
+                if (oa != sent) cnt[b][bk(oa)]--;
+                if (oa != sent) cnt[a][bk(oa)]++;
+                if (ob != sent) cnt[b][bk(ob)]++;
+              }
+            }
+          }
+      }
+      std::vector<uint32_t> tab((size_t)4 * TBm * 4, 0);
+      for (int q = 0; q < 4; ++q)
+        for (int t = 0; t < TBm; ++t) {
+          const int i = q * TBm + t;
+          uint32_t o[8];
+          for (int e = 0; e < 8; ++e) o[e] = i < g->m ? roff[i][e] : sent;
+          for (int w = 0; w < 4; ++w) tab[((size_t)q * TBm + t) * 4 + w] = o[2 * w] | (o[2 * w + 1] << 16);
+        }
+      if ((rc = bp->rowtab.alloc(tab.size() * 4))) return fail(rc);
+      if (hipMemcpy(bp->rowtab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(set_err(QLDPC_EHIP, "upload m2v row table"));
+    }
     kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch, bp->tail,
                         bp->m2s, bp->fb, bp->d2k).dec_k;
     if (bp->engine >= 3) {
@@ -996,7 +1096,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
 
 int qldpc_bp_destroy(qldpc_bp* bp) {
   if (!bp) return 0;
-  for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->perm, &bp->rperm, &bp->work, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp,
+  for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->rowtab, &bp->perm, &bp->rperm, &bp->work, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp,
                     &bp->ps_ce, &bp->ps_ws, &bp->h_rp, &bp->h_rcol, &bp->h_rcpos, &bp->h_cp, &bp->h_crpos, &bp->h_ws})
     d->release();
   delete bp;
@@ -1032,7 +1132,7 @@ int qldpc_bp_kernel_id(const qldpc_bp* bp, int32_t* kernel_id, int32_t* row_chun
   int id = bp->engine;
   if (bp->engine == 3) {
     if (bp->m2s)
-      id = bp->m2s == 2 ? 31103 : 11103;
+      id = bp->m2s == 2 ? 31103 : bp->m2s == 3 ? 40103 : 11103;
     else if (bp->fb)
       id = 21013 + ((bp->d3k >= 8 && bp->d2k > 0) ? 100000 * std::min(bp->d2k, 4) : 0);  // + D2K digit
     else if (bp->tail)
@@ -1094,6 +1194,9 @@ static SSector ssector_of(const qldpc_bp* bp, const unsigned long long* lmask, i
   s.nch = bp->nch;
   s.vpl = bp->VPL;
   s.alpha = bp->alpha;
+  s.rows = static_cast<const uint32_t*>(bp->rowtab.p);
+  s.vlast = bp->m2v_vlast;
+  s.vnl = bp->m2v_nl;
   return s;
 }
 
@@ -1151,7 +1254,7 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     a.conv = d_conv;
     a.B = B;
     a.mmax = bp->g->m;
-    a.vslots = (1 + bp->g->m * bp->nch) * (16 / tsize);
+    a.vslots = bp->vslots_m2v ? bp->vslots_m2v : (1 + bp->g->m * bp->nch) * (16 / tsize);
     a.img_bytes = (int)slot_img_bytes(a.vslots, a.mmax, tsize);
     a.chunk = chunk_for(B, cap, bp->NS);
     a.work = nullptr;
@@ -1198,6 +1301,8 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
                       // the fused kernel runs one layout family for both sectors
                       (dec_x && dec_z &&
                        (dec_x->m2s != dec_z->m2s || dec_x->tail != dec_z->tail || dec_x->fb != dec_z->fb)) ||
+                      // m2v: the kernel's compile-time D3K sets both sectors' V layouts
+                      (dec_x && dec_z && dec_x->m2s == 3 && dec_x->d3k != dec_z->d3k) ||
                       env_int("QLDPC_MC_STAGED", 0) == 1;
   if (staged) {  // staged pipeline around decode_batch (staged.hip): any decoder pair
     if (dec_x && dec_z && (dec_x->g->n != dec_z->g->n || dec_x->g->device != dec_z->g->device))
@@ -1269,7 +1374,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   } else {
     const int tsize = mc->precision == 32 ? 4 : 8;
     for (qldpc_bp* d : {dec_x, dec_z})
-      if (d) mc->vslots = std::max(mc->vslots, (1 + d->g->m * d->nch) * (16 / tsize));
+      if (d) mc->vslots = std::max(mc->vslots, d->vslots_m2v ? d->vslots_m2v : (1 + d->g->m * d->nch) * (16 / tsize));
     mc->img_bytes = (int)slot_img_bytes(mc->vslots, mc->mmax, tsize);
     if (mc->engine >= 3) {
       if (!r_fits(mc->engine, mc->vslots, mc->mmax, tsize, mc->ea_shift, mc->tail, mc->m2s, mc->fb))

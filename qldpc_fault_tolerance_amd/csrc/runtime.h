@@ -63,6 +63,9 @@ struct qldpc_bp {
   std::vector<double> probs;
   qldpc_rt::DevBuf vchk, llr;  // engine 1: packed u16 check ids; engines 2-4: edge words (check | slot<<16)
   qldpc_rt::DevBuf rdeg;       // engines 3/4: u8 row degrees (by check label)
+  qldpc_rt::DevBuf rowtab;     // m2v: the check phase's row table [kM2vRows][TB] x 4 u32
+  int vslots_m2v = 0;          // m2v: V slots of the variable-major layout (0 = row-major formula)
+  int m2v_vlast = 0, m2v_nl = 0;  // m2v: first V slot of the last variable slot, its per-edge stride
   qldpc_rt::DevBuf work;       // engine 3 decode_batch: chunk-queue head
   // engines 3/4: variable of each (k, t) slot (-1 = padding).  Engine 3 sorts
   // degree <= 3 variables first so that slots k < d3k skip the 4th edge slot.
@@ -75,6 +78,7 @@ struct qldpc_bp {
   int ea_shift = 0;  // engine 3: 2 = dword-scaled LDS addresses in the edge words (images > 64 KiB)
   int tail = 0;      // engine 3: 1 = rows of nch chunks + one tail slot per row (bp_reg.h eng_tail)
   int m2s = 0;       // engine 3: 1 = one-word check state, m2 in the argmin slot (bp_reg.h eng_m2s);
+                     // 3 = the same with variable-major V slots (eng_m2v);
                      // 2 = c2v written into the slots by the check phase (eng_c2s)
   int fb = 0;        // engine 3: 1 = byte F words (fp32 space-time family, 512 threads; bp_reg.h eng_fb)
   // engine 5 (product-sum, bp_ps.hip): CSR / CSC on the device, optional HBM message workspace

@@ -1,5 +1,6 @@
-"""The fp64 one-slot families against the oracle: "c2v in slot" (engine id 31103, bp_reg.h
-eng_c2s, the default for the headline graphs) and "m2 in slot" (11103, eng_m2s, QLDPC_C2S=0).
+"""The fp64 one-slot families against the oracle: "m2 in slot" (engine id 11103, bp_reg.h eng_m2s,
+the default for the headline graphs), "c2v in slot" (31103, eng_c2s, QLDPC_C2S=1) and m2s with
+variable-major V slots (40103, eng_m2v, QLDPC_M2V=1).
 
 The headline graphs (hgp_34_n1600 hz / hx: rows of exactly 7, column degrees 3 / 4 with the
 degree-3 variables filling 4 whole slots of 256 lanes) run in float64 with rows of 3 chunks + a
@@ -25,10 +26,10 @@ def _synd(H, p, B, seed):
     return (e.astype(np.int64) @ H.T.astype(np.int64) % 2).astype(np.uint8)
 
 
-def _dec(H, probs, mi, alpha=0.625, m2s=True, vpl=0, c2s=True):
+def _dec(H, probs, mi, alpha=0.625, m2s=True, vpl=0, c2s=True, m2v=False):
     from qldpc_fault_tolerance_amd.engine import DeviceBP
 
-    env = {"QLDPC_M2S": "1" if m2s else "0", "QLDPC_C2S": "1" if c2s else "0"}
+    env = {"QLDPC_M2S": "1" if m2s else "0", "QLDPC_C2S": "1" if c2s else "0", "QLDPC_M2V": "1" if m2v else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -52,6 +53,8 @@ def test_headline_graphs_select_c2s_family(gpu):
         assert g1["kernel_id"] == 11103 and g1["blocks_per_cu"] == 3 and g1["lds_bytes"] > g["lds_bytes"], (g1, g)
         g0 = _dec(H, 0.06, 160, m2s=False).geometry()
         assert g0["kernel_id"] == 103 and g0["blocks_per_cu"] == 2, g0
+        g2 = _dec(H, 0.06, 160, c2s=False, m2v=True).geometry()  # variable-major V slots
+        assert g2["kernel_id"] == 40103 and g2["blocks_per_cu"] == 3, g2
     # outside the envelope (mixed-degree slots: n225's 144 degree-3 variables over 64 lanes) -> two-word family
     assert _dec(codes.get_code("hgp_34_n225").hz, 0.05, 22).geometry()["kernel_id"] not in (11103, 31103)
 
@@ -67,24 +70,25 @@ def test_m2s_decode_matches_oracle(gpu, oracle, sector, p):
     c, i, v = _dec(H, p, 160).decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, p, 160, "minimum_sum", 0.625, synd, 64)
     assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64))
-    for kw in ({"c2s": False}, {"m2s": False}):
+    for kw in ({"c2s": False}, {"m2s": False}, {"c2s": False, "m2v": True}):
         c0, i0, v0 = _dec(H, p, 160, **kw).decode_batch(synd)
         assert np.array_equal(c, c0) and np.array_equal(i, i0) and np.array_equal(v, v0), kw
 
 
-@pytest.mark.parametrize("c2s", [True, False])
-def test_m2s_adaptive_alpha_and_zero_priors_match_oracle(gpu, oracle, c2s):
+@pytest.mark.parametrize("fam", ["c2s", "m2s", "m2v"])
+def test_m2s_adaptive_alpha_and_zero_priors_match_oracle(gpu, oracle, fam):
     """Adaptive alpha and all-zero priors on the c2s / m2s families; non-uniform priors take the
-    two-word family (both keep one prior in SGPRs: QLDPC_M2S_UNIL)."""
+    two-word family (all keep one prior in SGPRs: QLDPC_M2S_UNIL)."""
+    c2s, m2v = fam == "c2s", fam == "m2v"
     code = codes.get_code("hgp_34_n1600")
     H = code.hz
     synd = _synd(H, 0.05, 256, seed=5)
-    c, i, v = _dec(H, 0.05, 60, alpha=0.0, c2s=c2s).decode_batch(synd)
+    c, i, v = _dec(H, 0.05, 60, alpha=0.0, c2s=c2s, m2v=m2v).decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, 0.05, 60, "minimum_sum", 0.0, synd, 64)
     assert np.array_equal(c, oc.astype(np.int64)) and np.array_equal(i, oi) and np.array_equal(v, ov)
     # every prior zero (p = 0.5): messages that are exactly +-0 on the one-prior kernels
-    dec = _dec(H, 0.5, 12, c2s=c2s)
-    assert dec.geometry()["kernel_id"] == (31103 if c2s else 11103)
+    dec = _dec(H, 0.5, 12, c2s=c2s, m2v=m2v)
+    assert dec.geometry()["kernel_id"] == {"c2s": 31103, "m2s": 11103, "m2v": 40103}[fam]
     c, i, v = dec.decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, 0.5, 12, "minimum_sum", 0.625, synd, 64)
     assert np.array_equal(c, oc.astype(np.int64)) and np.array_equal(i, oi) and np.array_equal(v, ov)
@@ -92,21 +96,22 @@ def test_m2s_adaptive_alpha_and_zero_priors_match_oracle(gpu, oracle, c2s):
     rng = np.random.default_rng(3)
     probs = np.full(code.N, 0.04)
     probs[rng.random(code.N) < 0.3] = 0.5
-    dec = _dec(H, probs, 40, c2s=c2s)
+    dec = _dec(H, probs, 40, c2s=c2s, m2v=m2v)
     assert dec.geometry()["kernel_id"] == 103
     c, i, v = dec.decode_batch(synd)
     oc, oi, ov = oracle.bp_decode_batch(H, probs, 40, "minimum_sum", 0.625, synd, 64)
     assert np.array_equal(c, oc.astype(np.int64)) and np.array_equal(i, oi) and np.array_equal(v, ov)
 
 
-@pytest.mark.parametrize("c2s", [True, False])
-def test_m2s_fused_mc_matches_oracle_per_shot(gpu, oracle, c2s):
+@pytest.mark.parametrize("fam", ["c2s", "m2s", "m2v"])
+def test_m2s_fused_mc_matches_oracle_per_shot(gpu, oracle, fam):
     from qldpc_fault_tolerance_amd.engine import DeviceMC
 
     code = codes.get_code("hgp_34_n1600")
     n, p, S = code.N, 0.07, 400
-    dx, dz = _dec(code.hz, p, 160, c2s=c2s), _dec(code.hx, p, 160, vpl=7, c2s=c2s)
-    assert dx.geometry()["kernel_id"] == dz.geometry()["kernel_id"] == (31103 if c2s else 11103)
+    c2s, m2v = fam == "c2s", fam == "m2v"
+    dx, dz = _dec(code.hz, p, 160, c2s=c2s, m2v=m2v), _dec(code.hx, p, 160, vpl=7, c2s=c2s, m2v=m2v)
+    assert dx.geometry()["kernel_id"] == dz.geometry()["kernel_id"] == {"c2s": 31103, "m2s": 11103, "m2v": 40103}[fam]
     res = DeviceMC(code, dx, dz).run(p / 2, p / 2, p / 2, 0x51D5EED2, 777, S, "Total", per_shot=True)
     ref = oracle.mc_run(code, p / 2, p / 2, p / 2, seed=0x51D5EED2, shot_begin=777, shot_count=S, logical_mode="Total",
                         max_iter=160, precision=64, per_shot=True)
