@@ -1,0 +1,13 @@
+#!/bin/bash
+# Closing check of the final tree: smoke(), the GPU suite, the default bench line.
+set -u
+R=$(cd "$(dirname "$0")/.." && pwd)
+O=$R/gpurun_out/r03_closing
+mkdir -p "$O"
+cd "$R" || exit 1
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { tail -20 "$O/smoke.log"; exit 1; }
+tail -2 "$O/smoke.log"
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 || { tail -30 "$O/pytest_gpu.log"; exit 1; }
+tail -2 "$O/pytest_gpu.log"
+timeout -k 10 400 python3 -u bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail "$O/bench.err"; exit 1; }
+python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print('bench', round(d['value']), round(r['frac'],4), r['kernel_ms'], r['traffic'], d['cpu_baseline']['value'])" "$O/bench.json"
