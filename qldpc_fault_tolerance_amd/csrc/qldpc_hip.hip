@@ -449,6 +449,78 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
             lslot[edge_of(i, j)] = best;
           }
         }
+    // Then a seeded annealed local search over the rows' slot permutations: swap the positions of
+    // two edges of one row (or move one into a free position) when Σ_read groups Σ_bank count²
+    // (weight 4: ds_read_b64, 32-lane groups, slot mod 32) + Σ_store groups Σ_bank count² (weight
+    // 1: ds_write_b64, 16-lane groups, slot mod 16) does not rise by more than the temperature.
+    const int iters = env_int("QLDPC_M2S_ANNEAL", 0);  // (opt-in until measured)
+    if (iters > 0) {
+      const int nrg = VPL * DM * ((TB + 31) / 32), nwg = VPL * DM * ((TB + 15) / 16);
+      std::vector<int> erg(g->nnz, -1), ewg(g->nnz, -1);
+      for (int k = 0; k < VPL; ++k)
+        for (int t = 0; t < TB; ++t) {
+          const int j = slot_var[(size_t)k * TB + t];
+          if (j < 0) continue;
+          const auto& rows = g->col_rows[j];
+          for (int d = 0; d < (int)rows.size() && d < DM; ++d) {
+            const int e = edge_of(rows[d], j);
+            erg[e] = (k * DM + d) * ((TB + 31) / 32) + t / 32;
+            ewg[e] = (k * DM + d) * ((TB + 15) / 16) + t / 16;
+          }
+        }
+      std::vector<int> rc((size_t)nrg * 32, 0), wc((size_t)nwg * 16, 0);
+      // position -> edge per row (-1 = free)
+      std::vector<int> at((size_t)g->m * rwt, -1);
+      for (int i = 0; i < g->m; ++i)
+        for (int e = g->row_ptr[i]; e < g->row_ptr[i + 1]; ++e) {
+          at[(size_t)i * rwt + lslot[e]] = e;
+          if (erg[e] < 0) continue;
+          const int sl = vbase_u + phys(i, lslot[e]);
+          rc[(size_t)erg[e] * 32 + sl % 32]++;
+          wc[(size_t)ewg[e] * 16 + sl % 16]++;
+        }
+      auto put = [&](int e, int sl, int sg) {
+        rc[(size_t)erg[e] * 32 + sl % 32] += sg;
+        wc[(size_t)ewg[e] * 16 + sl % 16] += sg;
+      };
+      auto ins = [&](int e, int sl) {  // cost of inserting edge e at slot sl (counts without it)
+        return 4 * (2 * rc[(size_t)erg[e] * 32 + sl % 32] + 1) + (2 * wc[(size_t)ewg[e] * 16 + sl % 16] + 1);
+      };
+      uint64_t rs = 0x2545F4914F6CDD1Dull;
+      auto rnd = [&]() { rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17; return rs; };
+      for (int it = 0; it < iters; ++it) {
+        const int i = (int)(rnd() % (uint64_t)g->m);
+        const int a = (int)(rnd() % (uint64_t)rwt), b = (int)(rnd() % (uint64_t)rwt);
+        if (a == b) continue;
+        const int ea = at[(size_t)i * rwt + a], eb = at[(size_t)i * rwt + b];
+        if ((ea < 0 || erg[ea] < 0) && (eb < 0 || erg[eb] < 0)) continue;
+        if ((ea >= 0 && erg[ea] < 0) || (eb >= 0 && erg[eb] < 0)) continue;
+        const int sa = vbase_u + phys(i, a), sb = vbase_u + phys(i, b);
+        // exact change of the objective: both edges out, then each configuration inserted one
+        // edge after the other
+        if (ea >= 0) put(ea, sa, -1);
+        if (eb >= 0) put(eb, sb, -1);
+        long long before = 0, after = 0;
+        if (ea >= 0) { before += ins(ea, sa); put(ea, sa, +1); }
+        if (eb >= 0) before += ins(eb, sb);
+        if (ea >= 0) put(ea, sa, -1);
+        if (ea >= 0) { after += ins(ea, sb); put(ea, sb, +1); }
+        if (eb >= 0) after += ins(eb, sa);
+        if (ea >= 0) put(ea, sb, -1);
+        const double T = 6.0 * (1.0 - (double)it / iters);
+        const long long dlt = after - before;
+        const bool take = dlt <= 0 || (T > 0 && (double)(rnd() % 1000000) / 1e6 < std::exp(-(double)dlt / T));
+        if (take) {
+          if (ea >= 0) { put(ea, sb, +1); lslot[ea] = b; }
+          if (eb >= 0) { put(eb, sa, +1); lslot[eb] = a; }
+          at[(size_t)i * rwt + a] = eb;
+          at[(size_t)i * rwt + b] = ea;
+        } else {
+          if (ea >= 0) put(ea, sa, +1);
+          if (eb >= 0) put(eb, sb, +1);
+        }
+      }
+    }
   } else if (vbase_dw >= 0 && rwt <= 32) {
     std::vector<uint32_t> used(g->m, 0u);
     for (int k = 0; k < VPL; ++k)
