@@ -61,6 +61,12 @@ int qldpc_abi_version(void);
 const char *qldpc_last_error(void);
 int qldpc_device_count(int *out);
 
+/* Build flags of this library: QLDPC_BUILD_EXPERIMENTAL when the measured-and-not-kept kernel
+ * families (c2s 31103, m2v 40103, fp64 257-512 threads 303, engine 4) are compiled in
+ * (-DQLDPC_EXPERIMENTAL=1); the product build leaves them out and ignores their opt-ins. */
+#define QLDPC_BUILD_EXPERIMENTAL 1
+int qldpc_build_flags(void);
+
 /*
  * Tanner graph of a parity-check matrix H (m x n), CSR with columns ascending
  * inside each row (the `mod2sparse` order `ldpc` builds from the ndarray it is
@@ -316,8 +322,11 @@ int qldpc_comm_destroy(qldpc_comm *comm);
  * sizes S/ndev or S/ndev + 1, the first S%ndev devices one longer: the split of
  * parallel.shard_range), the counters are summed
  * with one grouped all-reduce (comms from qldpc_comm_init_all, in the same
- * device order) or, with comms NULL, on the host; the sum is added to *out.
- * Synchronous.
+ * device order: comms[d] must be rank d of ndev, on MC handle d's device, else
+ * QLDPC_EINVAL; per-process qldpc_comm_init_rank communicators are refused) or,
+ * with comms NULL, on the host; the sum is added to *out.  Each device is
+ * driven from its own host thread (BP+OSD launches are synchronous).
+ * Synchronous.  The ndev > 1 RCCL path has not yet run on a multi-GPU node.
  * Shots keyed by global index: the totals do not depend on ndev.
  */
 int qldpc_mc_run_sharded(qldpc_mc **mcs, qldpc_comm **comms, int32_t ndev, double px, double py, double pz,

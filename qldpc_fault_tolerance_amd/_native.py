@@ -26,8 +26,9 @@ EXPORTED = [
     "qldpc_bp_bank_stats", "qldpc_bp_create_hbm", "qldpc_mc_set_osd", "qldpc_comm_unique_id",
     "qldpc_comm_init_rank", "qldpc_comm_init_all", "qldpc_comm_rank", "qldpc_comm_allreduce_counters",
     "qldpc_comm_allreduce_counters_group", "qldpc_comm_destroy", "qldpc_mc_run_sharded", "qldpc_sample_errors",
-    "qldpc_stream_sync", "qldpc_bp_kernel_id",
+    "qldpc_stream_sync", "qldpc_bp_kernel_id", "qldpc_build_flags",
 ]
+BUILD_EXPERIMENTAL = 1  # qldpc_build_flags(): the measured-and-not-kept kernel families are compiled in
 COMM_ID_BYTES = 128
 
 
@@ -159,6 +160,8 @@ def _declare(L):
     L.qldpc_bp_kernel_id.argtypes = [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]
     L.qldpc_stream_sync.restype = ctypes.c_int
     L.qldpc_stream_sync.argtypes = [_vp]
+    L.qldpc_build_flags.restype = ctypes.c_int
+    L.qldpc_build_flags.argtypes = []
 
 
 def lib():
@@ -186,6 +189,12 @@ def check(rc: int, what: str = "") -> None:
     if rc != 0:
         msg = lib().qldpc_last_error().decode(errors="replace")
         raise QldpcError(f"{what} failed (rc={rc}): {msg}")
+
+
+def experimental_families() -> bool:
+    """True when the library carries the opt-in c2s / m2v / 303 / engine-4 kernels
+    (built with ``-DQLDPC_EXPERIMENTAL=1``, e.g. ``tools/build_variant.py``)."""
+    return bool(lib().qldpc_build_flags() & BUILD_EXPERIMENTAL)
 
 
 def device_count() -> int:

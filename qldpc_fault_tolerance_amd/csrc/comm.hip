@@ -21,6 +21,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/qldpc_hip.h"
@@ -214,42 +215,62 @@ int qldpc_mc_run_sharded(qldpc_mc** mcs, qldpc_comm** comms, int32_t ndev, doubl
                          uint64_t seed, uint64_t shot_begin, int64_t shot_count, int32_t logical_mode,
                          qldpc_counters* out) {
   if (!mcs || !out || ndev < 1 || shot_count < 0) return set_err(QLDPC_EINVAL, "bad argument");
+  std::vector<int> devs(ndev, 0);
+  for (int d = 0; d < ndev; ++d) {
+    if (!mcs[d] || !(mcs[d]->dec[0] || mcs[d]->dec[1])) return set_err(QLDPC_EINVAL, "NULL MC handle");
+    devs[d] = (mcs[d]->dec[0] ? mcs[d]->dec[0] : mcs[d]->dec[1])->g->device;
+    // only qldpc_comm_init_all communicators, in device order: rank d of ndev on MC handle d's
+    // device (per-process init_rank communicators would sum other processes' counters into
+    // shot blocks split by ndev, not by global rank)
+    if (comms && (!comms[d] || comms[d]->nranks != ndev || comms[d]->rank != d))
+      return set_err(QLDPC_EINVAL, "comms[d] must be rank d of an ndev-rank qldpc_comm_init_all communicator");
+    if (comms && comms[d]->device != devs[d])
+      return set_err(QLDPC_EINVAL, "MC handle d and communicator d are on different devices");
+  }
   std::vector<void*> cnt(ndev, nullptr), streams(ndev, nullptr);
+  std::vector<int> rcs(ndev, 0);
+  std::vector<std::string> why(ndev);
   auto cleanup = [&] {
     for (int d = 0; d < ndev; ++d) {
+      (void)hipSetDevice(devs[d]);
       if (cnt[d]) (void)hipFree(cnt[d]);
       if (streams[d]) (void)hipStreamDestroy((hipStream_t)streams[d]);
     }
   };
-  // device d owns a contiguous block of global shots (parallel.shard_range)
-  for (int d = 0; d < ndev; ++d) {
-    if (!mcs[d] || !(mcs[d]->dec[0] || mcs[d]->dec[1])) {
-      cleanup();
-      return set_err(QLDPC_EINVAL, "NULL MC handle");
-    }
-    const int dev = (mcs[d]->dec[0] ? mcs[d]->dec[0] : mcs[d]->dec[1])->g->device;
-    if (comms && comms[d]->device != dev) {
-      cleanup();
-      return set_err(QLDPC_EINVAL, "MC handle d and communicator d are on different devices");
-    }
-    hipError_t e = hipSetDevice(dev);
+  // device d owns a contiguous block of global shots (parallel.shard_range).  Each device is
+  // driven from its own host thread: with BP+OSD (qldpc_mc_set_osd) a launch is synchronous
+  // (it reads the OSD candidate counts back), so one thread would run the devices one after
+  // another.
+  auto run_one = [&](int d) {
+    hipError_t e = hipSetDevice(devs[d]);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(reinterpret_cast<hipStream_t*>(&streams[d]), hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&cnt[d], sizeof(qldpc_counters));
     if (e == hipSuccess) e = hipMemsetAsync(cnt[d], 0, sizeof(qldpc_counters), (hipStream_t)streams[d]);
     if (e != hipSuccess) {
-      cleanup();
-      return set_err(QLDPC_EHIP, std::string("qldpc_mc_run_sharded setup: ") + hipGetErrorString(e));
+      rcs[d] = QLDPC_EHIP;
+      why[d] = std::string("qldpc_mc_run_sharded setup: ") + hipGetErrorString(e);
+      return;
     }
     // parallel.shard_range: blocks of base or base + 1 shots, the first `extra` ranks one longer
     const int64_t base = shot_count / ndev, extra = shot_count % ndev;
     const int64_t lo = d * base + std::min<int64_t>(d, extra), cnt_d = base + (d < extra ? 1 : 0);
-    int rc = qldpc_mc_launch(mcs[d], px, py, pz, seed, shot_begin + (uint64_t)lo, cnt_d, logical_mode, nullptr, cnt[d],
+    rcs[d] = qldpc_mc_launch(mcs[d], px, py, pz, seed, shot_begin + (uint64_t)lo, cnt_d, logical_mode, nullptr, cnt[d],
                              nullptr, nullptr, nullptr, nullptr, 0, streams[d]);
-    if (rc) {
-      cleanup();
-      return rc;
-    }
+    if (rcs[d]) why[d] = qldpc_last_error();  // thread-local: carried to the caller's thread
+  };
+  if (ndev == 1) {
+    run_one(0);
+  } else {
+    std::vector<std::thread> th;
+    th.reserve(ndev);
+    for (int d = 0; d < ndev; ++d) th.emplace_back(run_one, d);
+    for (auto& t : th) t.join();
   }
+  for (int d = 0; d < ndev; ++d)
+    if (rcs[d]) {
+      cleanup();
+      return set_err(rcs[d], why[d]);
+    }
   if (ndev > 1 && comms) {
     int rc = qldpc_comm_allreduce_counters_group(comms, cnt.data(), streams.data(), ndev);
     if (rc) {
@@ -262,10 +283,13 @@ int qldpc_mc_run_sharded(qldpc_mc** mcs, qldpc_comm** comms, int32_t ndev, doubl
   std::vector<qldpc_counters> c(nread);
   hipError_t e = hipSuccess;
   for (int d = 0; d < nread && e == hipSuccess; ++d) {
-    e = hipSetDevice((mcs[d]->dec[0] ? mcs[d]->dec[0] : mcs[d]->dec[1])->g->device);
+    e = hipSetDevice(devs[d]);
     if (e == hipSuccess) e = hipMemcpyAsync(&c[d], cnt[d], sizeof(qldpc_counters), hipMemcpyDeviceToHost, (hipStream_t)streams[d]);
   }
-  for (int d = 0; d < ndev && e == hipSuccess; ++d) e = hipStreamSynchronize((hipStream_t)streams[d]);
+  for (int d = 0; d < ndev && e == hipSuccess; ++d) {
+    e = hipSetDevice(devs[d]);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)streams[d]);
+  }
   cleanup();
   if (e != hipSuccess) return set_err(QLDPC_EHIP, std::string("qldpc_mc_run_sharded: ") + hipGetErrorString(e));
   int64_t* dst = reinterpret_cast<int64_t*>(out);

@@ -4,6 +4,7 @@
 #include "variants.h"
 
 namespace qldpc {
+#if QLDPC_EXPERIMENTAL
 SVariant get_r4variant_f64(int vpl) { return pick_rvpl<double, 4>(vpl); }
 SVariant get_r4variant_f64_w(int vpl) {
   switch (vpl) {
@@ -15,4 +16,9 @@ SVariant get_r4variant_f64_w(int vpl) {
     default: return SVariant{nullptr, nullptr, nullptr, nullptr};
   }
 }
+#else
+// measured-and-not-kept family: built only with -DQLDPC_EXPERIMENTAL=1 (tools/build_variant.py)
+SVariant get_r4variant_f64(int vpl) { return SVariant{nullptr, nullptr, nullptr, nullptr}; }
+SVariant get_r4variant_f64_w(int vpl) { return SVariant{nullptr, nullptr, nullptr, nullptr}; }
+#endif
 }  // namespace qldpc

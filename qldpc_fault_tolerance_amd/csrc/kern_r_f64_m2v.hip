@@ -7,6 +7,7 @@
 #include "variants.h"
 
 namespace qldpc {
+#if QLDPC_EXPERIMENTAL
 SVariant get_rvariant_f64_m2v(int vpl, int d3k) {
   switch (vpl) {
     case 4: return pick_rd3k<double, 4, 40103, 4, 256, 3>(d3k);
@@ -17,4 +18,8 @@ SVariant get_rvariant_f64_m2v(int vpl, int d3k) {
     default: return SVariant{nullptr, nullptr, nullptr, nullptr};
   }
 }
+#else
+// measured-and-not-kept family: built only with -DQLDPC_EXPERIMENTAL=1 (tools/build_variant.py)
+SVariant get_rvariant_f64_m2v(int vpl, int d3k) { return SVariant{nullptr, nullptr, nullptr, nullptr}; }
+#endif
 }  // namespace qldpc

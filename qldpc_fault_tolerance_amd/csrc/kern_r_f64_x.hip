@@ -5,6 +5,7 @@
 #include "variants.h"
 
 namespace qldpc {
+#if QLDPC_EXPERIMENTAL
 SVariant get_rvariant_f64_x(int vpl, int d3k) {
   switch (vpl) {
     case 3: return pick_rd3k<double, 3, 303, 4, 512, 0>(d3k);
@@ -12,4 +13,8 @@ SVariant get_rvariant_f64_x(int vpl, int d3k) {
     default: return SVariant{nullptr, nullptr, nullptr, nullptr};
   }
 }
+#else
+// measured-and-not-kept family: built only with -DQLDPC_EXPERIMENTAL=1 (tools/build_variant.py)
+SVariant get_rvariant_f64_x(int vpl, int d3k) { return SVariant{nullptr, nullptr, nullptr, nullptr}; }
+#endif
 }  // namespace qldpc

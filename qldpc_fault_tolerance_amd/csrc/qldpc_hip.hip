@@ -94,7 +94,7 @@ unsigned long long* debug_stamps_buffer() {
 // fp64 engine-3 kernels for 257-512-thread workgroups (engine id 303, VPL 3-4); opt-in QLDPC_F64X=1
 bool use_f64x(int engine, int precision, int dmax, int tb, int vpl, int ea_shift) {
   return engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && tb > 256 && tb <= 512 && vpl >= 3 &&
-         vpl <= 4 && env_int("QLDPC_F64X", 0) != 0;
+         vpl <= 4 && QLDPC_EXPERIMENTAL && env_int("QLDPC_F64X", 0) != 0;
 }
 
 // Slot-family kernels of an engine (2, 3 or 4).
@@ -265,6 +265,8 @@ int qldpc_debug_stamps(unsigned long long* out) {
 int qldpc_abi_version(void) { return QLDPC_ABI_VERSION; }
 
 const char* qldpc_last_error(void) { return qldpc_rt::g_err.c_str(); }
+
+int qldpc_build_flags(void) { return QLDPC_EXPERIMENTAL ? QLDPC_BUILD_EXPERIMENTAL : 0; }
 
 int qldpc_device_count(int* out) {
   if (!out) return set_err(QLDPC_EINVAL, "out is NULL");
@@ -795,6 +797,8 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
   QLDPC_HIP(hipSetDevice(g->device));
   if (bp_method == QLDPC_PRODUCT_SUM) return create_ps(g, channel_probs, max_iter, precision, out);
   const int want_engine = forced_engine ? forced_engine : env_int("QLDPC_ENGINE", 3);
+  if (want_engine == 4 && !QLDPC_EXPERIMENTAL)
+    return set_err(QLDPC_ENOTSUP, "engine 4 is built only with -DQLDPC_EXPERIMENTAL=1 (tools/build_variant.py)");
   auto* bp = new qldpc_bp();
   bp->g = g;
   bp->engine = ((want_engine >= 1 && want_engine <= 4) || want_engine == 6) ? want_engine : 3;
@@ -934,7 +938,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         // (profiles/r03/c2s/), so m2s stays the default
         bool full = true;
         for (int i = 0; i < g->m && full; ++i) full = g->row_ptr[i + 1] - g->row_ptr[i] == 7;
-        if (full && env_int("QLDPC_C2S", 0) != 0 && r_fits(3, (1 + g->m * 3) * 2, g->m, 8, 0, 1, 2)) bp->m2s = 2;
+        if (full && QLDPC_EXPERIMENTAL && env_int("QLDPC_C2S", 0) != 0 && r_fits(3, (1 + g->m * 3) * 2, g->m, 8, 0, 1, 2)) bp->m2s = 2;
         // variable-major V slots (bp_reg.h eng_m2v, kern_r_f64_m2v.hip): edge (k, d) of lane t at
         // slot (ecnt(k) + d) * 256 + t, the last variable slot at ecnt * 256 + d * NL + t, then one
         // sentinel slot; the check phase's rows come from a register table (m <= 4 * 256)
@@ -942,7 +946,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         const int nlast = g->n - (vpl - 1) * 256, NL = (nlast + 63) & ~63;
         const int ecl = 3 * std::min(vpl - 1, d3) + 4 * std::max(0, vpl - 1 - d3);
         const int vm = ecl * 256 + (vpl - 1 < d3 ? 3 : 4) * NL + 1;
-        if (bp->m2s == 1 && tb == 256 && g->m <= 4 * 256 && vm * 8 < 65536 && env_int("QLDPC_M2V", 0) != 0 &&
+        if (bp->m2s == 1 && tb == 256 && g->m <= 4 * 256 && vm * 8 < 65536 && QLDPC_EXPERIMENTAL && env_int("QLDPC_M2V", 0) != 0 &&
             r_fits(3, vm, g->m, 8, 0, 0, 1)) {
           bp->m2s = 3;
           bp->tail = 0;
@@ -1427,8 +1431,10 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
                       // the fused kernel runs one layout family for both sectors
                       (dec_x && dec_z &&
                        (dec_x->m2s != dec_z->m2s || dec_x->tail != dec_z->tail || dec_x->fb != dec_z->fb)) ||
-                      // m2v: the kernel's compile-time D3K sets both sectors' V layouts
-                      (dec_x && dec_z && dec_x->m2s == 3 && dec_x->d3k != dec_z->d3k) ||
+                      // one-slot families (m2s / c2s / m2v) keep no dummy edge on a real variable:
+                      // the kernel's compile-time D3K must be each sector's own (a degree-3
+                      // variable past it would run the 4-edge path and read the shared dummy slot)
+                      (dec_x && dec_z && dec_x->m2s && dec_x->d3k != dec_z->d3k) ||
                       env_int("QLDPC_MC_STAGED", 0) == 1;
   if (staged) {  // staged pipeline around decode_batch (staged.hip): any decoder pair
     if (dec_x && dec_z && (dec_x->g->n != dec_z->g->n || dec_x->g->device != dec_z->g->device))

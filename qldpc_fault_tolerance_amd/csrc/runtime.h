@@ -4,6 +4,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// measured-and-not-kept kernel families (c2s, m2v, fp64 x 512 threads, engine 4): out of the
+// product build unless -DQLDPC_EXPERIMENTAL=1
+#ifndef QLDPC_EXPERIMENTAL
+#define QLDPC_EXPERIMENTAL 0
+#endif
+
 #include <string>
 #include <vector>
 

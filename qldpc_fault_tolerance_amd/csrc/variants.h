@@ -9,6 +9,12 @@
 #pragma once
 #include "bp_reg.h"
 
+// measured-and-not-kept kernel families (c2s, m2v, fp64 x 512 threads, engine 4): out of the
+// product build unless -DQLDPC_EXPERIMENTAL=1
+#ifndef QLDPC_EXPERIMENTAL
+#define QLDPC_EXPERIMENTAL 0
+#endif
+
 namespace qldpc {
 
 using DecLaunch = hipError_t (*)(dim3, dim3, size_t, hipStream_t, const DecArgs&);

@@ -89,3 +89,17 @@ def test_notebook_pin_wer_transforms():
         assert np.isclose(nbp.wer_current(c, S, K, R), word_error_rate_phenl(c, S, K, R), rtol=1e-12, atol=0)
     a, b = nbp.wer_commented(1, 10000, 100, 6), nbp.wer_current(1, 10000, 100, 6)
     assert np.isclose(a, b, rtol=1e-3)
+
+
+def test_pin_uniformity_statistics():
+    """tests/notebook_pin.py's combined test: mid-rank percentiles never hit 0
+    or 1, uniform percentiles pass, percentiles crowded at one end fail both KS and Fisher."""
+    import notebook_pin as nbp
+
+    fits = np.linspace(0.0, 1.0, 101)
+    assert 0 < nbp.mid_percentile(-1.0, fits) < 0.01 and 0.99 < nbp.mid_percentile(2.0, fits) < 1
+    assert abs(nbp.mid_percentile(0.5, fits) - 0.5) < 1e-9
+    u = nbp.uniformity((np.arange(15) + 0.5) / 15)
+    assert u["ks_p"] > 0.9 and u["fisher_p"] > 0.5
+    low = nbp.uniformity(np.full(15, 0.03))
+    assert low["ks_p"] < 1e-6 and low["fisher_p"] < 1e-6
