@@ -6,6 +6,7 @@ Run in the build container only (``/root/reference`` is not on the GPU box):
     python tests/golden/make_golden.py phen     # reference_harness_phen_n225.npz
     python tests/golden/make_golden.py configs  # reference_harness_configs.npz (configs 2-5)
     python tests/golden/make_golden.py fits     # reference_fits.npz (threshold tooling)
+    python tests/golden/make_golden.py schedules  # reference_circuit_schedules.npz (CX schedules)
 
 The reference modules import third-party packages that are absent here
 (``graph_tools``, ``ldpc``, ``bposd``, ``stim``, …), so empty stub
@@ -510,8 +511,51 @@ def main_notebook():
     print("wrote", path, k, "cases")
 
 
+def schedule_cases():
+    """(name, H) of the CX-schedule fixtures: the demo's d3 toric code, the d3 surface code of the
+    Threshold notebook (ring codes without their last row), hgp_34_n225 and GenBicycleA1."""
+    def ring(d):
+        h = np.zeros((d, d), np.uint8)
+        for i in range(d):
+            h[i, i] = h[i, (i + 1) % d] = 1
+        return h
+
+    tor = codes.hgp(ring(3), ring(3))
+    sur = codes.hgp(ring(3)[:-1, :], ring(3)[:-1, :])
+    n225 = codes.get_code("hgp_34_n225")
+    gbc = codes.get_code("GenBicycleA1")
+    return [("toric3_hx", tor.hx), ("toric3_hz", tor.hz), ("surface3_hx", sur.hx), ("surface3_hz", sur.hz),
+            ("n225_hx", n225.hx), ("n225_hz", n225.hz), ("gbcA1_hx", gbc.hx)]
+
+
+def main_schedules():
+    """ColorationCircuit / RandomCircuit (src/CircuitScheduling.py) of the reference itself: it imports
+    only numpy and networkx, both present, so no stub is needed."""
+    sys.path.insert(0, REF_SRC)
+    import CircuitScheduling as CS  # noqa: E402  (the reference's own module)
+
+    out = {}
+    for name, H in schedule_cases():
+        for kind, fn in (("color", CS.ColorationCircuit), ("random", CS.RandomCircuit)):
+            sched = fn(np.asarray(H).astype(int))
+            keys, vals, offs = [], [], [0]
+            for step in sched:
+                for k in step:  # insertion order kept
+                    keys.append(int(k))
+                    vals.append(int(step[k]))
+                offs.append(len(keys))
+            out[f"{name}_{kind}_keys"] = np.array(keys, np.int32)
+            out[f"{name}_{kind}_vals"] = np.array(vals, np.int32)
+            out[f"{name}_{kind}_offs"] = np.array(offs, np.int32)
+    path = os.path.join(HERE, "reference_circuit_schedules.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "notebook":
+    if len(sys.argv) > 1 and sys.argv[1] == "schedules":
+        main_schedules()
+    elif len(sys.argv) > 1 and sys.argv[1] == "notebook":
         main_notebook()
     elif len(sys.argv) > 1 and sys.argv[1] == "phen":
         main_phen()
