@@ -329,9 +329,46 @@ int qldpc_comm_destroy(qldpc_comm *comm);
  * Synchronous.  The ndev > 1 RCCL path has not yet run on a multi-GPU node.
  * Shots keyed by global index: the totals do not depend on ndev.
  */
+/* The shot-block split qldpc_mc_run_sharded uses (= parallel.shard_range): part `part` of `nparts`
+ * owns [begin, begin + count) of `total` shots, block sizes differ by <= 1, the first total % nparts
+ * parts one longer.  Host-only (no GPU needed). */
+int qldpc_shard_range(int64_t total, int32_t nparts, int32_t part, int64_t *begin, int64_t *count);
 int qldpc_mc_run_sharded(qldpc_mc **mcs, qldpc_comm **comms, int32_t ndev, double px, double py, double pz,
                          uint64_t seed, uint64_t shot_begin, int64_t shot_count, int32_t logical_mode,
                          qldpc_counters *out);
+
+/*
+ * Circuit-level space-time shot loop (CodeSimulator_Circuit_SpaceTime._single_run / WordErrorRate,
+ * src/Simulators_SpaceTime.py:968-1049) for many samples per launch.  Inputs (host CSR graphs
+ * from qldpc_graph_create; qldpc_fault_tolerance_amd/circuit.py builds them):
+ *   dem, dem_obs : detectors x mechanisms / observables x mechanisms of the FULL circuit's DEM
+ *                  (the stim detector_sampler's distribution, :940; rows = num_cycles * m
+ *                  detectors, num_cycles = num_rounds * num_rep + 1), probs [M] host doubles;
+ *   dec1         : decoder1 on h1 (num_rep * m rows; GenFaultHyperGraph's first layer, :955);
+ *   h1_space_cor : GenCorrecHyperGraph (m x n1), L1 (K x n1) the first layer's observables;
+ *   dec2, L2     : decoder2 on h2 (m x n2) and the last layer's observables.
+ * Sample s draws mechanism j when Philox4x32-10(key = seed, ctr = (j, shot, 0x51D50003)) as a
+ * 53-bit uniform is < probs[j] (shot = shot_begin + s).  Counters: shots, failures, sector 0 =
+ * decoder1 decodes (num_rounds per sample), sector 1 = decoder2 decodes.  d_fail [S] (or NULL),
+ * d_detobs [S][D + K] sampled detector and observable bits (or NULL).  Async on `stream` except
+ * with a host OSD stage (synchronous per batch).  dec1 = dec2 = NULL (and NULL h1_space_cor / L1 /
+ * L2) makes a sampler-only handle for qldpc_circ_sample (decoders outside the engine).
+ */
+typedef struct qldpc_circ qldpc_circ;
+int qldpc_circ_create(const qldpc_graph *dem, const qldpc_graph *dem_obs, const double *probs, qldpc_bp *dec1,
+                      const qldpc_graph *h1_space_cor, const qldpc_graph *L1, qldpc_bp *dec2, const qldpc_graph *L2,
+                      int32_t num_rounds, int32_t num_rep, int64_t max_batch, qldpc_circ **out);
+/* decoder2 as bposd_decoder (ST_BPOSD_Decoder_Circuit, src/Decoders_SpaceTime.py:277-292): dec2 from
+ * qldpc_bp_create_soft and ONE of a GPU OSD (uniform priors) or a host OSD stage on h2. */
+int qldpc_circ_set_final_osd(qldpc_circ *circ, qldpc_osd_gpu *osd_gpu, const qldpc_osd *osd_host);
+int qldpc_circ_info(const qldpc_circ *circ, int32_t *detectors, int32_t *observables, int32_t *mechanisms);
+int qldpc_circ_launch(qldpc_circ *circ, uint64_t seed, uint64_t shot_begin, int64_t shot_count, void *d_counters,
+                      uint8_t *d_fail, uint8_t *d_detobs, void *stream);
+/* The sampling step alone (stim's detector sampler): d_out [S][D + K] uint8 detector then
+ * observable bits of samples shot_begin.. (the draws qldpc_circ_launch decodes).  Async. */
+int qldpc_circ_sample(qldpc_circ *circ, uint64_t seed, uint64_t shot_begin, int64_t shot_count, uint8_t *d_out,
+                      void *stream);
+int qldpc_circ_destroy(qldpc_circ *circ);
 
 /*
  * The sampling step alone (CodeSimulator_DataError._generate_error,

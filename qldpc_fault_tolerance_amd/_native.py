@@ -26,7 +26,9 @@ EXPORTED = [
     "qldpc_bp_bank_stats", "qldpc_bp_create_hbm", "qldpc_mc_set_osd", "qldpc_comm_unique_id",
     "qldpc_comm_init_rank", "qldpc_comm_init_all", "qldpc_comm_rank", "qldpc_comm_allreduce_counters",
     "qldpc_comm_allreduce_counters_group", "qldpc_comm_destroy", "qldpc_mc_run_sharded", "qldpc_sample_errors",
-    "qldpc_stream_sync", "qldpc_bp_kernel_id", "qldpc_build_flags",
+    "qldpc_stream_sync", "qldpc_bp_kernel_id", "qldpc_build_flags", "qldpc_circ_create", "qldpc_circ_set_final_osd",
+    "qldpc_circ_info", "qldpc_circ_launch", "qldpc_circ_sample", "qldpc_circ_destroy",
+    "qldpc_shard_range",
 ]
 BUILD_EXPERIMENTAL = 1  # qldpc_build_flags(): the measured-and-not-kept kernel families are compiled in
 COMM_ID_BYTES = 128
@@ -162,6 +164,20 @@ def _declare(L):
     L.qldpc_stream_sync.argtypes = [_vp]
     L.qldpc_build_flags.restype = ctypes.c_int
     L.qldpc_build_flags.argtypes = []
+    L.qldpc_circ_create.restype = ctypes.c_int
+    L.qldpc_circ_create.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i64, _pp]
+    L.qldpc_circ_set_final_osd.restype = ctypes.c_int
+    L.qldpc_circ_set_final_osd.argtypes = [_vp, _vp, _vp]
+    L.qldpc_circ_info.restype = ctypes.c_int
+    L.qldpc_circ_info.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 3
+    L.qldpc_circ_launch.restype = ctypes.c_int
+    L.qldpc_circ_launch.argtypes = [_vp, _u64, _u64, _i64, _vp, _vp, _vp, _vp]
+    L.qldpc_circ_sample.restype = ctypes.c_int
+    L.qldpc_circ_sample.argtypes = [_vp, _u64, _u64, _i64, _vp, _vp]
+    L.qldpc_shard_range.restype = ctypes.c_int
+    L.qldpc_shard_range.argtypes = [_i64, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]
+    L.qldpc_circ_destroy.restype = ctypes.c_int
+    L.qldpc_circ_destroy.argtypes = [_vp]
 
 
 def lib():

@@ -211,6 +211,16 @@ int qldpc_comm_destroy(qldpc_comm* c) {
   return 0;
 }
 
+int qldpc_shard_range(int64_t total, int32_t nparts, int32_t part, int64_t* begin, int64_t* count) {
+  if (!begin || !count || total < 0 || nparts < 1 || part < 0 || part >= nparts)
+    return set_err(QLDPC_EINVAL, "bad shard_range argument");
+  // parallel.shard_range: blocks of base or base + 1 shots, the first `extra` parts one longer
+  const int64_t base = total / nparts, extra = total % nparts;
+  *begin = part * base + std::min<int64_t>(part, extra);
+  *count = base + (part < extra ? 1 : 0);
+  return 0;
+}
+
 int qldpc_mc_run_sharded(qldpc_mc** mcs, qldpc_comm** comms, int32_t ndev, double px, double py, double pz,
                          uint64_t seed, uint64_t shot_begin, int64_t shot_count, int32_t logical_mode,
                          qldpc_counters* out) {
@@ -251,9 +261,8 @@ int qldpc_mc_run_sharded(qldpc_mc** mcs, qldpc_comm** comms, int32_t ndev, doubl
       why[d] = std::string("qldpc_mc_run_sharded setup: ") + hipGetErrorString(e);
       return;
     }
-    // parallel.shard_range: blocks of base or base + 1 shots, the first `extra` ranks one longer
-    const int64_t base = shot_count / ndev, extra = shot_count % ndev;
-    const int64_t lo = d * base + std::min<int64_t>(d, extra), cnt_d = base + (d < extra ? 1 : 0);
+    int64_t lo = 0, cnt_d = 0;
+    (void)qldpc_shard_range(shot_count, ndev, d, &lo, &cnt_d);
     rcs[d] = qldpc_mc_launch(mcs[d], px, py, pz, seed, shot_begin + (uint64_t)lo, cnt_d, logical_mode, nullptr, cnt[d],
                              nullptr, nullptr, nullptr, nullptr, 0, streams[d]);
     if (rcs[d]) why[d] = qldpc_last_error();  // thread-local: carried to the caller's thread

@@ -1169,6 +1169,11 @@ int osd_gpu_bposd_stage(qldpc_osd_gpu* osd, const uint8_t* synd, const double* p
   return 0;
 }
 
+// true when the host OSD stage was built on exactly this graph (shape and edges)
+bool osd_host_matches(const qldpc_osd* o, const qldpc_graph* g) {
+  return o && g && o->m == g->m && o->n == g->n && o->col_rows == g->col_rows;
+}
+
 // true when the GPU OSD handle was built on exactly this graph (shape and edges)
 bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g) {
   return o && g && o->host.m == g->m && o->host.n == g->n && o->host.col_rows == g->col_rows;

@@ -289,3 +289,70 @@ class ST_BP_Decoder_Class(DecoderClass):
                                       bp_method=self.decoder_default_params["bp_method"],
                                       ms_scaling_factor=self.decoder_default_params["ms_scaling_factor"],
                                       num_rep=p["num_rep"], precision=self.precision, device=self.device)
+
+
+# ------------------------------------------------------------------ circuit-level space-time
+class ST_BP_Decoder_Circuit(BPDecoder):
+    """``ST_BP_Decoder_Circuit(h, channel_probs, max_iter, bp_method, ms_scaling_factor)``
+    (``src/Decoders_SpaceTime.py:261-274``): BP on a fault hypergraph (``GenFaultHyperGraph``'s h1),
+    ``decode`` returns the correction mod 2.  ``h`` has a column per DEM error mechanism and
+    non-uniform ``channel_probs`` (the mechanisms' probabilities)."""
+
+    def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, precision: int = 64,
+                 device: int | None = None):
+        super().__init__(h, channel_probs, max_iter, bp_method, ms_scaling_factor, precision=precision,
+                         device=device)
+        self.space_decoder = self.decoder
+
+    def decode(self, synd):
+        return super().decode(synd) % 2
+
+
+class ST_BPOSD_Decoder_Circuit(BPOSD_Decoder):
+    """``ST_BPOSD_Decoder_Circuit(h, channel_probs, max_iter, bp_method, ms_scaling_factor, osd_method,
+    osd_order)`` (``src/Decoders_SpaceTime.py:277-292``): ``bposd_decoder`` on h2; ``decode`` returns
+    ``osdw_decoding``.  DEM priors are non-uniform, so the OSD half runs on the host stage."""
+
+
+class ST_BP_Decoder_Circuit_Class(DecoderClass):
+    """``src/Decoders_SpaceTime.py:296-321``: keys ``h``, ``code_h``, ``channel_probs``;
+    ``max_iter = int(n(code_h) / max_iter_ratio)``."""
+
+    def __init__(self, max_iter_ratio: int, bp_method: str, ms_scaling_factor: float, precision: int = 64):
+        self.decoder_default_params = {"max_iter_ratio": max_iter_ratio, "bp_method": bp_method,
+                                       "ms_scaling_factor": ms_scaling_factor}
+        self.precision = precision
+
+    def GetDecoder(self, code_and_noise_channel_params):
+        p = code_and_noise_channel_params
+        assert "h" in p.keys(), "missing the check matrix h"
+        assert "code_h" in p.keys(), "missing the code"
+        assert "channel_probs" in p.keys(), "missing the channel_probs"
+        _, num_qubits = np.shape(p["code_h"])
+        d = self.decoder_default_params
+        return ST_BP_Decoder_Circuit(h=p["h"], channel_probs=p["channel_probs"],
+                                     max_iter=int(num_qubits / d["max_iter_ratio"]), bp_method=d["bp_method"],
+                                     ms_scaling_factor=d["ms_scaling_factor"], precision=self.precision)
+
+
+class ST_BPOSD_Decoder_Circuit_Class(DecoderClass):
+    """``src/Decoders_SpaceTime.py:323-357``: a ``BPOSD_Decoder`` on ``h`` with ``max_iter =
+    n(code_h) / max_iter_ratio`` passed as a float (quirk Q1: truncated by ldpc)."""
+
+    def __init__(self, max_iter_ratio: int, bp_method: str, ms_scaling_factor: float, osd_method: str,
+                 osd_order: int, precision: int = 64):
+        self.decoder_default_params = {"max_iter_ratio": max_iter_ratio, "bp_method": bp_method,
+                                       "ms_scaling_factor": ms_scaling_factor, "osd_method": osd_method,
+                                       "osd_order": osd_order}
+        self.precision = precision
+
+    def GetDecoder(self, code_and_noise_channel_params):
+        p = code_and_noise_channel_params
+        assert "h" in p.keys(), "missing the check matrix h"
+        assert "code_h" in p.keys(), "missing the code"
+        assert "channel_probs" in p.keys(), "missing the channel_probs"
+        _, num_qubits = np.shape(p["code_h"])
+        d = self.decoder_default_params
+        return BPOSD_Decoder(h=p["h"], channel_probs=p["channel_probs"], max_iter=num_qubits / d["max_iter_ratio"],
+                             bp_method=d["bp_method"], ms_scaling_factor=d["ms_scaling_factor"],
+                             osd_method=d["osd_method"], osd_order=d["osd_order"], precision=self.precision)

@@ -345,6 +345,7 @@ class MCResult:
     corr: np.ndarray | None = None
     iters: np.ndarray | None = None
     trace: np.ndarray | None = None
+    detobs: np.ndarray | None = None
 
     @staticmethod
     def from_words(w: np.ndarray) -> "MCResult":
@@ -583,4 +584,107 @@ class DevicePhenl:
         h = getattr(self, "handle", None)
         if h and _native._lib is not None:
             _native.lib().qldpc_phenl_destroy(h)
+            self.handle = None
+
+
+class DeviceCircuit:
+    """Circuit-level space-time shot loop of ``CodeSimulator_Circuit_SpaceTime`` on one GPU
+    (``qldpc_circ_*``, csrc/circuit.hip).
+
+    ``dem`` is the FULL circuit's detector error model (:class:`~.circuit.DetectorErrorModel`),
+    ``dec1`` decodes each round on h1 (num_rep·m rows), ``dec2`` the final layer on h2; ``hs``
+    (h1_space_cor), ``L1`` and ``L2`` are dense 0/1 matrices as ``GenCorrecHyperGraph`` /
+    ``GenFaultHyperGraph`` return them.  ``osd``: a :class:`DeviceOSD` (uniform priors) or a
+    :class:`HostOSD` on h2 makes decoder2 BP+OSD (``dec2`` built with ``soft=True``).
+    """
+
+    def __init__(self, dem, dec1: "DeviceBP | None" = None, hs=None, L1=None, dec2: "DeviceBP | None" = None, L2=None,
+                 num_rounds: int = 0, num_rep: int = 1, osd=None, max_batch: int = 0, device: int | None = None):
+        sampler_only = dec1 is None and dec2 is None
+        if device is None:
+            if dec1 is not None:
+                device = dec1.graph.device
+            else:
+                from .parallel import local_device_index
+
+                device = local_device_index()
+        dev = device
+        self.device = dev
+        self.dem = dem
+        self.decoders = (dec1, dec2)
+        self.num_rounds, self.num_rep = int(num_rounds), int(num_rep)
+        mats = [dem.check_matrix(), dem.observable_matrix()] + ([] if sampler_only else [hs, L1, L2])
+        self._g = [DeviceGraph(np.asarray(a, dtype=np.uint8) % 2, device=dev) for a in mats]
+        self._probs = np.ascontiguousarray(np.asarray(dem.probs, dtype=np.float64))
+        hd = (lambda i: None) if sampler_only else (lambda i: self._g[i].handle)  # noqa: E731
+        h = ctypes.c_void_p()
+        _native.check(_native.lib().qldpc_circ_create(
+            self._g[0].handle, self._g[1].handle, self._probs.ctypes.data_as(ctypes.c_void_p),
+            None if sampler_only else dec1.handle, hd(2), hd(3), None if sampler_only else dec2.handle, hd(4),
+            self.num_rounds, self.num_rep, int(max_batch), ctypes.byref(h)), "qldpc_circ_create")
+        self.handle = h
+        self._osd = osd
+        if osd is not None:
+            gpu = osd.handle if isinstance(osd, DeviceOSD) else None
+            host = osd.handle if isinstance(osd, HostOSD) else None
+            _native.check(_native.lib().qldpc_circ_set_final_osd(h, gpu, host), "qldpc_circ_set_final_osd")
+
+    @property
+    def num_detectors(self) -> int:
+        return self.dem.num_detectors
+
+    @property
+    def num_observables(self) -> int:
+        return self.dem.num_observables
+
+    def new_counters(self):
+        torch = _torch()
+        return torch.zeros(_native.COUNTER_WORDS, dtype=torch.int64, device=torch.device("cuda", self.device))
+
+    def launch(self, seed, shot_begin, shot_count, counters, fail=None, detobs=None, stream=None):
+        torch = _torch()
+        s = stream if stream is not None else _stream_handle(torch, counters.device)
+
+        def ptr(t):
+            return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+        _native.check(_native.lib().qldpc_circ_launch(self.handle, int(seed) & (2**64 - 1), int(shot_begin),
+                                                      int(shot_count), ptr(counters), ptr(fail), ptr(detobs), s),
+                      "qldpc_circ_launch")
+
+    def sample(self, seed, shot_begin, shot_count):
+        """Detector + observable bits [S, D + K] (uint8, host) of samples ``shot_begin..`` — the
+        ``detector_sampler.sample(shots, append_observables=True)`` of the reference."""
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        S = int(shot_count)
+        out = torch.zeros((S, self.num_detectors + self.num_observables), dtype=torch.uint8, device=dev)
+        _native.check(_native.lib().qldpc_circ_sample(self.handle, int(seed) & (2**64 - 1), int(shot_begin), S,
+                                                      ctypes.c_void_p(out.data_ptr()), _stream_handle(torch, dev)),
+                      "qldpc_circ_sample")
+        torch.cuda.synchronize(dev)
+        return out.cpu().numpy()
+
+    def run(self, seed, shot_begin, shot_count, per_shot: bool = False) -> "MCResult":
+        """Counters of ``shot_count`` samples (``per_shot``: also ``fail`` [S] and the sampled
+        detector / observable bits ``detobs`` [S, D + K] as host arrays)."""
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        cnt = self.new_counters()
+        S = int(shot_count)
+        fail = torch.zeros(S, dtype=torch.uint8, device=dev) if per_shot else None
+        detobs = torch.zeros((S, self.num_detectors + self.num_observables), dtype=torch.uint8, device=dev) \
+            if per_shot else None
+        self.launch(seed, shot_begin, S, cnt, fail, detobs)
+        torch.cuda.synchronize(dev)
+        res = MCResult.from_words(cnt.cpu().numpy())
+        if per_shot:
+            res.fail = fail.cpu().numpy()
+            res.detobs = detobs.cpu().numpy()
+        return res
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _native._lib is not None:
+            _native.lib().qldpc_circ_destroy(h)
             self.handle = None

@@ -38,6 +38,17 @@ def shard_range(total: int, rank: int, world_size: int, begin: int = 0):
     return b, c
 
 
+def native_shard_range(total: int, nparts: int, part: int):
+    """The split ``qldpc_mc_run_sharded`` applies inside the C ABI (``qldpc_shard_range``; host-only,
+    no GPU): must equal :func:`shard_range` (tests/test_distributed_cpu.py)."""
+    from . import _native
+
+    b, c = ctypes.c_int64(), ctypes.c_int64()
+    _native.check(_native.lib().qldpc_shard_range(int(total), int(nparts), int(part), ctypes.byref(b), ctypes.byref(c)),
+                  "qldpc_shard_range")
+    return b.value, c.value
+
+
 def allreduce_counters(counters):
     """Sum a counter tensor over all ranks in place (no-op when not distributed).
 

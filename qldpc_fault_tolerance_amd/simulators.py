@@ -673,6 +673,230 @@ class CodeSimulator_Phenon_SpaceTime:
         return word_error_rate_per_cycle(fails, total, self.K, total_num_cycles), total
 
 
+class CodeSimulator_Circuit_SpaceTime:
+    """Circuit-level space-time simulator (``src/Simulators_SpaceTime.py:672-1077``).
+
+    ``_generate_circuit`` builds the reference's syndrome-extraction circuits (:mod:`.circuit`:
+    explicit op lists with stim's semantics, ``AddCXError`` noise) and the full circuit's detector
+    error model; ``_generate_circuit_graph`` derives ``circuit_graph`` (h1 / L1 / channel_ps1 of
+    the first layer, h2 / L2 / channel_ps2 of the last) and ``h1_space_cor`` from the one-round
+    fault circuit's DEM, as ``GenFaultHyperGraph`` / ``GenCorrecHyperGraph`` do.  ``WordErrorRate``
+    runs every sample on the GPU (``qldpc_circ_launch``: DEM mechanisms sampled by Philox,
+    detectors by bit-sliced XOR, the round loop on the BP engine, decoder2 BP or BP+OSD) when
+    decoder1_z / decoder2_z are this engine's decoders; other decoders run the reference's
+    ``_decoding_samples`` loop per sample on GPU-sampled detectors.
+
+    Deviation: for ``eval_logical_type='X'`` the reference swaps hx/hz and lx/lz IN the caller's
+    code object (``:676-690``); here a shallow copy is swapped and the caller's object is left alone.
+    """
+
+    def __init__(self, code=None, decoder1_z=None, decoder1_x=None, decoder2_z=None, decoder2_x=None, p=0,
+                 num_cycles=1, num_rep=1, error_params=None, eval_logical_type="Z", circuit_type="coloration",
+                 rand_scheduling_seed=0, seed=None, max_batch=0):
+        import copy as _copy
+
+        from . import circuit as _circ
+
+        if eval_logical_type == "X":  # :676-690, on a copy
+            code = _copy.copy(code)
+            code.hx, code.hz = code.hz, code.hx
+            code.lx, code.lz = code.lz, code.lx
+            decoder1_z, decoder2_z = decoder1_x, decoder2_x
+        self.eval_code = code
+        self.hx_ext = np.hstack([code.hx, np.identity(np.shape(code.hx)[0])])
+        self.hz_ext = np.hstack([code.hz, np.identity(np.shape(code.hz)[0])])
+        self.decoder1_z = decoder1_z
+        self.decoder2_z = decoder2_z
+        self.N = code.N
+        self.K = code.K
+        self.pz = p
+        self.synd_prob = p
+        self.min_logical_weight = self.N
+        self.num_cycles = num_cycles
+        self.num_rep = num_rep
+        self.num_rounds = int((self.num_cycles - 1) / self.num_rep)
+        assert np.abs((self.num_cycles - 1) / self.num_rep - self.num_rounds) <= 1e-2
+        self.circuit = _circ.StimCircuit()
+        self.fault_circuit = _circ.StimCircuit()
+        self.error_params = error_params
+        self.max_stab_weight_x = int(np.max(np.sum(code.hx, axis=1)))
+        self.max_stab_weight_z = int(np.max(np.sum(code.hz, axis=1)))
+        if circuit_type == "random":
+            self.scheduling_X = _circ.RandomCircuit(code.hx)
+            self.scheduling_Z = _circ.RandomCircuit(code.hz)
+        elif circuit_type == "coloration":
+            self.scheduling_X = _circ.ColorationCircuit(code.hx)
+            self.scheduling_Z = _circ.ColorationCircuit(code.hz)
+        self.num_logicals = self.eval_code.lx.shape[0]
+        self.num_checks = self.eval_code.hx.shape[0]
+        self.detector_sampler = None
+        self.circuit_graph = None
+        self.h1_space_cor = None
+        self.dem = None
+        self.fault_dem = None
+        self.seed = int(seed) if seed is not None else None
+        self.max_batch = int(max_batch)
+        self._shot_offset = 0
+        self._dev = None
+        self._dev_key = None
+        self.last_result = None
+
+    # -- circuits and hypergraphs ---------------------------------------------------
+    def _generate_circuit(self):
+        """``:737-940``: the full circuit (num_rounds rounds + the final data measurement) and the
+        one-round fault circuit, both with CX noise; the full circuit's DEM is the sampler."""
+        from . import circuit as _circ
+
+        c = self.eval_code
+        self.circuit, self.fault_circuit = _circ.syndrome_circuits(
+            c.hx, c.hz, c.lx, self.error_params, self.pz, self.num_rounds, self.num_rep, self.scheduling_X,
+            self.scheduling_Z)
+        self.dem = self.circuit.detector_error_model(flatten_loops=True)
+        self.detector_sampler = _DetectorSampler(self)
+
+    def _generate_circuit_graph(self):
+        """``:942-966``."""
+        from . import circuit as _circ
+
+        self.fault_dem = self.fault_circuit.detector_error_model(flatten_loops=True)
+        H_list, L_list, P_list = _circ.GenFaultHyperGraph(self.fault_dem, num_rounds=self.num_rounds,
+                                                           num_rep=self.num_rep, num_logicals=self.num_logicals)
+        self.circuit_graph = {"h1": H_list[0], "L1": L_list[0], "channel_ps1": P_list[0],
+                              "h2": H_list[-1], "L2": L_list[-1], "channel_ps2": P_list[-1]}
+        self.h1_space_cor = _circ.GenCorrecHyperGraph(self.fault_dem, num_rounds=self.num_rounds, num_rep=self.num_rep,
+                                                      num_checks=self.num_checks, num_logicals=self.num_logicals)
+
+    # -- reference per-sample path (plugin decoders) -------------------------------
+    def _decoding_samples(self, samples):
+        """``:968-1025``: per sample the round loop of decoder1, then decoder2; 1 = failure."""
+        h1, L1 = self.circuit_graph["h1"], self.circuit_graph["L1"]
+        h2, L2 = self.circuit_graph["h2"], self.circuit_graph["L2"]
+        m, K = self.num_checks, len(self.eval_code.lx)
+        out = []
+        for sample in np.asarray(samples):
+            hist = 1.0 * np.reshape(np.array(sample[:-K]), [self.num_cycles, m])
+            logical = 1.0 * np.array(sample[-K:])
+            dets = [np.reshape(hist[j * self.num_rep:(j + 1) * self.num_rep, :], [self.num_rep * m])
+                    for j in range(self.num_rounds)]
+            fin = hist[self.num_rounds * self.num_rep:, :]
+            dets.append(np.reshape(fin, [fin.shape[0] * fin.shape[1]]))
+            syn_cor, log_cor = 0, 0
+            for j in range(self.num_rounds):
+                syn = dets[j]
+                syn[:m] = (syn[:m] + syn_cor) % 2
+                cor = self.decoder1_z.decode(syn)
+                syn_cor = (syn_cor + (self.h1_space_cor @ cor) % 2) % 2
+                log_cor = (log_cor + L1 @ cor % 2) % 2
+            final_syn = (dets[-1] + syn_cor) % 2
+            final_cor = self.decoder2_z.decode(final_syn)
+            log_cor = (log_cor + L2 @ final_cor % 2) % 2
+            res_syn = (final_syn + h2 @ final_cor) % 2
+            res_log = (logical + log_cor) % 2
+            out.append(1 if (res_syn.any() or res_log.any()) else 0)
+        return out
+
+    def _single_run(self):
+        samples = self.detector_sampler.sample(shots=1, append_observables=True)
+        return self._decoding_samples(samples)[0]
+
+    # -- fused engine path ---------------------------------------------------------
+    def _engine_parts(self):
+        """(decoder1's DeviceBP, decoder2's DeviceBP, decoder2's OSD or None), or None."""
+        b1 = _engine_bp(self.decoder1_z)
+        if b1 is None:
+            return None
+        d2 = self.decoder2_z
+        if _is_bposd(d2):
+            osd = getattr(d2, "gpu_osd", None) or d2.osd
+            return b1, d2.decoder, osd
+        b2 = _engine_bp(d2)
+        return None if b2 is None else (b1, b2, None)
+
+    def _device(self):
+        from .engine import DeviceCircuit
+
+        parts = self._engine_parts()
+        key = None if parts is None else tuple(id(x) for x in parts)
+        if self._dev is None or self._dev_key != key:
+            if self.circuit_graph is None:
+                raise RuntimeError("call _generate_circuit() and _generate_circuit_graph() first")
+            cg = self.circuit_graph
+            if parts is None:
+                self._dev = DeviceCircuit(self.dem, max_batch=self.max_batch)
+            else:
+                b1, b2, osd = parts
+                self._dev = DeviceCircuit(self.dem, b1, self.h1_space_cor, cg["L1"], b2, cg["L2"], self.num_rounds,
+                                          self.num_rep, osd=osd, max_batch=self.max_batch)
+            self._dev_key = key
+        return self._dev
+
+    def fused_counts(self, num_samples: int):
+        """``num_samples`` samples on the GPU (sharded over the torch.distributed ranks); the
+        all-reduced :class:`~.engine.MCResult`."""
+        from .engine import MCResult, _torch
+
+        if self._engine_parts() is None:
+            raise TypeError("fused path needs engine decoders (ST_BP_Decoder_Circuit / BPDecoder / BPOSD_Decoder)")
+        torch = _torch()
+        if self.seed is None:
+            self.seed = random.getrandbits(64)
+        dev = self._device()
+        rank, ws = parallel.world()
+        b, c = parallel.shard_range(num_samples, rank, ws, begin=self._shot_offset)
+        self._shot_offset += int(num_samples)
+        cnt = dev.new_counters()
+        dev.launch(self.seed, b, c, cnt)
+        parallel.allreduce_counters(cnt)
+        torch.cuda.synchronize(cnt.device)
+        res = MCResult.from_words(cnt.cpu().numpy())
+        self.last_result = res
+        return res
+
+    def _batch_failures(self, n: int) -> int:
+        if self._engine_parts() is not None:
+            return self.fused_counts(n).failures
+        samples = self.detector_sampler.sample(shots=n, append_observables=True)
+        return int(np.sum(self._decoding_samples(samples)))
+
+    def WordErrorRate(self, num_samples: int):
+        """``:1028-1049``: ``(wer per qubit per cycle, None)``; num_cycles must be odd."""
+        error_count = self._batch_failures(num_samples)
+        return word_error_rate_per_cycle(error_count, num_samples, self.K, self.num_cycles), None
+
+    def WordErrorRate_TargetFailure(self, target_failures, batch_size, max_batches):
+        """``:1051-1077``: batches until ``target_failures``; ``(wer, total_samples)``."""
+        assert int(self.num_cycles) % 2 == 1
+        total, fails = 0, 0
+        for _ in range(int(max_batches)):
+            fails += self._batch_failures(batch_size)
+            total += int(batch_size)
+            if fails >= target_failures:
+                break
+        print("failures:", fails)
+        return word_error_rate_per_cycle(fails, total, self.K, self.num_cycles), total
+
+
+class _DetectorSampler:
+    """``self.circuit.compile_detector_sampler()`` (``:940``) on the GPU: the full circuit's DEM
+    mechanisms sampled by Philox (``qldpc_circ_sample``); consecutive calls draw consecutive samples."""
+
+    def __init__(self, sim: "CodeSimulator_Circuit_SpaceTime"):
+        self.sim = sim
+
+    def sample(self, shots: int, append_observables: bool = True):
+        sim = self.sim
+        if sim.seed is None:
+            sim.seed = random.getrandbits(64)
+        from .engine import DeviceCircuit
+
+        dev = sim._dev if sim._dev is not None else DeviceCircuit(sim.dem, max_batch=sim.max_batch)
+        if sim._dev is None:
+            sim._dev, sim._dev_key = dev, None
+        out = dev.sample(sim.seed, sim._shot_offset, int(shots))
+        sim._shot_offset += int(shots)
+        return out if append_observables else out[:, :sim.dem.num_detectors]
+
+
 # -------------------------------------------------------------- code family
 
 
@@ -793,7 +1017,9 @@ class CodeFamily_SpaceTime:
     the unbound ``eval_p_adapt_list`` (UnboundLocalError); here it returns the same values
     nested like ``'data'`` (``eval_wer_list[c][i]`` = code c at ``eval_p_list[i]``, i.e. the
     reference's flat list reshaped to ``[len(code_list), len(eval_p_list)]`` as its commented-out
-    ``np.reshape`` does) and one p array per code.  ``'circuit'`` needs stim (absent) and raises.
+    ``np.reshape`` does) and one p array per code.  ``'circuit'`` (``:1220-1268``) builds the circuit
+    and fault graphs per (code, p) with :class:`CodeSimulator_Circuit_SpaceTime` (stim's role restated
+    in :mod:`.circuit`) and returns ``(eval_wer_list, eval_p_adapt_list)`` like the reference.
     """
 
     def __init__(self, code_list: list, decoder1_class, decoder2_class):
@@ -807,7 +1033,8 @@ class CodeFamily_SpaceTime:
         assert noise_model in ["data", "phenl", "circuit"], "noise_model should be one of [data, phenl, circuit]"
         assert eval_logical_type in ["X", "Z", "Total"], "eval_type should be one of [X, Y, Total]"
         if noise_model == "circuit":
-            raise NotImplementedError("circuit-level noise needs stim's detector error models (absent; SURVEY.md §8f)")
+            return self._eval_wer_circuit(eval_logical_type, eval_p_list, num_samples, num_cycles, num_rep,
+                                          circuit_type, circuit_error_params, if_adaptive, adaptive_params)
         eval_wer_list, eval_p_adapt_list = [], []
         for eval_code in self.code_list:
             per_code = []
@@ -839,6 +1066,40 @@ class CodeFamily_SpaceTime:
             eval_p_adapt_list.append(np.array(eval_p_list))
         if noise_model == "data":
             return eval_wer_list, eval_p_list  # :1166 eval_p_adapt_list = eval_p_list
+        return eval_wer_list, eval_p_adapt_list
+
+    def _eval_wer_circuit(self, eval_logical_type, eval_p_list, num_samples, num_cycles, num_rep, circuit_type,
+                          circuit_error_params, if_adaptive, adaptive_params):
+        """``src/Simulators_SpaceTime.py:1220-1268``: per code the (optionally WEREst-pruned) p list;
+        per p the circuit and fault graphs, decoder1 on h1 and decoder2 on h2 from the factories
+        (``code_h`` = hx), then ``WordErrorRate(num_samples)``."""
+        eval_wer_list, eval_p_adapt_list = [], []
+        for eval_code in self.code_list:
+            if if_adaptive:
+                WEREst, min_wer = adaptive_params["WEREst"], adaptive_params["min_wer"]
+                plist = [ep for ep in eval_p_list if WEREst(eval_code.N, ep) >= min_wer]
+            else:
+                plist = eval_p_list
+            per_code = []
+            for eval_p in plist:
+                p = eval_p
+                cep = circuit_error_params
+                error_params = {k: cep[k] * p for k in ("p_i", "p_state_p", "p_m", "p_CX", "p_idling_gate")}
+                sim = CodeSimulator_Circuit_SpaceTime(code=eval_code, decoder1_z=None, decoder1_x=None,
+                                                      decoder2_z=None, decoder2_x=None, p=p, num_cycles=num_cycles,
+                                                      num_rep=num_rep, error_params=error_params,
+                                                      eval_logical_type=eval_logical_type, circuit_type=circuit_type,
+                                                      rand_scheduling_seed=1)
+                sim._generate_circuit()
+                sim._generate_circuit_graph()
+                g = sim.circuit_graph
+                sim.decoder1_z = self.decoder1_class.GetDecoder({"code_h": eval_code.hx, "h": g["h1"],
+                                                                 "channel_probs": g["channel_ps1"]})
+                sim.decoder2_z = self.decoder2_class.GetDecoder({"code_h": eval_code.hx, "h": g["h2"],
+                                                                 "channel_probs": g["channel_ps2"]})
+                per_code.append(sim.WordErrorRate(num_samples=num_samples)[0])
+            eval_p_adapt_list.append(np.array(plist))
+            eval_wer_list.append(np.array(per_code))
         return eval_wer_list, eval_p_adapt_list
 
     def EvalThreshold(self, noise_model: str, eval_logical_type: str, eval_method: str, est_threshold: float,

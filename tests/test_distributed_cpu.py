@@ -198,3 +198,18 @@ def test_decoders_default_to_local_rank_device(monkeypatch):
                 decoders.BPOSD_Decoder_Class, decoders.ST_BP_Decoder_Class, decoders.FirstMinBPDecoder,
                 engine.DeviceBP, engine.DeviceGraph):
         assert inspect.signature(cls.__init__).parameters["device"].default is None, cls
+
+
+def test_native_shard_split_equals_shard_range():
+    """qldpc_mc_run_sharded's per-device shot blocks (the C ABI's qldpc_shard_range, host-only) are
+    parallel.shard_range's: contiguous, covering, sizes within one (bench.py --comm native)."""
+    from qldpc_fault_tolerance_amd import _native, parallel
+
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libqldpc_hip.so not built")
+    for total in (0, 1, 7, 64, 1000, 262_144 * 8 + 5):
+        for n in (1, 2, 3, 4, 7, 8):
+            blocks = [parallel.native_shard_range(total, n, d) for d in range(n)]
+            assert blocks == [parallel.shard_range(total, d, n) for d in range(n)]
+            assert sum(c for _, c in blocks) == total
+            assert all(blocks[d][0] + blocks[d][1] == blocks[d + 1][0] for d in range(n - 1))

@@ -1,0 +1,136 @@
+"""Circuit-level space-time decoding on the GPU (csrc/circuit.hip).
+
+* The DEM sampler (``qldpc_circ_sample``) == the oracle's Philox draws of every mechanism, and the
+  detector / observable bits the fused launch decodes are the same draws.
+* The fused shot loop (``qldpc_circ_launch``: rounds of decoder1 on h1, space / logical
+  corrections, decoder2 BP+OSD on h2 through the host OSD stage, failure check) == the oracle's
+  restatement of ``CodeSimulator_Circuit_SpaceTime._decoding_samples`` per sample
+  (``oracle/circuit_oracle.py``), bit for bit.
+* The reference's per-sample plugin path (``_decoding_samples`` with foreign decoders) == the fused
+  path on the same samples.
+* The demo (``SpaceTimeDecodingDemo.ipynb`` cells 2-3: d3 toric, p = 1e-3, CX noise only,
+  num_rep 3, num_cycles 13, BP + BP+OSD-E(10)) against its printed WER 0.000193 (10,000 samples):
+  the printed failure count must be a plausible binomial draw at the engine's rate.  This is the
+  only stim-era output the reference holds; everything else here is parity-unpinned against stim.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from qldpc_fault_tolerance_amd import codes
+
+pytestmark = pytest.mark.gpu
+
+
+def _ring(d):
+    h = np.zeros((d, d), np.uint8)
+    for i in range(d):
+        h[i, i] = h[i, (i + 1) % d] = 1
+    return h
+
+
+def _sim(p, ep_scale, num_cycles=13, num_rep=3, osd=True, max_iter_ratio=10, circuit_type="coloration", seed=7):
+    from qldpc_fault_tolerance_amd.decoders import ST_BP_Decoder_Circuit, ST_BPOSD_Decoder_Circuit
+    from qldpc_fault_tolerance_amd.simulators import CodeSimulator_Circuit_SpaceTime
+
+    code = codes.hgp(_ring(3), _ring(3))
+    ep = {k: v * p for k, v in ep_scale.items()}
+    sim = CodeSimulator_Circuit_SpaceTime(code=code, p=p, num_cycles=num_cycles, num_rep=num_rep, error_params=ep,
+                                          eval_logical_type="Z", circuit_type=circuit_type, seed=seed)
+    sim._generate_circuit()
+    sim._generate_circuit_graph()
+    g = sim.circuit_graph
+    mi = int(code.N / max_iter_ratio)
+    sim.decoder1_z = ST_BP_Decoder_Circuit(g["h1"], g["channel_ps1"], mi, "minimum_sum", 0.625)
+    if osd:
+        sim.decoder2_z = ST_BPOSD_Decoder_Circuit(g["h2"], g["channel_ps2"], mi, "minimum_sum", 0.625, "osd_e", 10)
+    else:
+        sim.decoder2_z = ST_BP_Decoder_Circuit(g["h2"], g["channel_ps2"], mi, "minimum_sum", 0.625)
+    return sim, mi
+
+
+ALL_NOISE = {"p_i": 1.0, "p_state_p": 1.0, "p_m": 1.0, "p_CX": 1.0, "p_idling_gate": 1.0}
+DEMO = {"p_i": 0.0, "p_state_p": 0.0, "p_m": 0.0, "p_CX": 1.0, "p_idling_gate": 0.0}
+
+
+def test_dem_sampler_matches_oracle_draws(gpu):
+    import circuit_oracle
+
+    sim, _ = _sim(4e-3, ALL_NOISE)
+    dem = sim.dem
+    S = 192
+    got = sim._device().sample(sim.seed, 1000, S)
+    e = circuit_oracle.sample_mechanisms(dem.probs, sim.seed, 1000, S).astype(np.int64)
+    want = np.hstack([(e @ dem.check_matrix().T.astype(np.int64)) % 2, (e @ dem.observable_matrix().T.astype(np.int64)) % 2])
+    assert got.shape == want.shape and np.array_equal(got, want.astype(np.uint8))
+
+
+@pytest.mark.parametrize("osd,ratio,ctype", [(True, 10, "coloration"), (False, 3, "random"), (True, 2, "random")])
+def test_fused_circuit_loop_matches_oracle_per_sample(gpu, osd, ratio, ctype):
+    import circuit_oracle
+
+    sim, mi = _sim(3e-3, ALL_NOISE, osd=osd, max_iter_ratio=ratio, circuit_type=ctype)
+    g = sim.circuit_graph
+    dev = sim._device()
+    S, b0 = 1500, 4242
+    res = dev.run(sim.seed, b0, S, per_shot=True)
+    ref = circuit_oracle.circuit_run(sim.dem, g["h1"], g["L1"], g["channel_ps1"], sim.h1_space_cor, g["h2"], g["L2"],
+                                     g["channel_ps2"], sim.num_rounds, sim.num_rep, sim.num_checks, mi, mi,
+                                     sim.seed, b0, S, final_osd=osd)
+    D = sim.dem.num_detectors
+    assert np.array_equal(res.detobs[:, :D], ref["det"]) and np.array_equal(res.detobs[:, D:], ref["logical"])
+    assert np.array_equal(res.fail, ref["fail"]), (int(res.fail.sum()), ref["failures"])
+    assert res.failures == ref["failures"] and res.shots == S
+    assert res.sector_decodes == [S * sim.num_rounds, S]
+    assert 0 < ref["failures"] < S  # informative: both outcomes occur
+
+
+def test_plugin_path_equals_fused_path(gpu):
+    """Foreign decoders (plain objects with .decode, the reference's plugin contract) run
+    ``_decoding_samples`` per sample on GPU-sampled detectors; on the same draws the fused launch
+    counts the same failures."""
+    import oracle
+
+    sim, mi = _sim(3e-3, ALL_NOISE, osd=False, max_iter_ratio=3)
+    g = sim.circuit_graph
+
+    class OracleBP:
+        def __init__(self, h, p):
+            self.h, self.p = np.asarray(h, np.uint8), np.asarray(p)
+
+        def decode(self, synd):
+            c, _, _ = oracle.bp_decode_batch(self.h, self.p, mi, "minimum_sum", 0.625,
+                                             np.asarray(synd).reshape(1, -1).astype(np.uint8), 64)
+            return c[0].astype(np.int64)
+
+    S = 400
+    fused = sim.fused_counts(S).failures
+    sim._shot_offset = 0  # the same draws again
+    sim.decoder1_z, sim.decoder2_z = OracleBP(g["h1"], g["channel_ps1"]), OracleBP(g["h2"], g["channel_ps2"])
+    assert sim._engine_parts() is None
+    assert sim._batch_failures(S) == fused
+    assert 0 < fused < S
+
+
+def test_demo_wer_against_printed(gpu):
+    """SpaceTimeDecodingDemo.ipynb cell 3: WordErrorRate(10000) = 0.00019299501269032238.  The
+    engine's rate over 2e6 samples; the printed value's failure count (inverted through the per-cycle
+    WER formula, K = 2, 13 cycles) must lie inside the central 99.9 % of Binomial(10000, engine LER)."""
+    from scipy import stats
+
+    sim, _ = _sim(1e-3, DEMO)
+    assert sim.num_rounds == 4 and sim.K == 2
+    S = 2_000_000
+    res = sim.fused_counts(S)
+    ler = res.failures / S
+    w = 0.00019299501269032238
+    ler_q = (1 - (1 - 2 * w) ** 13) / 2
+    printed_ler = 1 - (1 - ler_q) ** 2
+    k = round(printed_ler * 10000)
+    assert abs(printed_ler * 10000 - k) < 1e-6  # an integer count: the inversion is exact
+    lo, hi = stats.binom.ppf([0.0005, 0.9995], 10000, ler)
+    print(f"engine LER {ler:.5g} ({res.failures}/{S}); printed count {k}/10000; 99.9% band [{lo}, {hi}]")
+    assert lo <= k <= hi
+    wer, _ = sim.WordErrorRate(10000)
+    assert 0 < wer < 1e-3 and math.isfinite(wer)
