@@ -56,7 +56,10 @@ def parse():
     ap.add_argument("--logical", default="Total", choices=("X", "Z", "Total"))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="data", choices=("data", "phenl", "bposd"),
+    ap.add_argument("--comm", default="torch", choices=("torch", "native"),
+                    help="torch: one rank per GPU (torchrun), counters all-reduced by torch.distributed; native: ONE "
+                         "process drives --gpus GPUs through the C ABI (qldpc_mc_run_sharded + qldpc_comm_init_all)")
+    ap.add_argument("--workload", default="data", choices=("data", "phenl", "bposd", "circuit"),
                     help="data = headline (config 2); phenl = space-time phenomenological (config 5)")
     ap.add_argument("--num-rep", type=int, default=3)
     ap.add_argument("--dec2", default="bp", choices=("bp", "bposd"),
@@ -69,6 +72,19 @@ def pauli_probs(eval_p):
     """EvalWER data branch arithmetic (src/Simulators.py:763-764): p = eval_p*3/2, [p/3]*3."""
     p = eval_p * 3 / 2
     return p / 3, p / 3, p / 3
+
+
+def cpu_model() -> str:
+    """The host CPU (lscpu's "Model name", from /proc/cpuinfo) for the cpu_baseline record."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.lower().startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(code, eval_p, max_iter, logical, budget_s):
@@ -89,7 +105,8 @@ def cpu_baseline(code, eval_p, max_iter, logical, budget_s):
     r = oracle.mc_run(code, px, py, pz, seed=SEED, shot_begin=0, shot_count=S2, logical_mode=logical,
                       probs_x=eval_p, probs_z=eval_p, max_iter=max_iter, precision=64, nthreads=cores)
     dt = time.perf_counter() - t0
-    return {"value": S2 / dt, "unit": "shots/s", "cores": cores, "kind": "port",
+    return {"value": S2 / dt, "unit": "shots/s", "cores": cores, "kind": "port", "cpu_model": cpu_model(),
+            "host_logical_cpus": os.cpu_count(),
             "sample": f"{S2} shots of the same workload (shots 0..{S2 - 1}, same seed), oracle/qldpc_oracle.c "
                       f"fp64 with {cores} OpenMP threads, {dt:.1f} s; LER={r['failures'] / S2:.4g}",
             "note": "ORACLE PORT, not the reference: the reference's own CPU path (Python + the third-party ldpc "
@@ -460,6 +477,125 @@ def bposd_main(a, torch, dist, world, rank, dev):
         dist.destroy_process_group()
 
 
+def native_comm_main(a, torch):
+    """``--comm native``: ONE process drives ``--gpus`` GPUs through the C ABI only, as a host that
+    binds ``libqldpc_hip.so`` without torch.distributed would: per GPU its own
+    decoders and MC handle, ``qldpc_comm_init_all`` communicators, and per step one
+    ``qldpc_mc_run_sharded`` call over ``--shots`` x N global shots (per-device blocks =
+    parallel.shard_range, one host thread per device, one grouped RCCL all-reduce of the counters)."""
+    from qldpc_fault_tolerance_amd import codes
+    from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceMC, run_sharded
+    from qldpc_fault_tolerance_amd.parallel import NativeComm
+
+    if a.workload != "data":
+        raise SystemExit("--comm native runs the data workload (config 2)")
+    n = int(a.gpus)
+    ndev = torch.cuda.device_count()
+    if n > ndev:
+        raise SystemExit(f"--comm native --gpus {n}: only {ndev} GPUs visible")
+    code = codes.get_code(a.code)
+    N = code.N
+    mi = int(N / a.max_iter_ratio)
+    p, S = a.p, int(a.shots)
+    px, py, pz = pauli_probs(p)
+    mcs = []
+    for d in range(n):
+        dx = DeviceBP(code.hz, p * np.ones(N), max_iter=mi, ms_scaling_factor=0.625, precision=a.precision, device=d)
+        dz = DeviceBP(code.hx, p * np.ones(N), max_iter=mi, ms_scaling_factor=0.625, precision=a.precision, device=d,
+                      vars_per_thread=dx.geometry()["vars_per_thread"])
+        mcs.append(DeviceMC(code, dx, dz))
+    comms = NativeComm.init_all(list(range(n))) if n > 1 else None
+    for i in range(a.warmup):
+        run_sharded(mcs, comms, px, py, pz, SEED, i * S * n, S * n, a.logical)
+    for d in range(n):
+        torch.cuda.synchronize(d)
+    t0 = time.perf_counter()
+    res = None
+    for i in range(a.steps):
+        r = run_sharded(mcs, comms, px, py, pz, SEED, (a.warmup + i) * S * n, S * n, a.logical)
+        res = r if res is None else res.merge(r)
+    elapsed = time.perf_counter() - t0
+    if res.shots != S * n * a.steps:
+        raise RuntimeError(f"counter mismatch: {res.shots} != {S} x {n} x {a.steps}")
+    dec = sum(res.sector_decodes)
+    emit({"metric": "BP-decoded shots/sec (node) on hgp_34_n1600 + % of HBM/LDS roofline", "value": res.shots / elapsed,
+          "unit": "shots/s", "n_gpus": n, "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
+          "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+          "dtype": "f32" if a.precision == 32 else "f64",
+          "data": "synthetic: Philox-sampled depolarizing errors on the synthesized [[1600,64]] HGP stand-in",
+          "config": {"workload": f"{a.code} code-capacity BP shot loop, eval_p={p}, min-sum alpha=0.625, max_iter={mi}, "
+                                 f"eval_logical_type={a.logical}", "code": a.code, "p": p, "shots_per_gpu_step": S,
+                     "parallelism": f"shot-sharded x{n}, one process, C-ABI qldpc_mc_run_sharded"
+                                    + (" + qldpc_comm_init_all (RCCL)" if comms else "")},
+          "decodes_per_s": dec / elapsed, "mean_iters_per_decode": sum(res.sector_iters) / max(dec, 1),
+          "logical_error_rate": res.failures / max(res.shots, 1), "comm": "native"})
+
+
+def circuit_main(a, torch, dist, world, rank, dev):
+    """Circuit-level space-time (not the headline): the demo configuration of
+    SpaceTimeDecodingDemo.ipynb cell 2 (hgp(ring_code(3), ring_code(3)), p = 1e-3, CX noise only,
+    num_rep 3, num_cycles 13, ST_BP_Decoder_Circuit + ST_BPOSD_Decoder_Circuit OSD-E(10)) unless
+    --p / --num-rep / --num-cycles say otherwise.  One step = ``--shots`` samples per GPU through
+    ``qldpc_circ_launch`` (DEM sampling, the round loop, decoder2 BP+OSD on the host OSD stage)."""
+    from qldpc_fault_tolerance_amd import codes
+    from qldpc_fault_tolerance_amd.decoders import ST_BP_Decoder_Circuit, ST_BPOSD_Decoder_Circuit
+    from qldpc_fault_tolerance_amd.simulators import CodeSimulator_Circuit_SpaceTime
+
+    ring = np.zeros((3, 3), np.uint8)
+    for i in range(3):
+        ring[i, i] = ring[i, (i + 1) % 3] = 1
+    code = codes.hgp(ring, ring, name="toric_d3")
+    p = a.p if a.p != DEFAULT_P else 1e-3
+    ep = {"p_i": 0.0, "p_state_p": 0.0, "p_m": 0.0, "p_CX": p, "p_idling_gate": 0.0}
+    sim = CodeSimulator_Circuit_SpaceTime(code=code, p=p, num_cycles=a.num_cycles, num_rep=a.num_rep, error_params=ep,
+                                          eval_logical_type="Z", seed=SEED + 7)
+    sim._generate_circuit()
+    sim._generate_circuit_graph()
+    g = sim.circuit_graph
+    mi = int(code.N / 10)
+    sim.decoder1_z = ST_BP_Decoder_Circuit(g["h1"], g["channel_ps1"], mi, "minimum_sum", 0.625, device=dev.index)
+    sim.decoder2_z = ST_BPOSD_Decoder_Circuit(g["h2"], g["channel_ps2"], mi, "minimum_sum", 0.625, "osd_e", 10,
+                                              device=dev.index)
+    S = int(a.shots)
+    for _ in range(a.warmup):
+        sim.fused_counts(S * world)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    shots = fails = 0
+    for _ in range(a.steps):
+        r = sim.fused_counts(S * world)
+        shots, fails = shots + r.shots, fails + r.failures
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    from qldpc_fault_tolerance_amd.simulators import word_error_rate_per_cycle
+
+    out = {"metric": "circuit-level space-time samples/sec (SURVEY 8f rank 4; not the headline)",
+           "value": shots / elapsed, "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f64", "data": "synthetic: Philox-sampled DEM mechanisms of the restated stim circuit",
+           "config": {"workload": f"toric d3 (hgp(ring_code(3), ring_code(3))), p_CX={p}, num_rep={a.num_rep}, "
+                                  f"num_cycles={a.num_cycles}, BP (max_iter {mi}) rounds + BP+OSD-E(10) final",
+                      "samples_per_gpu_step": S, "dem_mechanisms": sim.dem.num_errors,
+                      "h1": list(np.shape(g["h1"])), "h2": list(np.shape(g["h2"])),
+                      "parallelism": f"sample-sharded x{world}"},
+           "logical_error_rate": fails / max(shots, 1),
+           "wer_per_cycle": word_error_rate_per_cycle(fails, shots, code.K, a.num_cycles),
+           "printed_reference_wer": 0.00019299501269032238 if p == 1e-3 and a.num_cycles == 13 and a.num_rep == 3
+           else None}
+    if rank == 0:
+        emit(out)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 _JSON_FD = None  # the real stdout: the JSON line is the only thing written there
 
 
@@ -475,7 +611,7 @@ def emit(out):
 def main():
     global _JSON_FD
     a = parse()
-    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1 and a.comm == "torch":
         sys.exit(spawn_ranks(a.gpus))
     # library chatter on fd 1 (gloo's connection lines, runtime notices) goes to stderr, so rank 0's
     # stdout carries exactly one JSON line
@@ -484,7 +620,7 @@ def main():
     os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     traffic = None
-    if a.workload == "data" and world == 1 and a.pmc_traffic:
+    if a.workload == "data" and world == 1 and a.pmc_traffic and a.comm == "torch":
         traffic = pmc_traffic(a)  # child processes, before this process initialises the GPU
     import torch
     import torch.distributed as dist
@@ -503,6 +639,10 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    if a.comm == "native":
+        return native_comm_main(a, torch)
+    if a.workload == "circuit":
+        return circuit_main(a, torch, dist, world, rank, dev)
     if a.workload == "phenl":
         return phenl_main(a, torch, dist, world, rank, dev)
     if a.workload == "bposd":

@@ -16,6 +16,7 @@
 //   mode 2 wr_mix  : its stores only (9 b64)
 //   mode 3 rd64    : 16 x ds_read_b64
 //   mode 4 rd128   : 8 x ds_read_b128
+//   mix_pipe(2)    : the row mix software-pipelined (1 or 2 rows per loop trip), stores overlapping loads
 // Prints per mode: time, LDS bytes moved, TB/s, and for mode 0 the algorithmic-byte equivalent.
 // Usage (GPU box): ./lds_calib [iters]   and under  rocprofv3 --pmc SQ_INSTS_LDS_LOAD_BANDWIDTH
 // SQ_INSTS_LDS_STORE_BANDWIDTH --kernel-trace -- ./lds_calib  for the counter calibration.
@@ -89,6 +90,76 @@ __global__ void __launch_bounds__(kThreads) lds_mix(int iters, unsigned long lon
   if (acc == 0x123456789ull) out[blockIdx.x] = acc;  // keeps the loads
 }
 
+// mode 5 "mix_pipe": the row mix software-pipelined like the kernel's variable phase (stores of
+// row r issued between the loads of row r + 1, their data from the previous iteration), so the
+// read and store paths overlap: 2 loads : 1 store, 15 b64 + 3 b128 loads and 9 b64 stores per row.
+template <int ROWS>
+__global__ void __launch_bounds__(kThreads) lds_pipe(int iters, unsigned long long* out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char img[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  auto* base = (__attribute__((address_space(3))) unsigned char*)img;
+  for (int i = tid; i < kImage / 8; i += kThreads) reinterpret_cast<lds_u64*>(base)[i] = (unsigned long long)i * 0x9E37u;
+  __syncthreads();
+  const int o64 = wave * 512 + lane * 8, o128 = wave * 1024 + lane * 16;
+  unsigned long long prev[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) prev[k] = (unsigned long long)(tid + k);
+  unsigned long long acc = 0;
+  for (int it = 0; it < iters; ++it) {
+    const int rot = opaque(it & 7);
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+      unsigned long long ld[18];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        // two loads, then one store of the previous row's data
+        const int a = 2 * k, b = 2 * k + 1;
+        if (a < 15) {
+          ld[a] = *reinterpret_cast<lds_u64*>(base + (((a + rot + r) * 2048 + o64) & (kReadRegion - 1)));
+        } else {
+          const u32x4 v = *reinterpret_cast<lds_u128*>(base + (((a + rot + r) * 4096 + o128) & (kReadRegion - 1)));
+          ld[a] = ((unsigned long long)v.x | ((unsigned long long)v.y << 32)) ^ ((unsigned long long)v.z << 7) ^ v.w;
+        }
+        if (b < 15) {
+          ld[b] = *reinterpret_cast<lds_u64*>(base + (((b + rot + r) * 2048 + o64) & (kReadRegion - 1)));
+        } else {
+          const u32x4 v = *reinterpret_cast<lds_u128*>(base + (((b + rot + r) * 4096 + o128) & (kReadRegion - 1)));
+          ld[b] = ((unsigned long long)v.x | ((unsigned long long)v.y << 32)) ^ ((unsigned long long)v.z << 7) ^ v.w;
+        }
+        *reinterpret_cast<lds_u64*>(base + kWriteBase + ((k + rot + r) % 9) * 2048 + o64) = prev[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) prev[k] = ld[2 * k] ^ ld[2 * k + 1];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc ^= prev[k];
+  if (acc == 0x123456789ull) out[blockIdx.x] = acc;
+}
+
+template <int ROWS>
+int run_pipe(const char* name, int iters, unsigned long long* out, int cus) {
+  const dim3 grid(cus * 3), block(kThreads);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  hipLaunchKernelGGL(lds_pipe<ROWS>, grid, block, kImage, 0, 4, out);
+  CK(hipEventRecord(a));
+  hipLaunchKernelGGL(lds_pipe<ROWS>, grid, block, kImage, 0, iters, out);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  // per lane and row: 15 x 8 + 3 x 16 = 168 B read, 9 x 8 = 72 B written
+  const double rows = (double)grid.x * kThreads * iters * ROWS, s = ms * 1e-3;
+  printf("{\"mode\": \"%s\", \"ms\": %.3f, \"read_bytes\": %.6e, \"write_bytes\": %.6e, \"TBps\": %.3f, "
+         "\"rows_per_s\": %.6e, \"algorithmic_TBps\": %.3f}\n", name, ms, rows * 168, rows * 72, rows * 240 / s / 1e12,
+         rows / s, rows * 224.0 / s / 1e12);
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return 0;
+}
+
 template <int MODE>
 int run(const char* name, int iters, unsigned long long* out, double rd_b, double wr_b, int cus) {
   const dim3 grid(cus * 3), block(kThreads);
@@ -130,6 +201,8 @@ int main(int argc, char** argv) {
   CK(hipFuncSetAttribute((const void*)lds_mix<2>, hipFuncAttributeMaxDynamicSharedMemorySize, kImage));
   CK(hipFuncSetAttribute((const void*)lds_mix<3>, hipFuncAttributeMaxDynamicSharedMemorySize, kImage));
   CK(hipFuncSetAttribute((const void*)lds_mix<4>, hipFuncAttributeMaxDynamicSharedMemorySize, kImage));
+  CK(hipFuncSetAttribute((const void*)lds_pipe<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kImage));
+  CK(hipFuncSetAttribute((const void*)lds_pipe<2>, hipFuncAttributeMaxDynamicSharedMemorySize, kImage));
   printf("{\"cus\": %d, \"iters\": %d, \"workgroups_per_cu\": 3, \"threads\": %d, \"lds_per_workgroup\": %d}\n", cus,
          iters, kThreads, kImage);
   // bytes per lane per iteration
@@ -138,6 +211,8 @@ int main(int argc, char** argv) {
   if (run<2>("wr_mix", iters, out, 0, 9 * 8, cus)) return 1;
   if (run<3>("rd64", iters, out, 16 * 8, 0, cus)) return 1;
   if (run<4>("rd128", iters, out, 8 * 16, 0, cus)) return 1;
+  if (run_pipe<1>("mix_pipe", iters, out, cus)) return 1;
+  if (run_pipe<2>("mix_pipe2", iters / 2, out, cus)) return 1;
   CK(hipDeviceSynchronize());
   return 0;
 }
