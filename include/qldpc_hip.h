@@ -287,6 +287,10 @@ int qldpc_mc_set_osd(qldpc_mc *mc, qldpc_osd_gpu *osd_x, qldpc_osd_gpu *osd_z);
  * the first) with the identity check order (`before`) and with the labels the
  * decoder uses (`after`, host-side label search at create time; QLDPC_LABEL=0
  * disables it).  0 / 0 for the other engines. */
+/* Static LDS model of the engine-3 fp64 variable phase, per workgroup and iteration (zeros for other
+ * families): out6 = {CS-gather LDS cycles, of which bank-conflict extra; V-slot read cycles, extra;
+ * v2c store group-cycles, extra} under the lane-group rules of MI355X_MICROARCH.md §LDS. */
+int qldpc_bp_lds_model(const qldpc_bp *bp, int64_t *out6);
 int qldpc_bp_bank_stats(const qldpc_bp *bp, int32_t *before, int32_t *after);
 
 /*

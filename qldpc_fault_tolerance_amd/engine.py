@@ -139,6 +139,10 @@ class DeviceBP:
         _native.check(_native.lib().qldpc_bp_kernel_id(self.handle, ctypes.byref(kid), ctypes.byref(nch)),
                       "bp_kernel_id")
         g["kernel_id"], g["row_chunks"] = kid.value, nch.value
+        lm = (ctypes.c_int64 * 6)()
+        _native.check(_native.lib().qldpc_bp_lds_model(self.handle, lm), "bp_lds_model")
+        g["lds_model"] = dict(zip(["cs_gather", "cs_gather_extra", "v_read", "v_read_extra", "v_store", "v_store_extra"],
+                                  list(lm)))
         return g
 
     def decode_batch_device(self, synd_dev, corr_dev, iters_dev=None, conv_dev=None, stream=None):
