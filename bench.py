@@ -520,6 +520,31 @@ def bposd_main(a, torch, dist, world, rank, dev):
         dist.destroy_process_group()
 
 
+def native_comm_check(torch, dist, world, rank, dev, local, reduced):
+    """After the timed steps (outside the timed region), all-reduce this rank's counters a second time
+    through the engine's own C-ABI collective (qldpc_comm_init_rank + qldpc_comm_allreduce_counters,
+    RCCL dlopen'ed by libqldpc_hip.so; rank 0's unique id broadcast over torch.distributed) and compare
+    with torch.distributed's result.  Never fatal: a failure is reported in the JSON line."""
+    if os.environ.get("QLDPC_NATIVE_COMM_CHECK", "1") == "0" or os.environ.get("QLDPC_DIST_BACKEND", "nccl") != "nccl":
+        return None
+    try:
+        from qldpc_fault_tolerance_amd.parallel import NativeComm
+
+        uid = [NativeComm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = NativeComm(dev.index, world, rank, uid[0])
+        comm.allreduce_counters(local)
+        torch.cuda.synchronize(dev)
+        same = bool(torch.equal(local, reduced))
+        comm.close()
+        ok = torch.tensor([1 if same else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        return {"native_allreduce_equals_torch": bool(ok.item()), "ranks": world,
+                "how": "qldpc_comm_init_rank + qldpc_comm_allreduce_counters (C ABI, RCCL) on each rank's counters"}
+    except Exception as e:  # noqa: BLE001
+        return {"native_allreduce_equals_torch": None, "error": repr(e)[:300]}
+
+
 def native_comm_main(a, torch):
     """``--comm native``: ONE process drives ``--gpus`` GPUs through the C ABI only, as a host that
     binds ``libqldpc_hip.so`` without torch.distributed would: per GPU its own
@@ -743,6 +768,7 @@ def main():
         "mean_iters_per_decode": r["iters"] / max(r["decodes"], 1),
         "nonconverged_frac": r["nonconv"] / max(r["decodes"], 1),
         "logical_error_rate": r["failures"] / max(r["shots"], 1),
+        "comm_check": r.get("comm_check"),
         "roofline": {"bound": bound, "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": roof_traffic,
                      "traffic_over_algorithmic": (roof_traffic / bytes_per_launch) if roof_traffic else None,
@@ -820,6 +846,7 @@ def time_data(a, precision, torch, dist, world, rank, dev):
         ev[i][0].record(stream)
         step(a.warmup + i)
         ev[i][1].record(stream)
+    local = cnt.clone() if world > 1 else None  # this rank's counters (for the C-ABI cross-check)
     if world > 1:
         dist.all_reduce(cnt)  # shots, failures, iterations, non-converged, histogram
     torch.cuda.synchronize(dev)
@@ -832,6 +859,8 @@ def time_data(a, precision, torch, dist, world, rank, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    comm_check = native_comm_check(torch, dist, world, rank, dev, local, cnt) if world > 1 and precision == a.precision \
+        else None
     w = cnt.cpu().numpy()
     shots = int(w[0])
     if shots != S * a.steps * world:
@@ -839,7 +868,7 @@ def time_data(a, precision, torch, dist, world, rank, dev):
     return {"value": shots / elapsed, "elapsed": elapsed, "kern_ms": kern_ms, "shots": shots, "failures": int(w[1]),
             "decodes": int(w[2] + w[3]), "iters": int(w[4] + w[5]), "nonconv": int(w[6] + w[7]),
             "kernel": kernel_name(dx or dz), "engine": (dx or dz).geometry()["engine"],
-            "kernel_id": (dx or dz).geometry().get("kernel_id")}
+            "kernel_id": (dx or dz).geometry().get("kernel_id"), "comm_check": comm_check}
 
 
 if __name__ == "__main__":
