@@ -203,6 +203,7 @@ int main(int argc, char** argv) {
   CK(hipFuncSetAttribute((const void*)lds_mix<4>, hipFuncAttributeMaxDynamicSharedMemorySize, kImage));
   CK(hipFuncSetAttribute((const void*)lds_pipe<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kImage));
   CK(hipFuncSetAttribute((const void*)lds_pipe<2>, hipFuncAttributeMaxDynamicSharedMemorySize, kImage));
+  CK(hipFuncSetAttribute((const void*)lds_pipe<4>, hipFuncAttributeMaxDynamicSharedMemorySize, kImage));
   printf("{\"cus\": %d, \"iters\": %d, \"workgroups_per_cu\": 3, \"threads\": %d, \"lds_per_workgroup\": %d}\n", cus,
          iters, kThreads, kImage);
   // bytes per lane per iteration
@@ -213,6 +214,7 @@ int main(int argc, char** argv) {
   if (run<4>("rd128", iters, out, 8 * 16, 0, cus)) return 1;
   if (run_pipe<1>("mix_pipe", iters, out, cus)) return 1;
   if (run_pipe<2>("mix_pipe2", iters / 2, out, cus)) return 1;
+  if (run_pipe<4>("mix_pipe4", iters / 4, out, cus)) return 1;
   CK(hipDeviceSynchronize());
   return 0;
 }
