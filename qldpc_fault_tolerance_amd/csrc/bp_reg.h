@@ -136,7 +136,9 @@ template <typename T, int ENG>
 constexpr int lb_waves(int LB) {
   // engine 4 fp64 images (no CS array) fit 3 workgroups per CU: <= 168 VGPRs
   // (the fp64 512-thread family: 2 workgroups of 8 waves per CU, 128 VGPRs)
-  return LB <= 256 ? (sizeof(T) == 8 ? ((eng_base(ENG) == 4 || eng_m2x(ENG)) ? 3 : 2) : 4)
+  // (the one-word family with packed addresses, engine id 10203: 4 workgroups per CU, 128 VGPRs)
+  return LB <= 256 ? (sizeof(T) == 8 ? (eng_m2s(ENG) && (ENG / 100) % 10 == 2 ? 4
+                                        : (eng_base(ENG) == 4 || eng_m2x(ENG)) ? 3 : 2) : 4)
                    : (LB <= 512 && (eng_kv64(ENG) || eng_fb(ENG))) ? 4 : 1;
 }
 __device__ inline unsigned long long qstamp() {
@@ -311,10 +313,14 @@ struct RState {
   // unpacked and absolute (ea = CS address, ev = V slot address): no unpack / base add
   // per access, 2 VALU per edge and iteration fewer
   static constexpr bool kSplit = (ENG / 100) % 10 == 1 && sizeof(T) == 8;  // engine id 103 (not 303)
+  // + 200 instead of + 100 on the one-word family (engine id 10203): the edge's CS and V slot byte
+  // addresses packed absolute into one VGPR (images < 64 KiB), unpacked by one VALU each per access:
+  // 16 fewer VGPRs for 16 edges per thread (LP L30: 4 workgroups per CU instead of 3)
+  static constexpr bool kPk = (ENG / 100) % 10 == 2 && sizeof(T) == 8 && eng_m2s(ENG) && !eng_m2v(ENG);
   // absolute LDS addresses: split words, or (dword-scaled packed words: the space-time families
   // 13 / 1013 / 21013) absolute dword indices, unpacked by one SDWA shift per access and used
   // without a base add
-  static constexpr bool kAbs = kSplit || (eng_sh(ENG) == 2 && QLDPC_ABS_SH2);
+  static constexpr bool kAbs = kSplit || kPk || (eng_sh(ENG) == 2 && QLDPC_ABS_SH2);
   // m2s with QLDPC_M2S_UNIL: one prior for every variable (uniform channel_probs, host-checked),
   // loaded by a scalar load: 2 SGPRs instead of 2 * VPL VGPRs
   static constexpr bool kUniL = eng_m2x(ENG) && QLDPC_M2S_UNIL;
@@ -361,6 +367,8 @@ template <typename T, int DMAX, int VPL, int ENG>
 __device__ inline uint32_t r_csa(const RState<T, DMAX, VPL, ENG>& R, int k, int t) {
   if constexpr (RState<T, DMAX, VPL, ENG>::kSplit)
     return R.ea[k][t];
+  else if constexpr (RState<T, DMAX, VPL, ENG>::kPk)
+    return R.ea[k][t] & 0xFFFFu;
   else if constexpr (RState<T, DMAX, VPL, ENG>::kAbs)
     return sdwa_shl<0, 2>(R.ea[k][t]);
   else
@@ -370,6 +378,8 @@ template <typename T, int DMAX, int VPL, int ENG>
 __device__ inline uint32_t r_va(const RState<T, DMAX, VPL, ENG>& R, int k, int t) {
   if constexpr (RState<T, DMAX, VPL, ENG>::kSplit)
     return R.ev[k][t];
+  else if constexpr (RState<T, DMAX, VPL, ENG>::kPk)
+    return R.ea[k][t] >> 16;
   else if constexpr (RState<T, DMAX, VPL, ENG>::kAbs)
     return sdwa_shl<1, 2>(R.ea[k][t]);
   else
@@ -392,6 +402,8 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
         // c2s: the absolute address of the edge's F word (entry = check label + 1)
         R.ea[k][t] = eng_c2s(ENG) ? sbase + Ly.f + 4u * echk(e) : sbase + echk(e) * (uint32_t)((eng_m2s(ENG) ? 1 : 2) * sizeof(T));
         if constexpr (!RState<T, DMAX, VPL, ENG>::kM2v) R.ev[k][t] = sbase + va;
+      } else if constexpr (RState<T, DMAX, VPL, ENG>::kPk) {  // absolute byte addresses, packed
+        R.ea[k][t] = (sbase + echk(e) * (uint32_t)sizeof(T)) | ((sbase + va) << 16);
       } else if constexpr (RState<T, DMAX, VPL, ENG>::kAbs) {  // absolute dword indices
         R.ea[k][t] = ((sbase + echk(e) * (uint32_t)(2 * sizeof(T))) >> 2) | (((sbase + va) >> 2) << 16);
       } else {
@@ -466,6 +478,7 @@ template <typename T, int DMAX, int VPL, int ENG>
 __device__ inline uint32_t r_fa(const RState<T, DMAX, VPL, ENG>& R, int k, int t, uint32_t fbase) {
   // CS entry (i + 1) of 2 words (fp32: 8 B, fp64: 16 B) or, m2s, one fp64 word (8 B) -> F word i + 1
   // (byte-F kernels: fp32 CS entries of 8 B -> F byte i + 1)
+  if constexpr (RState<T, DMAX, VPL, ENG>::kPk) return ((R.ea[k][t] & 0xFFFFu) >> 1) + fbase;
   if constexpr (RState<T, DMAX, VPL, ENG>::kAbs && !RState<T, DMAX, VPL, ENG>::kSplit) {
     // absolute dword index w = csa / 4 in the low half: csa >> 3 = w >> 1, csa >> 1 = 2 w, csa >> 2 = w
     const uint32_t w = R.ea[k][t];
@@ -952,11 +965,11 @@ __device__ inline void m_gather(const RState<T, DMAX, VPL, ENG>& R, int k, typen
   using U = typename FT<T>::U;
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
-    if constexpr (!eng_c2s(ENG)) an[t] = lds_ld<U, true>(nullptr, R.ea[k][t]);  // (c2s: ea = F word)
+    if constexpr (!eng_c2s(ENG)) an[t] = lds_ld<U, true>(nullptr, r_csa(R, k, t));  // (c2s: ea = F word)
     if constexpr (eng_m2v(ENG))
       vn[t] = lds_ld<U, true>(nullptr, m2v_va<T, DMAX, VPL, ENG, D3K, LB>(R, k, t));
     else
-      vn[t] = lds_ld<U, true>(nullptr, R.ev[k][t]);
+      vn[t] = lds_ld<U, true>(nullptr, r_va(R, k, t));
   }
 }
 
@@ -967,7 +980,7 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
                                  double* post, const int32_t* perm) {
   using U = typename FT<T>::U;
   constexpr bool KV1 = RState<T, DMAX, VPL, ENG>::kKeepV;
-  static_assert(sizeof(T) == 8 && RState<T, DMAX, VPL, ENG>::kSplit &&
+  static_assert(sizeof(T) == 8 && (RState<T, DMAX, VPL, ENG>::kSplit || RState<T, DMAX, VPL, ENG>::kPk) &&
                     (RState<T, DMAX, VPL, ENG>::kKeepV || eng_c2s(ENG)),
                 "m2s / c2s: fp64 split-address family only");
   T c[ND];
@@ -1015,7 +1028,7 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     if constexpr (eng_m2v(ENG))
       lds_st<U, true>(nullptr, m2v_va<T, DMAX, VPL, ENG, D3K, LB>(R, k, t), nv[t]);
     else
-      lds_st<U, true>(nullptr, R.ev[k][t], nv[t]);
+      lds_st<U, true>(nullptr, r_va(R, k, t), nv[t]);
     if constexpr (KV1) R.ov[k][t] = nv[t];
   }
   if (x != xprev) {
@@ -1505,7 +1518,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   if (AB) M.fbase = Ly.f - (sbase >> (eng_fb(ENG) ? 3 : (sizeof(T) == 4 || eng_m2s(ENG)) ? 1 : 2));
   const uint32_t fdelta = eng_base(ENG) == 4 ? Ly.f : M.fbase;
   // waves whose lanes all hold padding variables skip the last variable (engine 4)
-  const bool last_live = uni((VPL - 1) * TB + (tid & ~63) < n ? 1 : 0) != 0;
+  const bool last_live = uni((VPL - 1) * TB + (tid & ~63) < S.npos ? 1 : 0) != 0;
   uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);
   uint32_t* flags = lred + 8;
   const bool adaptive = S.alpha == 0.0;

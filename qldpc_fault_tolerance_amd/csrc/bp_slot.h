@@ -53,6 +53,8 @@ struct SSector {
   // byte offsets from the V base per word), the last variable slot's first V slot and per-edge stride
   const uint32_t* rows;
   int vlast, vnl;
+  int npos;                         // 1 + the last slot position holding a variable (= n unless the
+                                    // slot map pads a degree class to whole variable slots)
 };
 
 struct SMcArgs {
@@ -495,6 +497,7 @@ __device__ inline SSector pick_ssector(const SMcArgs& A, int qi) {
   S.rows = b ? A.sec[1].rows : A.sec[0].rows;
   S.vlast = b ? A.sec[1].vlast : A.sec[0].vlast;
   S.vnl = b ? A.sec[1].vnl : A.sec[0].vnl;
+  S.npos = b ? A.sec[1].npos : A.sec[0].npos;
   return S;
 }
 

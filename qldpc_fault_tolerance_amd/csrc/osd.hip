@@ -364,6 +364,11 @@ __device__ inline unsigned long long osd_stamp() {
 #endif
 }
 constexpr int kOsdMaxN = 8192;
+// register-row mode: pivot-row words read per batch ahead of their xors
+#ifndef QLDPC_OSD_XB
+#define QLDPC_OSD_XB 8
+#endif
+constexpr int kOsdXB = QLDPC_OSD_XB;
 // A/B build: one barrier per pivot in register-row mode (the candidate row published before the
 // search barrier, per-wave slots of two step parities)
 #ifndef QLDPC_OSD_1B
@@ -773,13 +778,22 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
             any = any || upd[j];
           }
           if (any) {  // one broadcast read of each pivot word serves all of the thread's rows
+            // pivot-row words read kOsdXB ahead of their xors (a rolling buffer): written as
+            // read-xor pairs, the compiler chained them with a wait after each read (13 LDS round
+            // trips per pivot on the 25-word rows, round 4 asm review)
+            constexpr int XB = kOsdXB;
+            u64 buf[XB];
+#pragma unroll
+            for (int u = 0; u < XB; ++u)
+              if (q + u < WR) buf[u] = prow[q + u];
+            const uint32_t ps = (uint32_t)prow[WR];
 #pragma unroll
             for (int q2 = q; q2 < WR; ++q2) {
-              const u64 pv = prow[q2];
+              const u64 pv = buf[(q2 - q) % XB];
+              if (q2 + XB < WR) buf[(q2 - q) % XB] = prow[q2 + XB];
 #pragma unroll
               for (int j = 0; j < RPT; ++j) row[j][q2] ^= upd[j] ? pv : 0ull;
             }
-            const uint32_t ps = (uint32_t)prow[WR];
 #pragma unroll
             for (int j = 0; j < RPT; ++j) sbit[j] ^= upd[j] ? ps : 0u;
           }

@@ -99,7 +99,7 @@ bool use_f64x(int engine, int precision, int dmax, int tb, int vpl, int ea_shift
 
 // Slot-family kernels of an engine (2, 3 or 4).
 SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int d3k, int ea_shift = 0, int tb = 1024,
-                      int nch = 0, int tail = 0, int m2s = 0, int fb = 0, int d2k = 0) {
+                      int nch = 0, int tail = 0, int m2s = 0, int fb = 0, int d2k = 0, int pk = 0) {
   // fp32 space-time family with byte F words (rows of 2 chunks + a tail slot, 512 threads, 2 per CU)
   if (fb) {
     const bool ok = engine == 3 && precision == 32 && dmax == 4 && ea_shift == 2 && nch == 2 && tail && tb == 512;
@@ -107,6 +107,9 @@ SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int 
   }
   // fp64 m2-in-slot family (rows of 3 chunks + a tail slot, <= 256 threads, 3 workgroups per CU)
   if (m2s) {
+    // rows of 8 (4 chunks, no tail array), column degree 5, 256 threads: engine id 10103
+    if (m2s == 1 && engine == 3 && precision == 64 && dmax == 5 && ea_shift == 0 && nch == 4 && !tail && tb == 256)
+      return pk ? get_rvariant_f64_m2s8pk(vpl, d3k) : get_rvariant_f64_m2s8(vpl, d3k);
     const bool ok = engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && nch == 3 && tail && tb <= 256;
     if (m2s == 3)  // variable-major V slots: no tail array, 256 threads
       return (engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && tb == 256) ? get_rvariant_f64_m2v(vpl, d3k)
@@ -392,7 +395,8 @@ static int upload_llr(qldpc_bp* bp) {
 // decode path maps syndromes through the inverse permutation (bp->rperm).
 static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
                              const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1,
-                             const std::vector<int>& lab = {}, int tail = 0, int m2s = 0) {
+                             const std::vector<int>& lab = {}, int tail = 0, int m2s = 0, int d3k = 0,
+                             int dummy0 = -1, int* ndummy = nullptr) {
   const int nv = 16 / tsize;  // messages per 16-byte chunk
   const int rw = nch * nv;
   const int rwt = rw + (tail ? 1 : 0);  // tail layouts: logical slot rw = the row's tail slot
@@ -451,12 +455,15 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
             lslot[edge_of(i, j)] = best;
           }
         }
-    // Then a seeded annealed local search over the rows' slot permutations: swap the positions of
-    // two edges of one row (or move one into a free position) when Σ_read groups Σ_bank count²
-    // (weight 4: ds_read_b64, 32-lane groups, slot mod 32) + Σ_store groups Σ_bank count² (weight
-    // 1: ds_write_b64, 16-lane groups, slot mod 16) does not rise by more than the temperature.
+    // Then a seeded annealed local search over the rows' slot permutations (swap the positions of
+    // two edges of one row, or move one into a free position) on the EXACT cost of the lane-group
+    // bank model (qldpc_bp_lds_model): per 32-lane read group the maximum number of addresses on one
+    // bank pair (slot mod 32), per 16-lane store group the same over slot mod 16; objective = reads
+    // + ws * stores, temperature T0 falling linearly to 0 (round 4; tools/dev/place_opt3.cpp is the
+    // offline study: 20 M moves take the n1600 hz model from 362 / 715 to 327 / 442 cycles).
     const int iters = env_int("QLDPC_M2S_ANNEAL", 0);  // (opt-in until measured)
     if (iters > 0) {
+      const double T0 = env_int("QLDPC_M2S_ANNEAL_T", 50) * 1e-3, ws = env_int("QLDPC_M2S_ANNEAL_WS", 1000) * 1e-3;
       const int nrg = VPL * DM * ((TB + 31) / 32), nwg = VPL * DM * ((TB + 15) / 16);
       std::vector<int> erg(g->nnz, -1), ewg(g->nnz, -1);
       for (int k = 0; k < VPL; ++k)
@@ -470,26 +477,41 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
             ewg[e] = (k * DM + d) * ((TB + 15) / 16) + t / 16;
           }
         }
-      std::vector<int> rc((size_t)nrg * 32, 0), wc((size_t)nwg * 16, 0);
-      // position -> edge per row (-1 = free)
-      std::vector<int> at((size_t)g->m * rwt, -1);
+      // per group: addresses per bank and a histogram of those counts (max in O(1) amortised)
+      struct BankG {
+        uint8_t cnt[32] = {0};
+        int hist[64] = {0};
+        int mx = 0;
+        void add(int b) { hist[cnt[b]]--; hist[++cnt[b]]++; mx = std::max(mx, (int)cnt[b]); }
+        void sub(int b) { hist[cnt[b]]--; hist[--cnt[b]]++; while (mx > 0 && hist[mx] == 0) --mx; }
+        int cost() const { return mx > 1 ? mx : 1; }
+      };
+      std::vector<BankG> RG(nrg), WG(nwg);
+      std::vector<int> at((size_t)g->m * rwt, -1);  // position -> edge per row (-1 = free)
+      auto put = [&](int e, int i, int sg) {
+        const int sl = vbase_u + phys(i, lslot[e]);
+        if (sg > 0) { RG[erg[e]].add(sl % 32); WG[ewg[e]].add(sl % 16); }
+        else { RG[erg[e]].sub(sl % 32); WG[ewg[e]].sub(sl % 16); }
+      };
       for (int i = 0; i < g->m; ++i)
         for (int e = g->row_ptr[i]; e < g->row_ptr[i + 1]; ++e) {
           at[(size_t)i * rwt + lslot[e]] = e;
-          if (erg[e] < 0) continue;
-          const int sl = vbase_u + phys(i, lslot[e]);
-          rc[(size_t)erg[e] * 32 + sl % 32]++;
-          wc[(size_t)ewg[e] * 16 + sl % 16]++;
+          if (erg[e] >= 0) put(e, i, +1);
         }
-      auto put = [&](int e, int sl, int sg) {
-        rc[(size_t)erg[e] * 32 + sl % 32] += sg;
-        wc[(size_t)ewg[e] * 16 + sl % 16] += sg;
-      };
-      auto ins = [&](int e, int sl) {  // cost of inserting edge e at slot sl (counts without it)
-        return 4 * (2 * rc[(size_t)erg[e] * 32 + sl % 32] + 1) + (2 * wc[(size_t)ewg[e] * 16 + sl % 16] + 1);
-      };
       uint64_t rs = 0x2545F4914F6CDD1Dull;
       auto rnd = [&]() { rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17; return rs; };
+      auto cost2 = [&](int ea, int eb) {  // cost of the (deduplicated) groups of two edges
+        double c = 0;
+        int r0 = -1, w0 = -1;
+        for (int e : {ea, eb}) {
+          if (e < 0) continue;
+          if (erg[e] != r0) c += RG[erg[e]].cost();
+          if (ewg[e] != w0) c += ws * WG[ewg[e]].cost();
+          r0 = erg[e];
+          w0 = ewg[e];
+        }
+        return c;
+      };
       for (int it = 0; it < iters; ++it) {
         const int i = (int)(rnd() % (uint64_t)g->m);
         const int a = (int)(rnd() % (uint64_t)rwt), b = (int)(rnd() % (uint64_t)rwt);
@@ -497,29 +519,24 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
         const int ea = at[(size_t)i * rwt + a], eb = at[(size_t)i * rwt + b];
         if ((ea < 0 || erg[ea] < 0) && (eb < 0 || erg[eb] < 0)) continue;
         if ((ea >= 0 && erg[ea] < 0) || (eb >= 0 && erg[eb] < 0)) continue;
-        const int sa = vbase_u + phys(i, a), sb = vbase_u + phys(i, b);
-        // exact change of the objective: both edges out, then each configuration inserted one
-        // edge after the other
-        if (ea >= 0) put(ea, sa, -1);
-        if (eb >= 0) put(eb, sb, -1);
-        long long before = 0, after = 0;
-        if (ea >= 0) { before += ins(ea, sa); put(ea, sa, +1); }
-        if (eb >= 0) before += ins(eb, sb);
-        if (ea >= 0) put(ea, sa, -1);
-        if (ea >= 0) { after += ins(ea, sb); put(ea, sb, +1); }
-        if (eb >= 0) after += ins(eb, sa);
-        if (ea >= 0) put(ea, sb, -1);
-        const double T = 6.0 * (1.0 - (double)it / iters);
-        const long long dlt = after - before;
-        const bool take = dlt <= 0 || (T > 0 && (double)(rnd() % 1000000) / 1e6 < std::exp(-(double)dlt / T));
+        const double before = cost2(ea, eb);
+        auto swap_ab = [&]() {
+          if (ea >= 0) put(ea, i, -1);
+          if (eb >= 0) put(eb, i, -1);
+          if (ea >= 0) lslot[ea] = lslot[ea] == a ? b : a;
+          if (eb >= 0) lslot[eb] = lslot[eb] == a ? b : a;
+          if (ea >= 0) put(ea, i, +1);
+          if (eb >= 0) put(eb, i, +1);
+        };
+        swap_ab();
+        const double dlt = cost2(ea, eb) - before;
+        const double T = T0 * (1.0 - (double)it / iters);
+        const bool take = dlt <= 0 || (T > 0 && (double)(rnd() % 1000000) / 1e6 < std::exp(-dlt / T));
         if (take) {
-          if (ea >= 0) { put(ea, sb, +1); lslot[ea] = b; }
-          if (eb >= 0) { put(eb, sa, +1); lslot[eb] = a; }
           at[(size_t)i * rwt + a] = eb;
           at[(size_t)i * rwt + b] = ea;
         } else {
-          if (ea >= 0) put(ea, sa, +1);
-          if (eb >= 0) put(eb, sb, +1);
+          swap_ab();
         }
       }
     }
@@ -560,6 +577,19 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
         out[((size_t)k * DM + d) * TB + t] = (uint32_t)(L(i) + 1) | ((uint32_t)slot << 16);
       }
     }
+  // m2s rows of 8: the missing edges of real variables (slots k >= d3k hold DM edge slots, k < d3k
+  // three) get private V slots from dummy0 on, lane-consecutive per (k, d) (conflict-free reads and
+  // stores), and the dummy CS entry 0
+  int nd = 0;
+  if (dummy0 >= 0)
+    for (int k = 0; k < VPL; ++k)
+      for (int d = 0; d < DM; ++d)
+        for (int t = 0; t < TB; ++t) {
+          const int j = slot_var[(size_t)k * TB + t];
+          if (j >= 0 && d >= (int)g->col_rows[j].size() && d < (k < d3k ? 3 : DM))
+            out[((size_t)k * DM + d) * TB + t] = (uint32_t)(dummy0 + nd++) << 16;
+        }
+  if (ndummy) *ndummy = nd;
 }
 
 // Static LDS model of one engine-3 fp64 variable phase (per workgroup and iteration): LDS-array
@@ -1041,21 +1071,61 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         }
       }
     }
-    const int vslots_e3 = bp->vslots_m2v ? bp->vslots_m2v : (1 + g->m * bp->nch) * (16 / tsize);
+    // the same family for rows of 8 and column degree 5 (kern_r_f64_m2s8.hip, engine id 10103): the
+    // lifted-product codes (LP_Matg8_L30: 750 degree-3 and 270 degree-5 columns, rows of 8).  Rows of
+    // 4 chunks, no tail array.  Slots k >= D3K hold 5 edge slots; a real variable with fewer edges
+    // there (a degree-3 variable in the slot shared with the degree-5 class) gets a PRIVATE dummy V
+    // slot per missing edge, past the rows, and the dummy CS entry 0 (+0, parity 0): no other lane
+    // writes that slot, so the variable phase always reads its own previous v2c back and takes
+    // c2v = +-0, which leaves every sum bit-exact (w-domain sums are never -0).  The two-word family
+    // runs these graphs at 2 workgroups per CU (256 VGPRs); the one-word state fits 3.
+    if (bp->engine == 3 && precision == 64 && DM == 5 && !bp->tail && !bp->m2s && g->max_row >= 1 && g->max_row <= 8 &&
+        env_int("QLDPC_M2S", 1) != 0 && env_int("QLDPC_M2S8", 1) != 0 && env_int("QLDPC_DEGSORT", 1) != 0) {
+      int tb = 0, vpl = 0, n3 = 0;
+      for (int j = 0; j < g->n; ++j) n3 += g->col_rows[j].size() <= 3;
+      bool uni = true;
+      for (int j = 1; j < g->n && QLDPC_M2S_UNIL; ++j) uni = uni && channel_probs[j] == channel_probs[0];
+      if (uni && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl, pref, vmax) && tb == 256 && vpl >= 4 &&
+          vpl <= 6) {
+        // the slot map below: degree <= 3 first, so slots k < n3 / tb (whole) hold degree <= 3 only
+        const int d3 = n3 == g->n ? vpl : n3 / tb;
+        int nd = 0;
+        for (int p = 0, c = 0; c < 2; ++c)
+          for (int j = 0; j < g->n; ++j) {
+            const int d = (int)g->col_rows[j].size();
+            if ((d <= 3 ? 0 : 1) != c) continue;
+            nd += ((p / tb) < d3 ? 3 : DM) - d;
+            ++p;
+          }
+        const int vs = (1 + g->m * 4) * 2 + nd;
+        if (vs < 0xFFFF && r_fits(3, vs, g->m, 8, 0, 0, 1)) {
+          bp->m2s = 1;
+          bp->nch = 4;
+          bp->ea_shift = 0;
+          bp->vslots_dummy = nd;
+          // packed absolute addresses, 4 workgroups per CU (opt-in until measured)
+          bp->m2s_pk = env_int("QLDPC_M2S8_PK", 0) != 0 && vpl <= 5 &&
+                       4 * r_lds_bytes((int)r_layout(3, vs, g->m, 8, 0, 1).total, kChunkMax) <= (size_t)kLdsMax;
+        }
+      }
+    }
+    const int vslots_e3 = bp->vslots_m2v ? bp->vslots_m2v : (1 + g->m * bp->nch) * (16 / tsize) + bp->vslots_dummy;
     if (bp->engine >= 3 && ((DM != 4 && !(bp->engine == 3 && (DM == 5 || DM == 6))) ||
                             (!bp->fb && choose_rgeometry(g->n, g->m, vars_per_thread, bp->TB, bp->VPL, pref, vmax)) ||
                             !r_fits(bp->engine, vslots_e3, g->m, tsize, bp->ea_shift, bp->tail, bp->m2s, bp->fb) ||
-                            (precision == 64 && DM == 5 &&
+                            (precision == 64 && DM == 5 && !bp->m2s &&
                              !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch)))) {
       bp->ea_shift = 0;
       bp->tail = 0;
       bp->m2s = 0;
+      bp->vslots_dummy = 0;
+      bp->m2s_pk = 0;
       bp->fb = 0;
       bp->engine = 2;  // graph outside the register engines' envelope
       bp->nch = (std::max(1, g->max_row) * tsize + 15) / 16;
       if (DM == 5 || DM == 6) bp->DMAX = DM = 8;  // engine 2 kernels come in 4 and 8 slots
     }
-    const int vslots2 = bp->vslots_m2v ? bp->vslots_m2v : (1 + g->m * bp->nch) * (16 / tsize);
+    const int vslots2 = bp->vslots_m2v ? bp->vslots_m2v : (1 + g->m * bp->nch) * (16 / tsize) + bp->vslots_dummy;
     if (bp->engine >= 3) {
       bp->NS = 1;
       bp->lds_bytes =
@@ -1100,6 +1170,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         if (!sort3 || cls(j) == pass) order.push_back(j);
     bp->slot_var.assign((size_t)VPL * TB, -1);
     for (int j = 0; j < g->n; ++j) bp->slot_var[j] = order[j];
+    bp->npos = g->n;
     bp->d3k = 0;
     if (sort3)
       for (int k = 0; k < VPL; ++k) {
@@ -1127,7 +1198,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
                              : -1;
     // fp64 engine-3 kernels are built with D3K = 0 only, except the <= 256-thread family
     if (precision != 32 && !use_f64w(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift, bp->nch) &&
-        !use_f64x(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift) && !bp->tail)
+        !use_f64x(bp->engine, precision, DM, bp->TB, bp->VPL, bp->ea_shift) && !bp->tail && !bp->m2s)
       bp->d3k = 0;
     std::vector<int> lab;
     if (bp->m2s == 3 && env_int("QLDPC_M2V_PERM", 0) != 0) {  // (opt-in: measured 1.6 % slower)
@@ -1196,8 +1267,11 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       if (g->m && hipMemcpy(bp->rperm.p, inv.data(), (size_t)g->m * 4, hipMemcpyHostToDevice) != hipSuccess)
         return fail(set_err(QLDPC_EHIP, "upload check labels"));
     }
+    int ndummy = 0;
     build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab, bp->tail,
-                     bp->m2s == 1 && env_int("QLDPC_M2S_PLACE", 1) != 0);
+                     bp->m2s == 1 && env_int("QLDPC_M2S_PLACE", 1) != 0, bp->d3k,
+                     bp->vslots_dummy ? (1 + g->m * bp->nch) * (16 / tsize) : -1, &ndummy);
+    if (ndummy != bp->vslots_dummy) return fail(set_err(QLDPC_EINVAL, "m2s private dummy slot count mismatch"));
     if (bp->engine == 3 && precision == 64 && bp->m2s != 3 && bp->ea_shift == 0)
       lds_model_var_phase(vchk, bp->TB, bp->VPL, DM, bp->d3k,
                           (uint32_t)r_layout(3, vslots2, g->m, tsize, bp->tail, bp->m2s).v, bp->m2s == 1,
@@ -1285,7 +1359,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         return fail(set_err(QLDPC_EHIP, "upload m2v row table"));
     }
     kern = slot_variant(bp->engine, precision, DM, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch, bp->tail,
-                        bp->m2s, bp->fb, bp->d2k).dec_k;
+                        bp->m2s, bp->fb, bp->d2k, bp->m2s_pk).dec_k;
     if (bp->engine >= 3) {
       // row degrees by check label: engine 4 keeps them in F, engine 3 their parity (bp_reg.h, w domain)
       std::vector<uint8_t> deg(std::max(1, g->m));
@@ -1357,7 +1431,7 @@ int qldpc_bp_kernel_id(const qldpc_bp* bp, int32_t* kernel_id, int32_t* row_chun
   int id = bp->engine;
   if (bp->engine == 3) {
     if (bp->m2s)
-      id = bp->m2s == 2 ? 31103 : bp->m2s == 3 ? 40103 : 11103;
+      id = bp->m2s == 2 ? 31103 : bp->m2s == 3 ? 40103 : bp->tail ? 11103 : bp->m2s_pk ? 10203 : 10103;
     else if (bp->fb)
       id = 21013 + ((bp->d3k >= 8 && bp->d2k > 0) ? 100000 * std::min(bp->d2k, 4) : 0);  // + D2K digit
     else if (bp->tail)
@@ -1422,6 +1496,7 @@ static SSector ssector_of(const qldpc_bp* bp, const unsigned long long* lmask, i
   s.rows = static_cast<const uint32_t*>(bp->rowtab.p);
   s.vlast = bp->m2v_vlast;
   s.vnl = bp->m2v_nl;
+  s.npos = bp->npos > 0 ? bp->npos : bp->g->n;
   return s;
 }
 
@@ -1479,7 +1554,7 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     a.conv = d_conv;
     a.B = B;
     a.mmax = bp->g->m;
-    a.vslots = bp->vslots_m2v ? bp->vslots_m2v : (1 + bp->g->m * bp->nch) * (16 / tsize);
+    a.vslots = bp->vslots_m2v ? bp->vslots_m2v : (1 + bp->g->m * bp->nch) * (16 / tsize) + bp->vslots_dummy;
     a.img_bytes = (int)slot_img_bytes(a.vslots, a.mmax, tsize);
     a.chunk = chunk_for(B, cap, bp->NS);
     a.work = nullptr;
@@ -1492,7 +1567,7 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     const long long nchunks = (B + a.chunk - 1) / a.chunk;
     const int grid = (int)std::max<long long>(1, std::min<long long>(nchunks, cap));
     SVariant v = slot_variant(bp->engine, bp->precision, bp->DMAX, bp->NS, bp->VPL, bp->d3k, bp->ea_shift, bp->TB, bp->nch,
-                              bp->tail, bp->m2s, bp->fb, bp->d2k);
+                              bp->tail, bp->m2s, bp->fb, bp->d2k, bp->m2s_pk);
     QLDPC_HIP(v.dec(dim3(grid), dim3(bp->TB), bp->lds_bytes, (hipStream_t)stream, a));
   }
   return 0;
@@ -1525,7 +1600,8 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
                       (dec_x && dec_x->tail && !dec_x->m2s) || (dec_z && dec_z->tail && !dec_z->m2s) ||
                       // the fused kernel runs one layout family for both sectors
                       (dec_x && dec_z &&
-                       (dec_x->m2s != dec_z->m2s || dec_x->tail != dec_z->tail || dec_x->fb != dec_z->fb)) ||
+                       (dec_x->m2s != dec_z->m2s || dec_x->tail != dec_z->tail || dec_x->fb != dec_z->fb ||
+                        dec_x->m2s_pk != dec_z->m2s_pk)) ||
                       // one-slot families (m2s / c2s / m2v) keep no dummy edge on a real variable:
                       // the kernel's compile-time D3K must be each sector's own (a degree-3
                       // variable past it would run the 4-edge path and read the shared dummy slot)
@@ -1593,6 +1669,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   mc->mmax = std::max(dec_x ? dec_x->g->m : 0, dec_z ? dec_z->g->m : 0);
   mc->tail = d0->tail;
   mc->m2s = d0->m2s;
+  mc->m2s_pk = d0->m2s_pk;
   mc->fb = d0->fb;
   const void* kern;
   if (mc->engine == 1) {
@@ -1601,7 +1678,9 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   } else {
     const int tsize = mc->precision == 32 ? 4 : 8;
     for (qldpc_bp* d : {dec_x, dec_z})
-      if (d) mc->vslots = std::max(mc->vslots, d->vslots_m2v ? d->vslots_m2v : (1 + d->g->m * d->nch) * (16 / tsize));
+      if (d)
+        mc->vslots = std::max(mc->vslots,
+                              d->vslots_m2v ? d->vslots_m2v : (1 + d->g->m * d->nch) * (16 / tsize) + d->vslots_dummy);
     mc->img_bytes = (int)slot_img_bytes(mc->vslots, mc->mmax, tsize);
     if (mc->engine >= 3) {
       if (!r_fits(mc->engine, mc->vslots, mc->mmax, tsize, mc->ea_shift, mc->tail, mc->m2s, mc->fb))
@@ -1614,7 +1693,7 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
       mc->lds_bytes = (int)slot_lds_bytes(mc->NS, mc->img_bytes, kChunkMax);
     }
     kern = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch,
-                        mc->tail, mc->m2s, mc->fb).mc_k;
+                        mc->tail, mc->m2s, mc->fb, 0, mc->m2s_pk).mc_k;
   }
   if (mc->lds_bytes > kLdsMax) return fail(set_err(QLDPC_ENOTSUP, "per-shot LDS image exceeds 160 KiB"));
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
@@ -1803,7 +1882,7 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
       if (!a.fail) a.fail = static_cast<uint8_t*>(mc->c_fail.p);  // per-shot verdicts the OSD stage revises
     }
     SVariant v = slot_variant(mc->engine, mc->precision, mc->DMAX, mc->NS, mc->VPL, mc->d3k, mc->ea_shift, mc->TB, mc->nch,
-                              mc->tail, mc->m2s, mc->fb);
+                              mc->tail, mc->m2s, mc->fb, 0, mc->m2s_pk);
     QLDPC_HIP(v.mc(dim3((unsigned)grid), dim3(mc->TB), mc->lds_bytes, st, a));
     if (bposd) {
       unsigned int nc[4] = {0, 0, 0, 0};

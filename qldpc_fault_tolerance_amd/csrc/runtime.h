@@ -72,6 +72,9 @@ struct qldpc_bp {
   qldpc_rt::DevBuf rowtab;     // m2v: the check phase's row table [kM2vRows][TB] x 4 u32
   int vslots_m2v = 0;          // m2v: V slots of the variable-major layout (0 = row-major formula)
   int m2v_vlast = 0, m2v_nl = 0;  // m2v: first V slot of the last variable slot, its per-edge stride
+  int m2s_pk = 0;        // m2s rows of 8 with packed absolute edge addresses (engine id 10203)
+  int vslots_dummy = 0;  // m2s rows of 8 (engine id 10103): private V slots of real variables' missing edges
+  int npos = 0;       // 1 + the last slot position holding a variable (SSector::npos)
   qldpc_rt::DevBuf work;       // engine 3 decode_batch: chunk-queue head
   // engines 3/4: variable of each (k, t) slot (-1 = padding).  Engine 3 sorts
   // degree <= 3 variables first so that slots k < d3k skip the 4th edge slot.
@@ -108,7 +111,7 @@ struct qldpc_mc {
   int d3k = 0;  // engine 3: compile-time degree-3 slot count of the kernel (min over sectors)
   int nch = 0;  // 16-byte chunks per check row when both sectors agree (else 0)
   int ea_shift = 0;
-  int tail = 0, m2s = 0, fb = 0;  // engine 3 layout flags shared by both sectors
+  int tail = 0, m2s = 0, fb = 0, m2s_pk = 0;  // engine 3 layout flags shared by both sectors
   // staged pipeline (staged.hip): product-sum decoders, or QLDPC_MC_STAGED=1
   bool staged = false;
   long long sbatch = 0;

@@ -58,6 +58,8 @@ SVariant get_rvariant_f64_st(int vpl, int d3k, int d2k = 0);  // kern_r_f64_st*.
 SVariant get_rvariant_f64_st_hi(int vpl, int d3k);
 SVariant get_rvariant_f32_st(int vpl, int d3k);  // kern_r_f32_st.hip: tail layout in float (engine id 1013)
 SVariant get_rvariant_f64_m2s(int vpl, int d3k);  // kern_r_f64_m2s.hip: m2 in the argmin slot, rows of 3 chunks + tail (engine id 11103)
+SVariant get_rvariant_f64_m2s8(int vpl, int d3k);  // kern_r_f64_m2s8.hip: m2s, rows of 4 chunks (8 edges), column degree 5 (engine id 10103)
+SVariant get_rvariant_f64_m2s8pk(int vpl, int d3k);  // the same with packed absolute edge addresses, 4 per CU (engine id 10203)
 SVariant get_rvariant_f64_m2v(int vpl, int d3k);  // kern_r_f64_m2v.hip: m2s with variable-major V slots (engine id 40103)
 SVariant get_rvariant_f64_c2s(int vpl, int d3k);  // kern_r_f64_c2s.hip: c2v written by the check phase into the slots (engine id 31103)
 SVariant get_rvariant_f32_stfb(int vpl, int d3k, int d2k);  // kern_r_f32_stfb.hip: fp32 tail layout, byte F, 512 threads (engine id 21013 + 100000 * D2K)
