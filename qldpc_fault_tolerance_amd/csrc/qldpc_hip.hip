@@ -21,6 +21,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -429,7 +431,8 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
     // contiguous lanes, bank pair s mod 16).  Place per 32-lane group: distinct s mod 32 over the
     // group first, distinct s mod 16 within each 16-lane half second.
     std::vector<uint32_t> used(g->m, 0u);
-    for (int k = 0; k < VPL; ++k)
+    const bool greedy = env_int("QLDPC_M2S_GREEDY", 1) != 0;
+    for (int k = 0; k < VPL && greedy; ++k)
       for (int d = 0; d < DM; ++d)
         for (int h0 = 0; h0 < TB; h0 += 32) {
           int c32[32] = {0}, c16[2][16] = {{0}};
@@ -461,7 +464,30 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
     // bank pair (slot mod 32), per 16-lane store group the same over slot mod 16; objective = reads
     // + ws * stores, temperature T0 falling linearly to 0 (round 4; tools/dev/place_opt3.cpp is the
     // offline study: 20 M moves take the n1600 hz model from 362 / 715 to 327 / 442 cycles).
-    const int iters = env_int("QLDPC_M2S_ANNEAL", 0);  // (opt-in until measured)
+    // default 4000 moves per edge (n1600: 21.5 M moves, ~3 s on one host core; measured +3.1 %:
+    // 1.221 M vs 1.184 M shots/s, bank-conflict share 0.338 -> 0.276, profiles/r04/passd/); the
+    // result is memoised per process for the same graph, lane map and layout (decoders for other
+    // error rates of one code reuse it)
+    const int iters_env = env_int("QLDPC_M2S_ANNEAL", -1);
+    const int iters = iters_env >= 0 ? iters_env : (int)std::min<long long>(4000LL * g->nnz, 1LL << 30);
+    static std::mutex memo_mu;
+    static std::map<uint64_t, std::vector<int>> memo;
+    uint64_t key = 0xcbf29ce484222325ull;
+    auto mix = [&](uint64_t v) { key = (key ^ v) * 0x100000001b3ull; };
+    if (iters > 0) {
+      for (int v : {g->m, g->n, TB, VPL, DM, nch, tail, vbase_u, iters, env_int("QLDPC_M2S_ANNEAL_T", 50),
+                    env_int("QLDPC_M2S_ANNEAL_WS", 1000)})
+        mix((uint64_t)(uint32_t)v);
+      for (int32_t v : slot_var) mix((uint64_t)(uint32_t)v);
+      for (int32_t v : g->col_idx) mix((uint64_t)(uint32_t)v);
+      for (int v : lslot) mix((uint64_t)(uint32_t)v);  // the greedy start
+      std::lock_guard<std::mutex> lk(memo_mu);
+      auto it = memo.find(key);
+      if (it != memo.end() && it->second.size() == lslot.size()) {
+        lslot = it->second;
+        goto placed;
+      }
+    }
     if (iters > 0) {
       const double T0 = env_int("QLDPC_M2S_ANNEAL_T", 50) * 1e-3, ws = env_int("QLDPC_M2S_ANNEAL_WS", 1000) * 1e-3;
       const int nrg = VPL * DM * ((TB + 31) / 32), nwg = VPL * DM * ((TB + 15) / 16);
@@ -539,7 +565,10 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
           swap_ab();
         }
       }
+      std::lock_guard<std::mutex> lk(memo_mu);
+      memo[key] = lslot;
     }
+  placed:;
   } else if (vbase_dw >= 0 && rwt <= 32) {
     std::vector<uint32_t> used(g->m, 0u);
     for (int k = 0; k < VPL; ++k)
@@ -1103,8 +1132,9 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
           bp->nch = 4;
           bp->ea_shift = 0;
           bp->vslots_dummy = nd;
-          // packed absolute addresses, 4 workgroups per CU (opt-in until measured)
-          bp->m2s_pk = env_int("QLDPC_M2S8_PK", 0) != 0 && vpl <= 5 &&
+          // packed absolute addresses, 4 workgroups per CU: LP L30 fp64 4.08 M vs 3.67 M shots/s
+          // (0.622 vs 0.561 of the LDS roofline, profiles/r04/passd/); QLDPC_M2S8_PK=0 keeps 10103
+          bp->m2s_pk = env_int("QLDPC_M2S8_PK", 1) != 0 && vpl <= 5 &&
                        4 * r_lds_bytes((int)r_layout(3, vs, g->m, 8, 0, 1).total, kChunkMax) <= (size_t)kLdsMax;
         }
       }
