@@ -137,6 +137,8 @@ def kernel_name(dec):
         return f"(anonymous namespace)::hdec_kernel<{t}, {'true' if xl else 'false'}> (engine 6, staged shot loop)"
     if g.get("kernel_id") in (11103, 31103, 40103):  # fp64 one-slot families (256 threads, NCH 3)
         return f"qldpc::rmc_kernel<double, 4, {g['vars_per_thread']}, {g['kernel_id']}, {g['degree3_slots']}, 256, 3>"
+    if g.get("kernel_id") in (10103, 10203):  # fp64 one-word rows of 8, column degree 5 (kern_r_f64_m2s8.hip)
+        return f"qldpc::rmc_kernel<double, 5, {g['vars_per_thread']}, {g['kernel_id']}, {g['degree3_slots']}, 256, 4>"
     mc = dec.graph.info()["max_col_deg"]
     dmax = 4 if mc <= 4 else (mc if g["engine"] == 3 and (mc <= 6 if dec.precision == 32 else mc == 5) else 8)
     nch = (max(1, dec.graph.info()["max_row_deg"]) * (4 if dec.precision == 32 else 8) + 15) // 16

@@ -28,6 +28,8 @@
 #include <cstdlib>
 #include <numeric>
 #include <thread>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "runtime.h"
@@ -394,6 +396,7 @@ struct OsdGpuArgs {
   int bits_off;  // LDS byte offset of the used / syndrome bit-vectors
   int pbuf_off;  // register-row mode: LDS byte offset of the pivot-row broadcast buffer
   int pnl_off;   // panel mode: LDS byte offset of the panel area (words, masks, pivot rows, indices)
+  int syn_lds;   // two-syndrome register-row kernel: LDS bytes per syndrome area
   long long ws_words, iws_ints;
 };
 
@@ -1065,6 +1068,367 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
     for (int k2 = 0; k2 < 10; ++k2) atomicAdd(&g_osd_stamps[k2], st[k2]);
 }
 
+// calls f(integral_constant<int, Q>) for Q = 0, 1, ... while it returns true (compile-time word index)
+template <int... Q, class F>
+__device__ __attribute__((always_inline)) inline void osd_for_words(std::integer_sequence<int, Q...>, F&& f) {
+  (void)(f(std::integral_constant<int, Q>{}) && ...);
+}
+
+// Two syndromes per workgroup (register-row mode, 768 threads, m <= 768; round 4, VERDICT r03 item
+// 5).  The Gauss-Jordan of one syndrome is a chain of ~780 dependent steps (wave minimum, LDS
+// atomic, barrier, pivot-row publication, barrier, row update) that leaves the CU mostly idle, and
+// an OSD workgroup cannot share its CU with another (768 x 163 VGPRs).  Here every thread holds
+// row tid of BOTH syndromes' permuted H (2 x WR words) and each step searches, publishes and
+// updates both, so one chain of barriers serves two eliminations.  Per syndrome: its own LDS area
+// (sort tables, bit-vectors, pivot-row buffer, staged pivots) at s * A.syn_lds, its own HBM slice
+// (blockIdx.x * 2 + s), the same sort / swap trace / candidates / outputs as osd_gpu_kernel, one
+// syndrome after the other.  A syndrome that finishes its word (no pivot left, or rank reached)
+// idles through the other's remaining steps of that word.  Outputs identical to osd_gpu_kernel.
+template <int WR>
+__global__ void __launch_bounds__(768) osd_rr2_kernel(OsdGpuArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, TB = blockDim.x;
+  const int m = A.m, n = A.n, W = A.W, RW = A.RW, NP = A.NP, rank = A.rank;
+  const int k = n - rank;
+  const int w = A.order < k ? A.order : k;
+  const int nh = A.method == 2 ? k : w;
+  __shared__ int s_piv[2][3], s_npiv[2];
+  __shared__ u64 s_best[2];
+  constexpr int XB = kOsdXB;
+  for (long long b0 = (long long)blockIdx.x * 2; b0 < A.B; b0 += 2ll * gridDim.x) {
+    bool act[2];
+    u64 row[2][WR];
+    uint32_t sbit[2];
+    bool used_r[2];
+    // (per-syndrome phases as lambdas on a compile-time s: the row registers are never indexed by
+    // a runtime value, which would put them in scratch)
+    auto prologue = [&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      const long long b = b0 + s;
+      act[s] = false;
+#pragma unroll
+      for (int q = 0; q < WR; ++q) row[s][q] = 0;
+      sbit[s] = 0;
+      used_r[s] = true;
+      if (b >= A.B || (A.shot && A.shot[b] < 0)) return;
+      uint8_t* ow = A.outw + b * (long long)n;
+      uint8_t* o0 = A.out0 ? A.out0 + b * (long long)n : nullptr;
+      if (A.conv && A.conv[b]) {  // BP converged: bposd_decoder returns the BP decoding
+        for (int j = tid; j < n; j += TB) {
+          const uint8_t v = A.bp_corr[b * (long long)n + j];
+          ow[j] = v;
+          if (o0) o0[j] = v;
+        }
+        return;
+      }
+      act[s] = true;
+      unsigned char* L = smem + (size_t)s * A.syn_lds;
+      u64* skey = reinterpret_cast<u64*>(L);
+      int32_t* sidx = reinterpret_cast<int32_t*>(skey + NP);
+      int32_t* pos = sidx + NP;
+      uint32_t* used = reinterpret_cast<uint32_t*>(L + A.bits_off);
+      uint32_t* sb = used + (m + 31) / 32;
+      const double* post = A.post + b * (long long)n;
+      const uint8_t* synd = A.synd + b * (long long)m;
+      // 1. stable ascending sort of the columns by posterior (bitonic on (key, index))
+      for (int q = tid; q < NP; q += TB) {
+        skey[q] = q < n ? ord_key(post[q]) : ~0ull;
+        sidx[q] = q < n ? q : 0x7FFFFFFF;
+      }
+      __syncthreads();
+      for (int size = 2; size <= NP; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int q = tid; q < NP / 2; q += TB) {
+            const int lo = 2 * q - (q & (stride - 1));
+            const int hi = lo + stride;
+            const bool up = (lo & size) == 0;
+            const u64 ka = skey[lo], kb = skey[hi];
+            const int ia = sidx[lo], ib = sidx[hi];
+            const bool gt = ka > kb || (ka == kb && ia > ib);
+            if (gt == up) {
+              skey[lo] = kb; skey[hi] = ka;
+              sidx[lo] = ib; sidx[hi] = ia;
+            }
+          }
+          __syncthreads();
+        }
+      for (int q = tid; q < n; q += TB) pos[sidx[q]] = q;
+      for (int q = tid; q < (m + 31) / 32; q += TB) {
+        used[q] = 0;
+        uint32_t v = 0;
+        for (int t = 0; t < 32 && q * 32 + t < m; ++t) v |= (uint32_t)(synd[q * 32 + t] & 1u) << t;
+        sb[q] = v;
+      }
+      if (tid == 0) {
+        s_npiv[s] = 0;
+        s_piv[s][0] = s_piv[s][1] = s_piv[s][2] = 0x7FFFFFFF;
+      }
+      __syncthreads();
+      // 2. row tid of the permuted H
+      const int i = tid;
+      used_r[s] = i >= m;
+      if (i < m) {
+        for (int e = A.rp[i]; e < A.rp[i + 1]; ++e) {
+          const int p = pos[A.ci[e]];
+          const int pq = p >> 6;
+          const u64 bit = 1ull << (p & 63);
+#pragma unroll
+          for (int q = 0; q < WR; ++q) row[s][q] ^= (pq == q) ? bit : 0ull;
+        }
+        sbit[s] = synd[i] & 1u;
+      }
+    };
+    prologue(std::integral_constant<int, 0>{});
+    prologue(std::integral_constant<int, 1>{});
+    if (!act[0] && !act[1]) continue;  // uniform
+    __syncthreads();
+    // 3. joint Gauss-Jordan over positions in order (per syndrome as osd_gpu_kernel's search skip)
+    int npiv[2] = {0, 0};
+    int step3 = 0;
+    // one word q per call, q compile-time (the unroller gives up on this loop nest: the row
+    // registers would then be indexed at run time and live in scratch); false = stop
+    auto word = [&](auto qc) __attribute__((always_inline)) -> bool {
+      constexpr int q = decltype(qc)::value;
+      if (q * 64 >= n) return false;  // uniform
+      bool dn[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) dn[s] = !act[s] || npiv[s] >= rank;
+      if (dn[0] && dn[1]) return false;  // uniform
+      const int bend = n - q * 64 < 64 ? n - q * 64 : 64;
+      const u64 wmask = bend < 64 ? (1ull << bend) - 1ull : ~0ull;
+      int bs[2] = {0, 0};
+      while (true) {  // uniform
+        const int slot = step3;
+        step3 = step3 == 2 ? 0 : step3 + 1;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          if (dn[s]) continue;  // uniform
+          const u64 lowm = (~0ull << bs[s]) & wmask;
+          const u64 mm = used_r[s] ? 0ull : (row[s][q] & lowm);
+          uint32_t key = mm ? ((uint32_t)(__ffsll((long long)mm) - 1) << 11) | (uint32_t)tid : 0x7FFFFFFFu;
+          key = wave_min_u32(key);
+          if ((tid & 63) == 0 && key != 0x7FFFFFFFu) atomicMin(&s_piv[s][slot], (int)key);
+        }
+        __syncthreads();
+        int kk[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) kk[s] = s_piv[s][slot];
+        if (tid == 0) {
+          const int nx = step3 == 2 ? 0 : step3 + 1;  // re-arm the slot two steps ahead
+          s_piv[0][nx] = 0x7FFFFFFF;
+          s_piv[1][nx] = 0x7FFFFFFF;
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          if (kk[s] == 0x7FFFFFFF) dn[s] = true;  // no pivot left in this word (uniform)
+        if (dn[0] && dn[1]) break;
+        bool hb[2];
+        int rr[2], fbs[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          hb[s] = false;
+          rr[s] = -1;
+          fbs[s] = 0;
+          if (dn[s]) continue;
+          const int fb = kk[s] >> 11, r = kk[s] & 2047;
+          fbs[s] = fb;
+          rr[s] = r;
+          hb[s] = ((row[s][q] >> fb) & 1ull) != 0;
+          if (tid == r) {
+            used_r[s] = true;
+            u64* pbuf = reinterpret_cast<u64*>(smem + (size_t)s * A.syn_lds + A.pbuf_off);
+#pragma unroll
+            for (int q2 = q; q2 < WR; ++q2) pbuf[q2] = row[s][q2];
+            pbuf[WR] = sbit[s];
+            int32_t* pivrow = A.iws + ((size_t)blockIdx.x * 2 + s) * A.iws_ints;
+            pivrow[npiv[s]] = r;
+            pivrow[rank + npiv[s]] = q * 64 + fb;  // pivpos
+          }
+          ++npiv[s];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          if (dn[s]) continue;
+          if (hb[s] && tid != rr[s]) {  // the pivot row's words q.., read XB ahead of their xors
+            const u64* prow = reinterpret_cast<const u64*>(smem + (size_t)s * A.syn_lds + A.pbuf_off);
+            u64 buf[XB];
+#pragma unroll
+            for (int u = 0; u < XB; ++u)
+              if (q + u < WR) buf[u] = prow[q + u];
+            const uint32_t ps = (uint32_t)prow[WR];
+#pragma unroll
+            for (int q2 = q; q2 < WR; ++q2) {
+              const u64 pv = buf[(q2 - q) % XB];
+              if (q2 + XB < WR) buf[(q2 - q) % XB] = prow[q2 + XB];
+              row[s][q2] ^= pv;
+            }
+            sbit[s] ^= ps;
+          }
+          bs[s] = fbs[s] + 1;
+          if (bs[s] >= bend || npiv[s] >= rank) dn[s] = true;
+        }
+        if (dn[0] && dn[1]) break;
+      }
+      return true;
+    };
+    osd_for_words(std::make_integer_sequence<int, WR>{}, word);
+    // 4-7 per syndrome: reduced rows -> HBM slice, swaps, bit-vectors, candidates, outputs
+    auto finish = [&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      if (!act[s]) return;  // uniform
+      const long long b = b0 + s;
+      unsigned char* L = smem + (size_t)s * A.syn_lds;
+      const int32_t* sidx = reinterpret_cast<const int32_t*>(reinterpret_cast<u64*>(L) + NP);
+      uint32_t* used = reinterpret_cast<uint32_t*>(L + A.bits_off);
+      uint32_t* sb = used + (m + 31) / 32;
+      int32_t* lpp = reinterpret_cast<int32_t*>(L + A.pbuf_off + (WR + 1) * 8);
+      u64* Mg = A.ws + ((size_t)blockIdx.x * 2 + s) * A.ws_words;
+      u64* X = Mg + (size_t)W * m;
+      int32_t* pivrow = A.iws + ((size_t)blockIdx.x * 2 + s) * A.iws_ints;
+      int32_t* pivpos = pivrow + rank;
+      int32_t* swp = pivpos + rank;
+      uint8_t* ow = A.outw + b * (long long)n;
+      uint8_t* o0 = A.out0 ? A.out0 + b * (long long)n : nullptr;
+      {
+        const int i = tid;
+        if (i < m) {
+#pragma unroll
+          for (int q = 0; q < WR; ++q)
+            if (q < W) Mg[(size_t)q * m + i] = row[s][q];
+        }
+        const unsigned long long sbal = __ballot(i < m && sbit[s]);
+        if ((tid & 63) == 0) {
+          const int w0 = (tid & ~63) >> 5;
+          if (w0 < (m + 31) / 32) sb[w0] = (uint32_t)sbal;
+          if (w0 + 1 < (m + 31) / 32) sb[w0 + 1] = (uint32_t)(sbal >> 32);
+        }
+      }
+      __syncthreads();  // pivrow / pivpos (global, written by the pivot owners) and sb visible
+      const int r = npiv[s];
+      for (int i = tid; i < r; i += TB) lpp[i] = pivpos[i];
+      __syncthreads();
+      for (int x = r + tid; x < r + nh && x < n; x += TB) {
+        int cur = x;
+        for (int i = r - 1; i >= 0; --i) {
+          const int pi = lpp[i];
+          cur = cur == i ? pi : (cur == pi ? i : cur);
+        }
+        swp[x] = cur;
+      }
+      __syncthreads();
+      const int RWr = (r + 63) / 64;
+      for (int t = tid >> 6; t < (1 + nh) * RWr; t += TB >> 6) {  // uniform per wave
+        const int j = t / RWr, q = t % RWr;
+        const int c = tid & 63, i = q * 64 + c;
+        bool bitv = false;
+        if (i < r) {
+          const int rw = pivrow[i];
+          if (j == 0) {
+            bitv = ((sb[rw >> 5] >> (rw & 31)) & 1u) != 0;
+          } else {
+            const int hp = swp[r + j - 1];
+            bitv = ((Mg[(size_t)(hp >> 6) * m + rw] >> (hp & 63)) & 1ull) != 0;
+          }
+        }
+        const unsigned long long v = __ballot(bitv);
+        if (c == 0) X[(size_t)j * RW + q] = v;
+      }
+      if (tid == 0) s_best[s] = ~0ull;
+      __syncthreads();
+      long long Lc = 1;
+      if (A.method == 1 && w > 0) Lc = 1ll << w;
+      if (A.method == 2 && w >= 0) Lc = 1 + (long long)k + (long long)w * (w - 1) / 2;
+      if (A.method == 0 || A.order == 0 || k == 0) Lc = 1;
+      u64 best = ~0ull;
+      for (long long c = tid; c < Lc; c += TB) {
+        int tj[2];
+        int nt = 0;
+        unsigned long long ebits = 0;
+        if (A.method == 1) {
+          ebits = (unsigned long long)c;
+          nt = __popcll(ebits);
+        } else if (c >= 1 && c <= k) {
+          tj[0] = (int)(c - 1);
+          nt = 1;
+        } else if (c > k) {
+          long long rem = c - 1 - k;
+          int i = 0;
+          while (rem >= w - 1 - i) {
+            rem -= w - 1 - i;
+            ++i;
+          }
+          tj[0] = i;
+          tj[1] = i + 1 + (int)rem;
+          nt = 2;
+        }
+        long long cnt = nt;
+        for (int q = 0; q < RWr; ++q) {
+          u64 v = X[q];
+          if (A.method == 1) {
+            for (unsigned long long e = ebits; e; e &= e - 1) v ^= X[(size_t)(1 + __ffsll((long long)e) - 1) * RW + q];
+          } else {
+            for (int a = 0; a < nt; ++a) v ^= X[(size_t)(1 + tj[a]) * RW + q];
+          }
+          cnt += __popcll(v);
+        }
+        const u64 key = ((u64)cnt << 40) | (u64)c;
+        if (key < best) best = key;
+      }
+      if (best != ~0ull) atomicMin(&s_best[s], best);
+      __syncthreads();
+      const long long cw = (long long)(s_best[s] & ((1ull << 40) - 1));
+      int tw[2];
+      int ntw = 0;
+      unsigned long long ewb = 0;
+      if (A.method == 1) {
+        ewb = (unsigned long long)cw;
+      } else if (cw >= 1 && cw <= k) {
+        tw[0] = (int)(cw - 1);
+        ntw = 1;
+      } else if (cw > k) {
+        long long rem = cw - 1 - k;
+        int i = 0;
+        while (rem >= w - 1 - i) {
+          rem -= w - 1 - i;
+          ++i;
+        }
+        tw[0] = i;
+        tw[1] = i + 1 + (int)rem;
+        ntw = 2;
+      }
+      for (int j = tid; j < n; j += TB) {
+        ow[j] = 0;
+        if (o0) o0[j] = 0;
+      }
+      __syncthreads();
+      for (int i = tid; i < r; i += TB) {
+        const int q = i >> 6, c = i & 63;
+        const u64 s0 = (X[q] >> c) & 1ull;
+        u64 v = X[q];
+        if (A.method == 1) {
+          for (unsigned long long e = ewb; e; e &= e - 1) v ^= X[(size_t)(1 + __ffsll((long long)e) - 1) * RW + q];
+        } else {
+          for (int a = 0; a < ntw; ++a) v ^= X[(size_t)(1 + tw[a]) * RW + q];
+        }
+        const int col = sidx[pivpos[i]];
+        ow[col] = (uint8_t)((v >> c) & 1ull);
+        if (o0) o0[col] = (uint8_t)s0;
+      }
+      if (tid == 0) {
+        if (A.method == 1) {
+          for (unsigned long long e = ewb; e; e &= e - 1) ow[sidx[swp[r + __ffsll((long long)e) - 1]]] = 1;
+        } else {
+          for (int a = 0; a < ntw; ++a) ow[sidx[swp[r + tw[a]]]] = 1;
+        }
+      }
+      __syncthreads();
+    };
+    finish(std::integral_constant<int, 0>{});
+    finish(std::integral_constant<int, 1>{});
+  }
+}
+
 }  // namespace
 
 struct qldpc_osd_gpu {
@@ -1073,6 +1437,7 @@ struct qldpc_osd_gpu {
   int wr = 0, pbuf_off = 0;  // register-row mode: compile-time words per row (0 = off), LDS pivot buffer
   int rr_tb = 0;             // register-row mode: threads per workgroup = m rounded up to waves
   int pnl = 0, pnl_off = 0;  // register-row mode: panel elimination (QLDPC_OSD_PNL), its LDS area
+  int nsy = 1, syn_lds = 0;  // register-row mode: syndromes per workgroup (osd_rr2_kernel), LDS per syndrome
   size_t lds = 0;
   long long ws_words = 0, iws_ints = 0;
   qldpc_rt::DevBuf rp, ci, ws, iws;
@@ -1159,6 +1524,13 @@ OsdKern osd_rr_kernel_t(int wr) {
   }
 }
 OsdKern osd_rr_kernel(int wr, int pnl) { return pnl ? osd_rr_kernel_t<1>(wr) : osd_rr_kernel_t<0>(wr); }
+OsdKern osd_rr2_kernel_of(int wr) {
+  switch (wr) {
+    case 20: return &osd_rr2_kernel<20>;
+    case 25: return &osd_rr2_kernel<25>;
+    default: return nullptr;
+  }
+}
 // LDS bytes of the panel area (osd_gpu_kernel PNL): half-words + masks [m] (u32), pivot rows [32][WR+1],
 // pk [32], pidx [m]
 inline size_t osd_pnl_bytes(int m, int wr) {
@@ -1262,6 +1634,14 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
     G->pnl_off = (int)((G->lds + 15) & ~(size_t)15);
     G->lds = (size_t)G->pnl_off + osd_pnl_bytes(m, G->wr);
   }
+  // two syndromes per workgroup (osd_rr2_kernel, the 768-thread register-row kernels): a second LDS
+  // area and HBM slice per workgroup; QLDPC_OSD_NSY=1 keeps one
+  const char* nsy_env = std::getenv("QLDPC_OSD_NSY");
+  if (G->wr >= 20 && !G->pnl && !QLDPC_OSD_1B && (nsy_env ? std::atoi(nsy_env) : 1) == 2 && osd_rr2_kernel_of(G->wr)) {
+    G->nsy = 2;
+    G->syn_lds = (int)((G->lds + 15) & ~(size_t)15);
+    G->lds = 2 * (size_t)G->syn_lds;
+  }
   G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW;
   G->iws_ints = 2ll * rank + 3ll * n;
   auto fail = [&](int code) {
@@ -1274,7 +1654,8 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || cus <= 0)
     return fail(set_err(QLDPC_EHIP, "device CU count"));
   int nb = 0;
-  const void* kf = G->wr ? reinterpret_cast<const void*>(osd_rr_kernel(G->wr, G->pnl))
+  const void* kf = G->nsy == 2 ? reinterpret_cast<const void*>(osd_rr2_kernel_of(G->wr))
+                  : G->wr ? reinterpret_cast<const void*>(osd_rr_kernel(G->wr, G->pnl))
                   : G->m_lds ? reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreadsLds>)
                              : reinterpret_cast<const void*>(&osd_gpu_kernel<kOsdThreads>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf,
@@ -1284,7 +1665,8 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   G->grid = cus * nb;
   const size_t E = g->col_idx.size();
   if ((rc = G->rp.alloc((size_t)(m + 1) * 4)) || (rc = G->ci.alloc(std::max<size_t>(E, 1) * 4)) ||
-      (rc = G->ws.alloc((size_t)G->grid * G->ws_words * 8)) || (rc = G->iws.alloc((size_t)G->grid * G->iws_ints * 4)))
+      (rc = G->ws.alloc((size_t)G->grid * G->nsy * G->ws_words * 8)) ||
+      (rc = G->iws.alloc((size_t)G->grid * G->nsy * G->iws_ints * 4)))
     return fail(rc);
   if (hipMemcpy(G->rp.p, g->row_ptr.data(), (size_t)(m + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
       (E && hipMemcpy(G->ci.p, g->col_idx.data(), E * 4, hipMemcpyHostToDevice) != hipSuccess))
@@ -1333,9 +1715,12 @@ int osd_gpu_decode_slots(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double
   a.method = osd->host.method; a.order = osd->host.order; a.NP = osd->NP; a.m_lds = osd->m_lds; a.bits_off = osd->bits_off;
   a.pbuf_off = osd->pbuf_off;
   a.pnl_off = osd->pnl_off;
+  a.syn_lds = osd->syn_lds;
   a.ws_words = osd->ws_words; a.iws_ints = osd->iws_ints;
-  const int grid = (int)std::min<long long>(B, osd->grid);
-  if (osd->wr)
+  const int grid = (int)std::min<long long>((B + osd->nsy - 1) / osd->nsy, osd->grid);
+  if (osd->nsy == 2)
+    hipLaunchKernelGGL(osd_rr2_kernel_of(osd->wr), dim3(grid), dim3(osd->rr_tb), osd->lds, (hipStream_t)stream, a);
+  else if (osd->wr)
     hipLaunchKernelGGL(osd_rr_kernel(osd->wr, osd->pnl), dim3(grid), dim3(osd->rr_tb), osd->lds, (hipStream_t)stream, a);
   else if (osd->m_lds)
     hipLaunchKernelGGL(osd_gpu_kernel<kOsdThreadsLds>, dim3(grid), dim3(kOsdThreadsLds), osd->lds, (hipStream_t)stream, a);
