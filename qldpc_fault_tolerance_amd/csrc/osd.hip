@@ -34,6 +34,7 @@
 
 #include "runtime.h"
 
+
 using qldpc_rt::set_err;
 
 struct qldpc_osd {
@@ -1068,6 +1069,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
     for (int k2 = 0; k2 < 10; ++k2) atomicAdd(&g_osd_stamps[k2], st[k2]);
 }
 
+#if QLDPC_EXPERIMENTAL
 // calls f(integral_constant<int, Q>) for Q = 0, 1, ... while it returns true (compile-time word index)
 template <int... Q, class F>
 __device__ __attribute__((always_inline)) inline void osd_for_words(std::integer_sequence<int, Q...>, F&& f) {
@@ -1084,6 +1086,9 @@ __device__ __attribute__((always_inline)) inline void osd_for_words(std::integer
 // (blockIdx.x * 2 + s), the same sort / swap trace / candidates / outputs as osd_gpu_kernel, one
 // syndrome after the other.  A syndrome that finishes its word (no pivot left, or rank reached)
 // idles through the other's remaining steps of that word.  Outputs identical to osd_gpu_kernel.
+// MEASURED AND NOT KEPT (experimental builds only): bit-exact (52 BP+OSD / phenl / circuit GPU
+// tests), but 2 x 25 row words leave too few of the 168 VGPRs (105 spilled): n1600 BP+OSD 539 k
+// vs 548 k shots/s with one syndrome per workgroup (profiles/r04/passf/).
 template <int WR>
 __global__ void __launch_bounds__(768) osd_rr2_kernel(OsdGpuArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1429,6 +1434,7 @@ __global__ void __launch_bounds__(768) osd_rr2_kernel(OsdGpuArgs A) {
   }
 }
 
+#endif  // QLDPC_EXPERIMENTAL
 }  // namespace
 
 struct qldpc_osd_gpu {
@@ -1525,11 +1531,16 @@ OsdKern osd_rr_kernel_t(int wr) {
 }
 OsdKern osd_rr_kernel(int wr, int pnl) { return pnl ? osd_rr_kernel_t<1>(wr) : osd_rr_kernel_t<0>(wr); }
 OsdKern osd_rr2_kernel_of(int wr) {
+#if QLDPC_EXPERIMENTAL
   switch (wr) {
     case 20: return &osd_rr2_kernel<20>;
     case 25: return &osd_rr2_kernel<25>;
     default: return nullptr;
   }
+#else
+  (void)wr;
+  return nullptr;
+#endif
 }
 // LDS bytes of the panel area (osd_gpu_kernel PNL): half-words + masks [m] (u32), pivot rows [32][WR+1],
 // pk [32], pidx [m]
