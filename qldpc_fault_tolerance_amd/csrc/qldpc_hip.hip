@@ -398,7 +398,7 @@ static int upload_llr(qldpc_bp* bp) {
 static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
                              const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1,
                              const std::vector<int>& lab = {}, int tail = 0, int m2s = 0, int d3k = 0,
-                             int dummy0 = -1, int* ndummy = nullptr) {
+                             int dummy0 = -1, int* ndummy = nullptr, int anneal = 0) {
   const int nv = 16 / tsize;  // messages per 16-byte chunk
   const int rw = nch * nv;
   const int rwt = rw + (tail ? 1 : 0);  // tail layouts: logical slot rw = the row's tail slot
@@ -458,6 +458,34 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
             lslot[edge_of(i, j)] = best;
           }
         }
+  } else if (vbase_dw >= 0 && rwt <= 32) {
+    std::vector<uint32_t> used(g->m, 0u);
+    for (int k = 0; k < VPL; ++k)
+      for (int d = 0; d < DM; ++d)
+        for (int h0 = 0; h0 < TB; h0 += sg) {
+          int cnt[32] = {0};
+          for (int t = h0; t < h0 + sg && t < TB; ++t) {
+            const int j = slot_var[(size_t)k * TB + t];
+            if (j < 0 || d >= (int)g->col_rows[j].size()) continue;
+            const int i = g->col_rows[j][d];
+            int best = -1, bc = 1 << 30;
+            for (int ls = 0; ls < rwt; ++ls) {
+              if ((used[i] >> ls) & 1u) continue;
+              const int c = cnt[(vbase_u + phys(i, ls)) % nb];
+              if (c < bc) {
+                bc = c;
+                best = ls;
+              }
+            }
+            used[i] |= 1u << best;
+            cnt[(vbase_u + phys(i, best)) % nb]++;
+            lslot[edge_of(i, j)] = best;
+          }
+        }
+  }
+  // Annealed placement (round 4, fp64 engine-3 families; `anneal` 1: the variable phase reads and
+  // stores each edge's V slot (m2s, the 1024-thread tail family), 2: stores only (own v2c in VGPRs)).
+  if (anneal && vbase_dw >= 0 && rwt <= 32) {
     // Then a seeded annealed local search over the rows' slot permutations (swap the positions of
     // two edges of one row, or move one into a free position) on the EXACT cost of the lane-group
     // bank model (qldpc_bp_lds_model): per 32-lane read group the maximum number of addresses on one
@@ -474,8 +502,9 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
     static std::map<uint64_t, std::vector<int>> memo;
     uint64_t key = 0xcbf29ce484222325ull;
     auto mix = [&](uint64_t v) { key = (key ^ v) * 0x100000001b3ull; };
+    bool hit = false;
     if (iters > 0) {
-      for (int v : {g->m, g->n, TB, VPL, DM, nch, tail, vbase_u, iters, env_int("QLDPC_M2S_ANNEAL_T", 50),
+      for (int v : {g->m, g->n, TB, VPL, DM, nch, tail, vbase_u, iters, anneal, env_int("QLDPC_M2S_ANNEAL_T", 50),
                     env_int("QLDPC_M2S_ANNEAL_WS", 1000)})
         mix((uint64_t)(uint32_t)v);
       for (int32_t v : slot_var) mix((uint64_t)(uint32_t)v);
@@ -485,11 +514,12 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
       auto it = memo.find(key);
       if (it != memo.end() && it->second.size() == lslot.size()) {
         lslot = it->second;
-        goto placed;
+        hit = true;
       }
     }
-    if (iters > 0) {
+    if (iters > 0 && !hit) {
       const double T0 = env_int("QLDPC_M2S_ANNEAL_T", 50) * 1e-3, ws = env_int("QLDPC_M2S_ANNEAL_WS", 1000) * 1e-3;
+      const double wr = anneal == 1 ? 1.0 : 0.0;  // 2: the family keeps its own v2c in VGPRs (no V reads)
       const int nrg = VPL * DM * ((TB + 31) / 32), nwg = VPL * DM * ((TB + 15) / 16);
       std::vector<int> erg(g->nnz, -1), ewg(g->nnz, -1);
       for (int k = 0; k < VPL; ++k)
@@ -531,7 +561,7 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
         int r0 = -1, w0 = -1;
         for (int e : {ea, eb}) {
           if (e < 0) continue;
-          if (erg[e] != r0) c += RG[erg[e]].cost();
+          if (erg[e] != r0) c += wr * RG[erg[e]].cost();
           if (ewg[e] != w0) c += ws * WG[ewg[e]].cost();
           r0 = erg[e];
           w0 = ewg[e];
@@ -568,31 +598,6 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
       std::lock_guard<std::mutex> lk(memo_mu);
       memo[key] = lslot;
     }
-  placed:;
-  } else if (vbase_dw >= 0 && rwt <= 32) {
-    std::vector<uint32_t> used(g->m, 0u);
-    for (int k = 0; k < VPL; ++k)
-      for (int d = 0; d < DM; ++d)
-        for (int h0 = 0; h0 < TB; h0 += sg) {
-          int cnt[32] = {0};
-          for (int t = h0; t < h0 + sg && t < TB; ++t) {
-            const int j = slot_var[(size_t)k * TB + t];
-            if (j < 0 || d >= (int)g->col_rows[j].size()) continue;
-            const int i = g->col_rows[j][d];
-            int best = -1, bc = 1 << 30;
-            for (int ls = 0; ls < rwt; ++ls) {
-              if ((used[i] >> ls) & 1u) continue;
-              const int c = cnt[(vbase_u + phys(i, ls)) % nb];
-              if (c < bc) {
-                bc = c;
-                best = ls;
-              }
-            }
-            used[i] |= 1u << best;
-            cnt[(vbase_u + phys(i, best)) % nb]++;
-            lslot[edge_of(i, j)] = best;
-          }
-        }
   }
   out.assign((size_t)VPL * DM * TB, kNoEdgeS);
   for (int k = 0; k < VPL; ++k)
@@ -1300,7 +1305,10 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     int ndummy = 0;
     build_slot_edges(g, bp->TB, bp->VPL, DM, tsize, bp->nch, bp->slot_var, vchk, vbase_dw, lab, bp->tail,
                      bp->m2s == 1 && env_int("QLDPC_M2S_PLACE", 1) != 0, bp->d3k,
-                     bp->vslots_dummy ? (1 + g->m * bp->nch) * (16 / tsize) : -1, &ndummy);
+                     bp->vslots_dummy ? (1 + g->m * bp->nch) * (16 / tsize) : -1, &ndummy,
+                     (bp->engine == 3 && precision == 64 && bp->m2s != 3)
+                         ? ((bp->m2s || bp->tail) ? 1 : env_int("QLDPC_ANNEAL_2W", 1) != 0 ? 2 : 0)
+                         : 0);
     if (ndummy != bp->vslots_dummy) return fail(set_err(QLDPC_EINVAL, "m2s private dummy slot count mismatch"));
     if (bp->engine == 3 && precision == 64 && bp->m2s != 3 && bp->ea_shift == 0)
       lds_model_var_phase(vchk, bp->TB, bp->VPL, DM, bp->d3k,
