@@ -291,6 +291,10 @@ int qldpc_mc_set_osd(qldpc_mc *mc, qldpc_osd_gpu *osd_x, qldpc_osd_gpu *osd_z);
  * families): out6 = {CS-gather LDS cycles, of which bank-conflict extra; V-slot read cycles, extra;
  * v2c store group-cycles, extra} under the lane-group rules of MI355X_MICROARCH.md §LDS. */
 int qldpc_bp_lds_model(const qldpc_bp *bp, int64_t *out6);
+/* The same model for the fp64 m2s family's V-slot placement of graph g, host only (no device, no
+ * decoder): the engine's geometry, degree sort, greedy placement and `anneal_iters` annealing moves
+ * (< 0 = the default, 4000 per edge; 0 = greedy only).  ENOTSUP outside the m2s envelope. */
+int qldpc_m2s_place_model(const qldpc_graph *g, int32_t anneal_iters, int64_t *out6);
 int qldpc_bp_bank_stats(const qldpc_bp *bp, int32_t *before, int32_t *after);
 
 /*

@@ -28,7 +28,7 @@ EXPORTED = [
     "qldpc_comm_allreduce_counters_group", "qldpc_comm_destroy", "qldpc_mc_run_sharded", "qldpc_sample_errors",
     "qldpc_stream_sync", "qldpc_bp_kernel_id", "qldpc_build_flags", "qldpc_circ_create", "qldpc_circ_set_final_osd",
     "qldpc_circ_info", "qldpc_circ_launch", "qldpc_circ_sample", "qldpc_circ_destroy",
-    "qldpc_shard_range", "qldpc_bp_lds_model",
+    "qldpc_shard_range", "qldpc_bp_lds_model", "qldpc_m2s_place_model",
 ]
 BUILD_EXPERIMENTAL = 1  # qldpc_build_flags(): the measured-and-not-kept kernel families are compiled in
 COMM_ID_BYTES = 128
@@ -176,6 +176,8 @@ def _declare(L):
     L.qldpc_circ_sample.argtypes = [_vp, _u64, _u64, _i64, _vp, _vp]
     L.qldpc_bp_lds_model.restype = ctypes.c_int
     L.qldpc_bp_lds_model.argtypes = [_vp, ctypes.POINTER(_i64)]
+    L.qldpc_m2s_place_model.restype = ctypes.c_int
+    L.qldpc_m2s_place_model.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(_i64)]
     L.qldpc_shard_range.restype = ctypes.c_int
     L.qldpc_shard_range.argtypes = [_i64, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]
     L.qldpc_circ_destroy.restype = ctypes.c_int

@@ -398,7 +398,7 @@ static int upload_llr(qldpc_bp* bp) {
 static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
                              const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1,
                              const std::vector<int>& lab = {}, int tail = 0, int m2s = 0, int d3k = 0,
-                             int dummy0 = -1, int* ndummy = nullptr, int anneal = 0) {
+                             int dummy0 = -1, int* ndummy = nullptr, int anneal = 0, int anneal_iters = -1) {
   const int nv = 16 / tsize;  // messages per 16-byte chunk
   const int rw = nch * nv;
   const int rwt = rw + (tail ? 1 : 0);  // tail layouts: logical slot rw = the row's tail slot
@@ -496,7 +496,7 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
     // 1.221 M vs 1.184 M shots/s, bank-conflict share 0.338 -> 0.276, profiles/r04/passd/); the
     // result is memoised per process for the same graph, lane map and layout (decoders for other
     // error rates of one code reuse it)
-    const int iters_env = env_int("QLDPC_M2S_ANNEAL", -1);
+    const int iters_env = anneal_iters >= 0 ? anneal_iters : env_int("QLDPC_M2S_ANNEAL", -1);
     const int iters = iters_env >= 0 ? iters_env : (int)std::min<long long>(4000LL * g->nnz, 1LL << 30);
     static std::mutex memo_mu;
     static std::map<uint64_t, std::vector<int>> memo;
@@ -1454,6 +1454,44 @@ int qldpc_bp_degree3_slots(const qldpc_bp* bp, int32_t* d3k) {
 int qldpc_bp_lds_model(const qldpc_bp* bp, int64_t* out6) {
   if (!bp || !out6) return set_err(QLDPC_EINVAL, "NULL argument");
   for (int q = 0; q < 6; ++q) out6[q] = bp->lds_model[q];
+  return 0;
+}
+
+int qldpc_m2s_place_model(const qldpc_graph* g, int32_t anneal_iters, int64_t* out6) {
+  if (!g || !out6) return set_err(QLDPC_EINVAL, "NULL argument");
+  // the decoder build of the fp64 m2s family (qldpc_bp_create), host side only: geometry, degree
+  // sort, greedy + annealed V-slot placement, then the static LDS model of its variable phase
+  int n3 = 0;
+  for (int j = 0; j < g->n; ++j) {
+    const int d = (int)g->col_rows[j].size();
+    if (d != 3 && d != 4) return set_err(QLDPC_ENOTSUP, "m2s placement model: column degrees 3 / 4 only");
+    n3 += d == 3;
+  }
+  int TB = 0, VPL = 0;
+  if (g->max_row < 1 || g->max_row > 7 || choose_rgeometry(g->n, g->m, 0, TB, VPL) || TB > 256 || VPL < 4 || VPL > 8 ||
+      !(n3 % TB == 0 || n3 == g->n))
+    return set_err(QLDPC_ENOTSUP, "graph outside the m2s envelope (rows <= 7, <= 256 threads x 4-8 slots)");
+  std::vector<int32_t> slot_var((size_t)VPL * TB, -1);
+  int p = 0;
+  for (int c = 0; c < 2; ++c)
+    for (int j = 0; j < g->n; ++j)
+      if (((int)g->col_rows[j].size() <= 3 ? 0 : 1) == c) slot_var[p++] = j;
+  int d3k = 0;
+  for (int k = 0; k < VPL; ++k) {
+    bool ok = true;
+    for (int t = 0; t < TB && ok; ++t) {
+      const int j = slot_var[(size_t)k * TB + t];
+      ok = j < 0 || (int)g->col_rows[j].size() <= 3;
+    }
+    if (!ok) break;
+    d3k = k + 1;
+  }
+  const int vslots = (1 + g->m * 3) * 2;
+  const uint32_t vbase = (uint32_t)r_layout(3, vslots, g->m, 8, 1, 1).v;
+  std::vector<uint32_t> edges;
+  build_slot_edges(g, TB, VPL, 4, 8, 3, slot_var, edges, (int)(vbase / 4), {}, 1, 1, d3k, -1, nullptr, 1,
+                   anneal_iters);
+  lds_model_var_phase(edges, TB, VPL, 4, d3k, vbase, true, out6);
   return 0;
 }
 

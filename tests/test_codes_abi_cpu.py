@@ -121,3 +121,50 @@ def test_shard_range_partitions_exactly():
             for b, c in spans:
                 assert b == pos
                 pos += c
+
+
+def _host_graph(L, H):
+    csr = codes.CSR.from_dense(np.asarray(H, np.uint8))
+    rp = np.ascontiguousarray(csr.row_ptr, np.int32)
+    ci = np.ascontiguousarray(csr.col_idx, np.int32)
+    h = ctypes.c_void_p()
+    assert L.qldpc_graph_create(0, H.shape[0], H.shape[1], rp.ctypes.data_as(ctypes.c_void_p),
+                                ci.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)) == 0
+    return h
+
+
+def test_m2s_annealed_placement_lowers_the_bank_model():
+    """qldpc_m2s_place_model runs the decoder build's host half (geometry, degree sort, greedy and
+    annealed V-slot placement) and the static LDS model of the m2s variable phase, no device needed.
+    On the headline hz graph the default anneal must cut the V-slot read and store conflicts the
+    GPU run measured (profiles/r04/passd/model0/1.txt: reads 382 -> 360, stores 676 -> 500), leave
+    the CS gathers alone (placement inside rows does not move a check's CS entry), and be
+    deterministic (seeded, and memoised per process)."""
+    L = _native.lib()
+    h = _host_graph(L, codes.get_code("hgp_34_n1600").hz)
+    out = (ctypes.c_int64 * 6)()
+    try:
+        assert L.qldpc_m2s_place_model(h, 0, out) == 0
+        greedy = list(out)
+        assert L.qldpc_m2s_place_model(h, 2_000_000, out) == 0
+        short = list(out)
+        assert L.qldpc_m2s_place_model(h, 2_000_000, out) == 0
+        assert list(out) == short  # deterministic
+    finally:
+        L.qldpc_graph_destroy(h)
+    assert greedy == [244, 52, 382, 190, 676, 292]  # == the decoder's own model on the GPU box
+    assert short[:2] == greedy[:2]
+    assert short[3] < greedy[3] and short[5] < greedy[5] - 40
+    # every group at least 1 cycle: cost = groups + extra
+    assert short[2] - short[3] == greedy[2] - greedy[3] and short[4] - short[5] == greedy[4] - greedy[5]
+
+
+def test_m2s_place_model_rejects_graphs_outside_the_family():
+    L = _native.lib()
+    h = _host_graph(L, codes.get_code("LP_Matg8_L30_Dmin20").hz)  # rows of 8, column degree 5
+    out = (ctypes.c_int64 * 6)()
+    try:
+        assert L.qldpc_m2s_place_model(h, 0, out) != 0
+        assert b"m2s" in L.qldpc_last_error()
+    finally:
+        L.qldpc_graph_destroy(h)
