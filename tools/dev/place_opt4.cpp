@@ -6,7 +6,7 @@
 // lane group, conflict-free reads / stores / CS gathers are an edge colouring.  Annealing over
 // label swaps (L), in-row position swaps including the CS position (P) on the exact lane-group
 // model of qldpc_bp_lds_model.
-//   g++ -O2 -o /tmp/place_opt4 tools/dev/place_opt4.cpp && /tmp/place_opt4 /tmp/hz.txt 20000000 PL [T0]
+//   g++ -O2 -o /tmp/place_opt4 tools/dev/place_opt4.cpp && /tmp/place_opt4 /tmp/hz.txt 20000000 PL [T0] [balance]
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -126,6 +126,122 @@ int main(int argc, char** argv) {
     for (int g = 0; g < NW; ++g)
       if (usedW[g]) w += W[g].cost();
   };
+  // optional phase 0 (argv[5] = balance moves): label swaps minimising, per read group, the spread of
+  // its rows' classes (lab mod 4) and, per store group, of (lab mod 2): sum of squared counts
+  const long long bal_iters = argc > 5 ? atoll(argv[5]) : 0;
+  if (bal_iters > 0) {
+    std::vector<std::vector<int>> rc4(NR, std::vector<int>(4, 0)), wc2(NW, std::vector<int>(2, 0));
+    auto bal_put = [&](int e, int sg) {
+      const int l = lab[ed[e].row];
+      rc4[rg(e)][l & 3] += sg;
+      wc2[wg(e)][l & 1] += sg;
+    };
+    for (size_t e = 0; e < ed.size(); ++e) bal_put((int)e, +1);
+    auto bcost = [&](const std::vector<int>& es) {
+      long long v = 0;
+      std::vector<int> gr, gw;
+      for (int e : es) { gr.push_back(rg(e)); gw.push_back(wg(e)); }
+      std::sort(gr.begin(), gr.end()); gr.erase(std::unique(gr.begin(), gr.end()), gr.end());
+      std::sort(gw.begin(), gw.end()); gw.erase(std::unique(gw.begin(), gw.end()), gw.end());
+      for (int g : gr) for (int q = 0; q < 4; ++q) v += (long long)rc4[g][q] * rc4[g][q];
+      for (int g : gw) for (int q = 0; q < 2; ++q) v += (long long)wc2[g][q] * wc2[g][q];
+      return v;
+    };
+    for (long long it = 0; it < bal_iters; ++it) {
+      const int i1 = (int)(rnd() % (uint64_t)m), i2 = (int)(rnd() % (uint64_t)m);
+      if (i1 == i2 || ((lab[i1] ^ lab[i2]) & 3) == 0) continue;
+      std::vector<int> es = row_e[i1];
+      es.insert(es.end(), row_e[i2].begin(), row_e[i2].end());
+      const long long before = bcost(es);
+      for (int e : es) bal_put(e, -1);
+      std::swap(lab[i1], lab[i2]);
+      for (int e : es) bal_put(e, +1);
+      if (bcost(es) > before) {
+        for (int e : es) bal_put(e, -1);
+        std::swap(lab[i1], lab[i2]);
+        for (int e : es) bal_put(e, +1);
+      }
+    }
+    long long worst = 0, sumsq = 0;
+    for (int g = 0; g < NR; ++g) for (int q = 0; q < 4; ++q) { worst = std::max<long long>(worst, rc4[g][q]); sumsq += (long long)rc4[g][q] * rc4[g][q]; }
+    printf("balance: max class count per read group %lld, sum sq %lld\n", worst, sumsq);
+    // re-seat every edge and the CS words under the new labels
+    for (auto& g : R) g.init();
+    for (auto& g : W) g.init();
+    for (auto& g : C) g.init();
+    csm.clear();
+    for (size_t e = 0; e < ed.size(); ++e) put((int)e, +1);
+  }
+  // optional phase 1 (argv[6] = 1): per label class (lab mod 4), a proper 8-edge-colouring of the
+  // bipartite multigraph rows x read groups (Konig: max degree 8 after balancing) by alternating-path
+  // recolouring; colour = the edge's position in its row, the row's free colour = its CS position.
+  // Conflict-free V-slot reads by construction (when every group holds <= 8 rows of each class).
+  if (argc > 6 && atoi(argv[6]) == 1) {
+    const int NC = 8;
+    // colour tables: at_row[i][c] = edge or -1, at_grp[g][c] = edge or -1 (per class: groups are shared
+    // across classes, so index by (class, group))
+    std::vector<std::vector<int>> at_row(m, std::vector<int>(NC, -1));
+    std::vector<std::vector<int>> at_grp((size_t)NR * 4, std::vector<int>(NC, -1));
+    std::vector<int> col(ed.size(), -1);
+    auto gkey = [&](int e) { return (size_t)rg(e) * 4 + (lab[ed[e].row] & 3); };
+    int failed = 0;
+    for (size_t e0 = 0; e0 < ed.size(); ++e0) {
+      const int e = (int)e0, i = ed[e].row;
+      const size_t gk = gkey(e);
+      int a = -1, b = -1;
+      for (int c2 = 0; c2 < NC && a < 0; ++c2)
+        if (at_row[i][c2] < 0) a = c2;
+      for (int c2 = 0; c2 < NC && b < 0; ++c2)
+        if (at_grp[gk][c2] < 0) b = c2;
+      if (a < 0 || b < 0) { ++failed; continue; }
+      if (at_grp[gk][a] >= 0) {
+        // flip the a/b alternating path that starts at group gk with colour a
+        std::vector<int> path;
+        size_t g = gk;
+        int row = -1;
+        int cur = a;
+        while (true) {
+          const int pe = at_grp[g][cur];
+          if (pe < 0) break;
+          path.push_back(pe);
+          row = ed[pe].row;
+          const int nxt = cur == a ? b : a;
+          const int qe = at_row[row][nxt];
+          if (qe < 0) break;
+          path.push_back(qe);
+          g = gkey(qe);
+          cur = a;  // from the group side we follow colour a again (a, b, a, b ...)
+          (void)cur;
+        }
+        for (int pe : path) {  // unassign
+          at_row[ed[pe].row][col[pe]] = -1;
+          at_grp[gkey(pe)][col[pe]] = -1;
+        }
+        for (int pe : path) {  // swap a <-> b
+          col[pe] = col[pe] == a ? b : a;
+          at_row[ed[pe].row][col[pe]] = pe;
+          at_grp[gkey(pe)][col[pe]] = pe;
+        }
+      }
+      if (at_row[i][a] >= 0 || at_grp[gk][a] >= 0) { ++failed; continue; }
+      col[e] = a;
+      at_row[i][a] = e;
+      at_grp[gk][a] = e;
+    }
+    // positions: colour = position; the CS word takes the row's free colour
+    for (int i = 0; i < m; ++i) {
+      for (int q = 0; q < 8; ++q) at[i][q] = -1;
+      for (int e : row_e[i]) if (col[e] >= 0) { at[i][col[e]] = e; ed[e].ps = col[e]; }
+      for (int e : row_e[i]) if (col[e] < 0) for (int q = 0; q < 8; ++q) if (at[i][q] == -1) { at[i][q] = e; ed[e].ps = q; break; }
+      for (int q = 0; q < 8; ++q) if (at[i][q] == -1) { at[i][q] = -2; break; }
+    }
+    printf("colouring: %d edges left uncoloured\n", failed);
+    for (auto& g : R) g.init();
+    for (auto& g : W) g.init();
+    for (auto& g : C) g.init();
+    csm.clear();
+    for (size_t e = 0; e < ed.size(); ++e) put((int)e, +1);
+  }
   long long c, r, w;
   totals(c, r, w);
   long long ng = 0, nw = 0;
