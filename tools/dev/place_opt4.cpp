@@ -236,6 +236,86 @@ int main(int argc, char** argv) {
       for (int q = 0; q < 8; ++q) if (at[i][q] == -1) { at[i][q] = -2; break; }
     }
     printf("colouring: %d edges left uncoloured\n", failed);
+    // phase 2 (argv[7] = moves): Kempe-chain recolouring inside one class graph (swap colours a <-> b
+    // along the alternating path through an edge): the colouring stays proper, so the reads stay
+    // conflict-free, while the positions of the chain's edges and the free colour (CS position) of
+    // its end rows change; accepted when CS + stores do not get worse (exact group costs)
+    const long long kmoves = argc > 7 ? atoll(argv[7]) : 0;
+    if (kmoves > 0) {
+      std::vector<int> tr, tw;
+      auto rebuild_at = [&](int i) {
+        for (int q = 0; q < 8; ++q) at[i][q] = -1;
+        for (int e : row_e[i]) { at[i][col[e]] = e; ed[e].ps = col[e]; }
+        for (int q = 0; q < 8; ++q) if (at[i][q] == -1) { at[i][q] = -2; break; }
+      };
+      for (int i = 0; i < m; ++i) rebuild_at(i);
+      for (auto& g : R) g.init();
+      for (auto& g : W) g.init();
+      for (auto& g : C) g.init();
+      csm.clear();
+      for (size_t e = 0; e < ed.size(); ++e) put((int)e, +1);
+      long long acc = 0;
+      for (long long it = 0; it < kmoves; ++it) {
+        const int e0 = (int)(rnd() % (uint64_t)ed.size());
+        const int a = col[e0];
+        int b = (int)(rnd() % 7);
+        if (b >= a) ++b;
+        // collect the chain: from e0 walk both directions alternating a/b
+        std::vector<int> chain{e0};
+        for (int dir = 0; dir < 2; ++dir) {
+          int e = e0;
+          bool at_group = dir == 0;  // first step: across the group (dir 0) or the row (dir 1)
+          int want = b;
+          for (int guard = 0; guard < 4000; ++guard) {
+            int nx = at_group ? at_grp[gkey(e)][want] : at_row[ed[e].row][want];
+            if (nx < 0 || nx == e0) break;
+            chain.push_back(nx);
+            e = nx;
+            at_group = !at_group;
+            want = want == a ? b : a;
+          }
+        }
+        std::sort(chain.begin(), chain.end());
+        chain.erase(std::unique(chain.begin(), chain.end()), chain.end());
+        if (chain.size() > 400) continue;
+        // affected rows: rows of chain edges (all their edges' CS entries move with the CS position)
+        std::vector<int> rows;
+        for (int e : chain) rows.push_back(ed[e].row);
+        std::sort(rows.begin(), rows.end());
+        rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
+        std::vector<int> es;
+        for (int i : rows) es.insert(es.end(), row_e[i].begin(), row_e[i].end());
+        tr.clear();
+        tw.clear();
+        for (int e : es) { tr.push_back(rg(e)); tw.push_back(wg(e)); }
+        auto cs_store = [&]() {
+          std::sort(tr.begin(), tr.end()); tr.erase(std::unique(tr.begin(), tr.end()), tr.end());
+          std::sort(tw.begin(), tw.end()); tw.erase(std::unique(tw.begin(), tw.end()), tw.end());
+          double v = 0;
+          for (int g : tr) v += C[g].cost() + R[g].cost();
+          for (int g : tw) v += W[g].cost();
+          return v;
+        };
+        const double before = cs_store();
+        auto flip = [&]() {
+          for (int e : es) put(e, -1);
+          for (int e : chain) { at_row[ed[e].row][col[e]] = -1; at_grp[gkey(e)][col[e]] = -1; }
+          for (int e : chain) col[e] = col[e] == a ? b : a;
+          for (int e : chain) { at_row[ed[e].row][col[e]] = e; at_grp[gkey(e)][col[e]] = e; }
+          for (int i : rows) rebuild_at(i);
+          for (int e : es) put(e, +1);
+        };
+        flip();
+        const double after = cs_store();
+        if (after > before) flip(); else ++acc;
+        if ((it + 1) % (kmoves / 5 > 0 ? kmoves / 5 : 1) == 0) {
+          long long c2, r2, w2;
+          totals(c2, r2, w2);
+          printf("kempe %lld: cs %lld read %lld store %lld (accepted %lld)\n", it + 1, c2, r2, w2, acc);
+          fflush(stdout);
+        }
+      }
+    }
     for (auto& g : R) g.init();
     for (auto& g : W) g.init();
     for (auto& g : C) g.init();
