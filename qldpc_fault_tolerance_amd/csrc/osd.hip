@@ -569,6 +569,8 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
         int* pk = reinterpret_cast<int*>(prow + 32 * (WR + 1));       // [32] pivot rows of the panel
         int* pidx = pk + 32;                                          // [m] panel index of a pivot row
         __shared__ int s_P;
+        __shared__ uint32_t s_wslot[2][LB / 64][2];  // PNL == 2: per step parity and wave, (half-word, mask)
+        int step3p = 0, sparp = 0;                   // PNL == 2: s_piv slot / s_wslot parity of the step
         uint32_t usedm = 0;  // search wave: bit s = row s * 64 + lane is used (rows >= m: always)
         if (tid < 64) {
 #pragma unroll
@@ -582,6 +584,68 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
           const int q = qh >> 1, h = qh & 1;
           if (qh * 32 >= n || npiv >= rank) break;  // uniform
           const int bend = n - qh * 32 < 32 ? n - qh * 32 : 32;
+          if constexpr (PNL == 2) {
+            // 1-2 (distributed panel, round 4): every thread keeps its own row's panel half-word and
+            // combination mask in VGPRs and searches it: per pivot one wave minimum, one LDS atomic
+            // and ONE barrier; each wave's best row publishes its (half-word, mask) in the wave's
+            // slot of this step's parity before that barrier, so the winner's pair is readable
+            // right after it (2 words, not the 25-word row of the per-pivot elimination)
+            uint32_t wv = 0, cm = 0;
+            if (tid < m) {
+              u64 wq = 0;
+#pragma unroll
+              for (int q2 = 0; q2 < WR; ++q2)
+                if (q2 == q) wq = row[0][q2];
+              wv = (uint32_t)(h ? wq >> 32 : wq);
+            }
+            bool usd = used_r[0];  // (rows >= m: used from the start)
+            const uint32_t wmask = bend < 32 ? (1u << bend) - 1u : ~0u;
+            int P = 0, b = 0;
+            while (b < bend && npiv < rank) {  // uniform
+              const int slot = step3p;
+              step3p = step3p == 2 ? 0 : step3p + 1;
+              const int par = sparp;
+              sparp ^= 1;
+              const uint32_t lowm = (~0u << b) & wmask;
+              const uint32_t mm = usd ? 0u : (wv & lowm);
+              uint32_t key = mm ? ((uint32_t)(__ffs((int)mm) - 1) << 11) | (uint32_t)tid : 0x7FFFFFFFu;
+              key = wave_min_u32(key);
+              if (key != 0x7FFFFFFFu && (uint32_t)tid == (key & 2047u)) {
+                s_wslot[par][tid >> 6][0] = wv;
+                s_wslot[par][tid >> 6][1] = cm;
+              }
+              if ((tid & 63) == 0 && key != 0x7FFFFFFFu) atomicMin(&s_piv[slot], (int)key);
+              __syncthreads();
+              const int kk = s_piv[slot];
+              if (tid == 0) s_piv[step3p == 2 ? 0 : step3p + 1] = 0x7FFFFFFF;  // re-arm two steps ahead
+              if (kk == 0x7FFFFFFF) break;  // no pivot left in this panel (uniform)
+              const int fb = kk >> 11, r = kk & 2047;
+              const uint32_t pwv = s_wslot[par][r >> 6][0], pmv = s_wslot[par][r >> 6][1];
+              if (tid == r) {
+                usd = true;
+                pivrow[npiv] = r;
+                pivpos[npiv] = qh * 32 + fb;
+                pk[P] = r;
+                pidx[r] = P;
+              }
+              const bool hb = ((wv >> fb) & 1u) != 0 && tid != r;
+              const uint32_t add = pmv | (1u << P);
+              wv ^= hb ? pwv : 0u;
+              cm ^= hb ? add : 0u;
+              ++P;
+              ++npiv;
+              b = fb + 1;
+            }
+            used_r[0] = usd;
+            if (tid < m) {
+              pw[tid] = wv;
+              pmask[tid] = cm;
+            }
+            if (tid == 0) {
+              s_P = P;
+              s_npiv = npiv;
+            }
+          } else {
           // 1. every row's panel half-word (up to date: all earlier panels applied)
           if (tid < m) {
             u64 wq = 0;
@@ -651,6 +715,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
               s_npiv = npiv;
             }
           }
+          }  // PNL == 1
           __syncthreads();
           const int P = s_P;
           npiv = s_npiv;
@@ -672,7 +737,30 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
             const uint32_t msk = pmask[tid];
             u64 accq = 0;
             for (int kx = 0; kx < P; ++kx) {  // uniform loop: one broadcast read per word
-              if ((msk >> kx) & 1u) {
+              if constexpr (PNL == 2) {
+                // branch-free: every word read (independent broadcast loads the compiler keeps in
+                // flight together) and applied under predicates; the conditional form chained a
+                // load-wait-xor per word behind uniform branches (the PNL = 1 measurement)
+                const bool mine = ((msk >> kx) & 1u) != 0;
+                if (!__any(mine)) continue;  // (no row of this wave names pivot kx)
+                const u64* src = prow + kx * (WR + 1);
+                constexpr int XB = kOsdXB;
+                u64 buf[XB];
+#pragma unroll
+                for (int u = 0; u < XB; ++u)
+                  if (u < WR) buf[u] = src[u];
+                const uint32_t vs = (uint32_t)src[WR];
+                const u64 lowq = (mine && h == 0) ? ~0ull : 0ull;
+#pragma unroll
+                for (int q2 = 0; q2 < WR; ++q2) {
+                  const u64 pv = buf[q2 % XB];
+                  if (q2 + XB < WR) buf[q2 % XB] = src[q2 + XB];
+                  const u64 sel = (mine && q2 > q) ? ~0ull : 0ull;
+                  row[0][q2] ^= pv & sel;
+                  if (q2 == q) accq ^= pv & lowq;  // (q uniform: a select, no branch)
+                }
+                sbit[0] ^= mine ? vs : 0u;
+              } else if ((msk >> kx) & 1u) {
                 const u64* src = prow + kx * (WR + 1);
 #pragma unroll
                 for (int q2 = 0; q2 < WR; ++q2) {
@@ -1529,7 +1617,9 @@ OsdKern osd_rr_kernel_t(int wr) {
     default: return nullptr;
   }
 }
-OsdKern osd_rr_kernel(int wr, int pnl) { return pnl ? osd_rr_kernel_t<1>(wr) : osd_rr_kernel_t<0>(wr); }
+OsdKern osd_rr_kernel(int wr, int pnl) {
+  return pnl == 2 ? osd_rr_kernel_t<2>(wr) : pnl ? osd_rr_kernel_t<1>(wr) : osd_rr_kernel_t<0>(wr);
+}
 OsdKern osd_rr2_kernel_of(int wr) {
 #if QLDPC_EXPERIMENTAL
   switch (wr) {
@@ -1641,7 +1731,7 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   // (profiles/r03/bposd_pnl/)
   const char* pnl_env = std::getenv("QLDPC_OSD_PNL");
   if (G->wr && pnl_env && std::atoi(pnl_env) != 0) {
-    G->pnl = 1;
+    G->pnl = std::atoi(pnl_env) == 2 ? 2 : 1;  // 2: the distributed panel search (one barrier per pivot)
     G->pnl_off = (int)((G->lds + 15) & ~(size_t)15);
     G->lds = (size_t)G->pnl_off + osd_pnl_bytes(m, G->wr);
   }
