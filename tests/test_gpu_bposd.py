@@ -134,14 +134,19 @@ def test_bposd_shot_loop_matches_oracle_per_shot(gpu, oracle):
 
 # elimination modes of osd_gpu_kernel: the default (register rows for m <= 768 / 1024), the
 # LDS-resident word-major image (QLDPC_OSD_RR=0) and the HBM slice (QLDPC_OSD_RR=0 QLDPC_OSD_LDS=0)
-_OSD_MODES = {"default": {}, "lds": {"QLDPC_OSD_RR": "0"}, "hbm": {"QLDPC_OSD_RR": "0", "QLDPC_OSD_LDS": "0"}}
+# and the opt-in panel eliminations of the register rows (QLDPC_OSD_PNL=1: one search wave; 2: every
+# thread searches its own row, one barrier per pivot; both measured slower)
+_OSD_MODES = {"default": {}, "lds": {"QLDPC_OSD_RR": "0"}, "hbm": {"QLDPC_OSD_RR": "0", "QLDPC_OSD_LDS": "0"},
+              "pnl1": {"QLDPC_OSD_PNL": "1"}, "pnl2": {"QLDPC_OSD_PNL": "2"}}
 
 
 @pytest.mark.parametrize("name,t0,method,order,mode", [
     ("hgp_34_n225", 0, "osd_e", 10, "default"), ("hgp_34_n225", 0, "osd_cs", 8, "default"), ("hgp_34_n225", 0, "osd_0", 0, "default"),
     ("hgp_34_n1600", 0, "osd_e", 10, "default"), ("hgp_34_n1600", 0, "osd_cs", 6, "default"), ("hgp_34_n225", 3, "osd_e", 8, "default"),
     ("hgp_34_n225", 0, "osd_e", 10, "lds"), ("hgp_34_n1600", 0, "osd_e", 10, "lds"), ("hgp_34_n225", 3, "osd_e", 8, "lds"),
-    ("hgp_34_n225", 0, "osd_e", 10, "hbm"), ("hgp_34_n1600", 0, "osd_cs", 6, "hbm"), ("hgp_34_n225", 3, "osd_e", 8, "hbm")])
+    ("hgp_34_n225", 0, "osd_e", 10, "hbm"), ("hgp_34_n1600", 0, "osd_cs", 6, "hbm"), ("hgp_34_n225", 3, "osd_e", 8, "hbm"),
+    ("hgp_34_n1600", 0, "osd_e", 10, "pnl1"), ("hgp_34_n225", 3, "osd_e", 8, "pnl1"),
+    ("hgp_34_n225", 0, "osd_cs", 8, "pnl2"), ("hgp_34_n1600", 0, "osd_e", 10, "pnl2"), ("hgp_34_n225", 3, "osd_e", 8, "pnl2")])
 def test_gpu_osd_matches_host_osd(gpu, monkeypatch, name, t0, method, order, mode):
     """GPU OSD kernel == native host OSD stage (itself pinned to the oracle in
     tests/test_osd_cpu.py) on GPU soft-BP posteriors, incl. a rank-deficient space-time graph
