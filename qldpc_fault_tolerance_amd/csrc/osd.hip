@@ -584,6 +584,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
           const int q = qh >> 1, h = qh & 1;
           if (qh * 32 >= n || npiv >= rank) break;  // uniform
           const int bend = n - qh * 32 < 32 ? n - qh * 32 : 32;
+          unsigned long long tp0 = QLDPC_STAMPS ? osd_stamp() : 0ull;
           if constexpr (PNL == 2) {
             // 1-2 (distributed panel, round 4): every thread keeps its own row's panel half-word and
             // combination mask in VGPRs and searches it: per pivot one wave minimum, one LDS atomic
@@ -719,6 +720,12 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
           __syncthreads();
           const int P = s_P;
           npiv = s_npiv;
+          if (QLDPC_STAMPS) {  // [8]: the panel's pivot search, [7]: its pivots
+            const unsigned long long t = osd_stamp();
+            st[8] += t - tp0;
+            st[7] += (unsigned long long)P;
+            tp0 = t;
+          }
           // 3. the panel's pivot rows publish their panel-start words q.. and syndrome bit
           if (tid < m) {
             const int kx = pidx[tid];
@@ -775,6 +782,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
             for (int q2 = 0; q2 < WR; ++q2)
               if (q2 == q) row[0][q2] = h ? ((row[0][q2] & kLo) | (fw << 32)) : (((row[0][q2] ^ accq) & kHi) | fw);
           }
+          if (QLDPC_STAMPS) st[9] += osd_stamp() - tp0;  // [9]: the panel's row updates
           // (the next panel rewrites pw[tid] / prow only behind its first two barriers)
         }
       } else {

@@ -36,6 +36,10 @@ tot = sum(v[:6])
 print(f"{name} p={p} shots={c} osd decodes={o} syndromes stamped={v[6]}")
 for k, nm in enumerate(names):
     print(f"{nm:20s} {100 * v[k] / max(1, tot):6.2f}%  {v[k] / max(1, v[6]):10.0f} clk per syndrome")
-print(f"positions per syndrome {v[7] / max(1, v[6]):.0f}; per position: {v[2] / max(1, v[7]):.0f} clk, "
-      f"of which search + barrier {v[8] / max(1, v[7]):.0f}, pivot-row publication + barrier (register rows) "
-      f"{v[9] / max(1, v[7]):.0f}")
+if os.environ.get("QLDPC_OSD_PNL", "0") in ("1", "2"):  # panel modes: [7] pivots, [8] panel searches, [9] panel updates
+    print(f"pivots per syndrome {v[7] / max(1, v[6]):.0f}; per pivot: {v[2] / max(1, v[7]):.0f} clk, "
+          f"of which the panel's pivot search {v[8] / max(1, v[7]):.0f}, the panel's row updates {v[9] / max(1, v[7]):.0f}")
+else:
+    print(f"positions per syndrome {v[7] / max(1, v[6]):.0f}; per position: {v[2] / max(1, v[7]):.0f} clk, "
+          f"of which search + barrier {v[8] / max(1, v[7]):.0f}, pivot-row publication + barrier (register rows) "
+          f"{v[9] / max(1, v[7]):.0f}")
