@@ -372,6 +372,12 @@ constexpr int kOsdMaxN = 8192;
 #define QLDPC_OSD_XB 8
 #endif
 constexpr int kOsdXB = QLDPC_OSD_XB;
+// register-row mode: the lean per-pivot loop (one stamped LDS max per wave instead of a
+// triple-buffered atomicMin, a DPP row-broadcast wave minimum, pivots recorded in LDS); 0 = the
+// round-3 loop (A/B builds)
+#ifndef QLDPC_OSD_LEAN
+#define QLDPC_OSD_LEAN 1
+#endif
 // A/B build: one barrier per pivot in register-row mode (the candidate row published before the
 // search barrier, per-wave slots of two step parities)
 #ifndef QLDPC_OSD_1B
@@ -420,6 +426,41 @@ __device__ inline uint32_t wave_min_u32(uint32_t v) {
             mn((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
 }
 
+// the same minimum in 6 DPP VALU + 1 readlane: rotations give every lane its 16-lane row's
+// minimum, row_bcast:15 / row_bcast:31 fold rows 0-1 / 2-3 / all into lane 63 (the GFX9 DPP
+// broadcasts; the s_nops are the DPP read-after-VALU-write wait states).  All lanes active.
+__device__ inline uint32_t wave_min_u32_bc(uint32_t v) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "s_nop 1"
+      : "+v"(v));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0
+__device__ inline uint32_t ffbl_u32(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// LDS max at byte address a by the calling lanes, completed before return (plain ds_max_u32: the
+// compiler's atomic optimizer would wrap a builtin atomic in a first-lane election per call)
+__device__ inline void lds_max_u32_sync(uint32_t a, uint32_t v) {
+  asm volatile("ds_max_u32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(a), "v"(v) : "memory");
+}
+
 __device__ inline u64 ord_key(double x) {
   if (x == 0.0) x = 0.0;  // -0 ties +0, as std::stable_sort's `<` has it
   const u64 u = (u64)__double_as_longlong(x);
@@ -449,6 +490,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   uint32_t* used = reinterpret_cast<uint32_t*>(smem + A.bits_off);  // [ceil(m/32)]
   uint32_t* sb = used + (m + 31) / 32;                         // [ceil(m/32)] syndrome, reduced
   __shared__ int s_piv[3], s_npiv;  // s_piv triple-buffered by position: reset two columns ahead
+  __shared__ uint32_t s_pivx;       // lean loop: (search step << 17) | (0x1FFFF - key), max over the waves
   __shared__ u64 s_best;
   u64* Mg = A.ws + (size_t)blockIdx.x * A.ws_words;
   u64* X = Mg + (size_t)W * m;  // X[0] = S0, X[1 + j] = x(h_j)
@@ -531,6 +573,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
     if (tid == 0) {
       s_npiv = 0;
       s_piv[0] = s_piv[1] = s_piv[2] = 0x7FFFFFFF;
+      s_pivx = 0u;
     }
     __syncthreads();
     if constexpr (kRR) {
@@ -785,6 +828,107 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
           if (QLDPC_STAMPS) st[9] += osd_stamp() - tp0;  // [9]: the panel's row updates
           // (the next panel rewrites pw[tid] / prow only behind its first two barriers)
         }
+      } else if constexpr (QLDPC_OSD_LEAN && !QLDPC_OSD_1B) {
+        // Lean per-pivot loop (round 4): same pivots as the loop below, fewer instructions per
+        // wave and step (a pivot step is bound by every wave's own instruction stream: all waves
+        // meet at its two barriers; profiles/r04/passo/).  The step's winner is the maximum of
+        // (step << 17) | (0x1FFFF - key) over one ds_max per wave: a stale value from an earlier
+        // step never matches the step, so the slot needs no re-arming.  Pivots go to an LDS list
+        // over the (dead) sort keys: (position << 11) | row.
+        int32_t* lkk = reinterpret_cast<int32_t*>(smem);
+        const uint32_t pivx_a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&s_pivx);
+        uint32_t step = 0;  // uniform
+        uint32_t um[RPT];   // ~0 while row tid + j * TB is a candidate (unused, < m), else 0
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) um[j] = used_r[j] ? 0u : ~0u;
+#pragma unroll
+        for (int q = 0; q < WR; ++q) {
+          if (q * 64 >= n || npiv >= rank) break;  // uniform
+          const int bend = n - q * 64 < 64 ? n - q * 64 : 64;
+          const u64 wmask = bend < 64 ? (1ull << bend) - 1ull : ~0ull;
+          int b = 0;
+          for (;;) {  // uniform
+            ++step;
+            asm volatile("" : "+s"(step));  // opaque: no strength-reduced copies of step << 17 per word
+            unsigned long long ts0 = 0;
+            if (QLDPC_STAMPS) {
+              ts0 = osd_stamp();
+              st[7] += 1;
+            }
+            const u64 lowm = (~0ull << b) & wmask;
+            // key = (first set bit >= b << 11) | row; a row without one gets first bit 0xFFFFFFFF
+            // (v_ffbl of 0), i.e. a key >= 0xFFFFF800, above every real key (<= 0x1FFFF)
+            uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < RPT; ++j) {
+              const uint32_t ml = (uint32_t)row[j][q] & (uint32_t)lowm & um[j];
+              const uint32_t mh = (uint32_t)(row[j][q] >> 32) & (uint32_t)(lowm >> 32) & um[j];
+              const uint32_t fl = ffbl_u32(ml), fh = ffbl_u32(mh) | 32u;
+              const uint32_t f = fl < fh ? fl : fh;
+              const uint32_t kj = (f << 11) | (uint32_t)(tid + j * TB);
+              key = kj < key ? kj : key;
+            }
+            key = wave_min_u32_bc(key);
+            if ((tid & 63) == 0 && key <= 0x1FFFFu) lds_max_u32_sync(pivx_a, (step << 17) | (0x1FFFFu - key));
+            __syncthreads();
+            if (QLDPC_STAMPS) {
+              const unsigned long long t = osd_stamp();
+              st[8] += t - ts0;
+              ts0 = t;
+            }
+            const uint32_t vx = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_pivx);  // uniform
+            if ((vx >> 17) != step) break;  // no pivot left in this word (uniform)
+            const uint32_t kk = 0x1FFFFu - (vx & 0x1FFFFu);
+            const int fb = (int)(kk >> 11), r = (int)(kk & 2047u);
+            bool hb[RPT];
+#pragma unroll
+            for (int j = 0; j < RPT; ++j) {
+              hb[j] = ((row[j][q] >> fb) & 1ull) != 0;
+              if (tid + j * TB == r) {
+                used_r[j] = true;
+                um[j] = 0u;
+#pragma unroll
+                for (int q2 = q; q2 < WR; ++q2) pbuf[q2] = row[j][q2];
+                pbuf[WR] = sbit[j];
+                lkk[npiv] = ((q * 64 + fb) << 11) | r;
+              }
+            }
+            ++npiv;
+            __syncthreads();
+            if (QLDPC_STAMPS) st[9] += osd_stamp() - ts0;
+            bool upd[RPT], any = false;
+#pragma unroll
+            for (int j = 0; j < RPT; ++j) {
+              upd[j] = hb[j] && tid + j * TB != r;
+              any = any || upd[j];
+            }
+            if (any) {  // pivot-row words through the rolling buffer, as below
+              constexpr int XB = kOsdXB;
+              u64 buf[XB];
+#pragma unroll
+              for (int u = 0; u < XB; ++u)
+                if (q + u < WR) buf[u] = pbuf[q + u];
+              const uint32_t ps = (uint32_t)pbuf[WR];
+#pragma unroll
+              for (int q2 = q; q2 < WR; ++q2) {
+                const u64 pv = buf[(q2 - q) % XB];
+                if (q2 + XB < WR) buf[(q2 - q) % XB] = pbuf[q2 + XB];
+#pragma unroll
+                for (int j = 0; j < RPT; ++j) row[j][q2] ^= upd[j] ? pv : 0ull;
+              }
+#pragma unroll
+              for (int j = 0; j < RPT; ++j) sbit[j] ^= upd[j] ? ps : 0u;
+            }
+            b = fb + 1;
+            if (b >= bend || npiv >= rank) break;  // uniform
+          }
+        }
+        // the pivot list -> pivrow / pivpos (every lkk write precedes one of the loop's barriers)
+        for (int i = tid; i < npiv; i += TB) {
+          const int v = lkk[i];
+          pivrow[i] = v & 2047;
+          pivpos[i] = v >> 11;
+        }
       } else {
       int step3 = 0;  // search step mod 3: s_piv slot of the step (triple-buffered as above)
       int spar = 0;   // search step mod 2
@@ -906,9 +1050,13 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
       for (int j = 0; j < RPT; ++j) {
         const int i = tid + j * TB;
         if (i < m) {
+          // opaque row pointer: the compiler otherwise hoists the WR word addresses out of the
+          // syndrome loop, 2 * WR VGPRs live through the whole elimination (round 4 asm review)
+          u64* mrow = Mg + i;
+          asm volatile("" : "+v"(mrow));
 #pragma unroll
           for (int q = 0; q < WR; ++q)
-            if (q < W) Mg[(size_t)q * m + i] = row[j][q];
+            if (q < W) mrow[(size_t)q * m] = row[j][q];
         }
         const unsigned long long sbal = __ballot(i < m && sbit[j]);
         if ((tid & 63) == 0) {
@@ -1183,8 +1331,12 @@ __device__ __attribute__((always_inline)) inline void osd_for_words(std::integer
 // syndrome after the other.  A syndrome that finishes its word (no pivot left, or rank reached)
 // idles through the other's remaining steps of that word.  Outputs identical to osd_gpu_kernel.
 // MEASURED AND NOT KEPT (experimental builds only): bit-exact (52 BP+OSD / phenl / circuit GPU
-// tests), but 2 x 25 row words leave too few of the 168 VGPRs (105 spilled): n1600 BP+OSD 539 k
-// vs 548 k shots/s with one syndrome per workgroup (profiles/r04/passf/).
+// tests), but 2 x 25 row words left too few of the 168 VGPRs (105 spilled): n1600 BP+OSD 539 k
+// vs 548 k shots/s with one syndrome per workgroup (profiles/r04/passf/).  Most of the pressure
+// was hoisted write-out addresses; with those opaque (1 dword spilled, 57 GPU tests green) it is
+// 537.5 k vs 539 k on one box (profiles/r04/passo/): two eliminations per chain of barriers cost
+// what two chains cost, i.e. a pivot step is bound by its VALU issue (~3 waves per SIMD x ~90
+// VALU x 4 cycles), not by the barrier latency.
 template <int WR>
 __global__ void __launch_bounds__(768) osd_rr2_kernel(OsdGpuArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1394,9 +1546,13 @@ __global__ void __launch_bounds__(768) osd_rr2_kernel(OsdGpuArgs A) {
       {
         const int i = tid;
         if (i < m) {
+          // opaque row pointer: the compiler otherwise hoists the WR word addresses out of the
+          // syndrome loop (2 * WR VGPRs live through the elimination: 105 VGPRs spilled -> 1 dword)
+          u64* mrow = Mg + i;
+          asm volatile("" : "+v"(mrow));
 #pragma unroll
           for (int q = 0; q < WR; ++q)
-            if (q < W) Mg[(size_t)q * m + i] = row[s][q];
+            if (q < W) mrow[(size_t)q * m] = row[s][q];
         }
         const unsigned long long sbal = __ballot(i < m && sbit[s]);
         if ((tid & 63) == 0) {
