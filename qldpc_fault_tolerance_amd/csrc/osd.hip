@@ -383,6 +383,24 @@ constexpr int kOsdXB = QLDPC_OSD_XB;
 #ifndef QLDPC_OSD_1B
 #define QLDPC_OSD_1B 0
 #endif
+// register-row mode: Four-Russians groups of kOsdG pivots (QLDPC_OSD_M4R): within a group only
+// the pivot word is updated per pivot (plus a mask of the group pivots' start rows each row has
+// absorbed); at the group's end every row xors in ONE table entry (the xor of its mask's start
+// rows) per remaining word.  MEASURED AND NOT KEPT (A/B builds only): bit-exact (57 GPU tests),
+// n1600 BP+OSD 595 k (G = 4) / 596 k (G = 6) vs 614 k with the lean loop, n225 10.6 M vs 12.3 M
+// (profiles/r04/passr/): the group ends' two extra barriers and table build cost more than the
+// row xors they save
+#ifndef QLDPC_OSD_M4R
+#define QLDPC_OSD_M4R 0
+#endif
+#ifndef QLDPC_OSD_G
+#define QLDPC_OSD_G 4
+#endif
+constexpr bool kOsdM4R = QLDPC_OSD_M4R && !QLDPC_OSD_1B;
+constexpr int kOsdG = QLDPC_OSD_G;
+// rows of (WR + 1) words in the register-row pivot area: the pivot row (1), the one-barrier build's
+// per-wave slots, or the Four-Russians table (2^G rows) and its per-pivot slots (4 rows)
+constexpr int osd_prows(int lb) { return QLDPC_OSD_1B ? 2 * (lb / 64) : kOsdM4R ? (1 << kOsdG) + 4 : 1; }
 
 
 struct OsdGpuArgs {
@@ -828,6 +846,111 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
           if (QLDPC_STAMPS) st[9] += osd_stamp() - tp0;  // [9]: the panel's row updates
           // (the next panel rewrites pw[tid] / prow only behind its first two barriers)
         }
+      } else if constexpr (kOsdM4R && RPT == 1) {
+        // Four-Russians groups (round 4): the lean loop's search and winner (same pivots), but a
+        // pivot updates only the pivot word q of the rows that have its bit (exact, the next
+        // search reads nothing else) and their mask cm over the group's pivots: pivot k's row,
+        // as it is when chosen, is its group-start row S_k xor the start rows its own mask names,
+        // so absorbing it is cm ^= mask(k) ^ (1 << k).  At the group's end the pivot owners
+        // publish their start rows (words q+1.., syndrome bit) as T[1 << k], the workgroup fills
+        // T[c] = xor of the S_k, k in c, and every row xors T[cm] into its words q+1.. and its
+        // syndrome bit: one LDS read and one xor per word for up to kOsdG pivots.
+        int32_t* lkk = reinterpret_cast<int32_t*>(smem);
+        const uint32_t pivx_a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&s_pivx);
+        u64* T = pbuf;                                         // [2^G][WR + 1]
+        u64* slot = pbuf + (size_t)(1 << kOsdG) * (WR + 1);   // [G][2]: pivot k's word q, its mask
+        uint32_t step = 0;  // uniform
+        uint32_t um = used_r[0] ? 0u : ~0u;
+        uint32_t cm = 0;    // the group pivots' start rows this row has absorbed
+        int gi = -1;        // this row's index among the group's pivots
+#pragma unroll
+        for (int q = 0; q < WR; ++q) {
+          if (q * 64 >= n || npiv >= rank) break;  // uniform
+          const int bend = n - q * 64 < 64 ? n - q * 64 : 64;
+          const u64 wmask = bend < 64 ? (1ull << bend) - 1ull : ~0ull;
+          int b = 0;
+          bool more = true;  // uniform
+          while (more) {
+            int k = 0;  // pivots in this group (uniform)
+            for (;;) {  // uniform
+              ++step;
+              asm volatile("" : "+s"(step));
+              if (QLDPC_STAMPS) st[7] += 1;
+              const u64 lowm = (~0ull << b) & wmask;
+              const uint32_t ml = (uint32_t)row[0][q] & (uint32_t)lowm & um;
+              const uint32_t mh = (uint32_t)(row[0][q] >> 32) & (uint32_t)(lowm >> 32) & um;
+              const uint32_t fl = ffbl_u32(ml), fh = ffbl_u32(mh) | 32u;
+              uint32_t key = ((fl < fh ? fl : fh) << 11) | (uint32_t)tid;
+              key = wave_min_u32_bc(key);
+              if ((tid & 63) == 0 && key <= 0x1FFFFu) lds_max_u32_sync(pivx_a, (step << 17) | (0x1FFFFu - key));
+              __syncthreads();
+              const uint32_t vx = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_pivx);  // uniform
+              if ((vx >> 17) != step) {  // no pivot left in this word
+                more = false;
+                break;
+              }
+              const uint32_t kk = 0x1FFFFu - (vx & 0x1FFFFu);
+              const int fb = (int)(kk >> 11), r = (int)(kk & 2047u);
+              const bool hb = ((row[0][q] >> fb) & 1ull) != 0;
+              if (tid == r) {
+                used_r[0] = true;
+                um = 0u;
+                gi = k;
+                slot[2 * k] = row[0][q];
+                slot[2 * k + 1] = cm;
+                lkk[npiv] = ((q * 64 + fb) << 11) | r;
+              }
+              ++npiv;
+              __syncthreads();
+              if (hb && tid != r) {
+                row[0][q] ^= slot[2 * k];
+                cm ^= (uint32_t)slot[2 * k + 1] ^ (1u << k);
+              }
+              ++k;
+              b = fb + 1;
+              if (b >= bend || npiv >= rank) {
+                more = false;
+                break;
+              }
+              if (k == kOsdG) break;
+            }
+            if (k > 0) {  // uniform: the group's end
+              if (gi >= 0) {
+                u64* d = T + (size_t)(1 << gi) * (WR + 1);
+#pragma unroll
+                for (int q2 = q + 1; q2 < WR; ++q2) d[q2] = row[0][q2];
+                d[WR] = sbit[0];
+              }
+              __syncthreads();
+              const int nw = WR - q;  // words q+1 .. WR-1 and the syndrome entry WR (constant once unrolled)
+              for (int t = tid; t < (nw << kOsdG); t += TB) {
+                const int c = t / nw, w = q + 1 + t % nw;
+                if ((c >> k) == 0 && (c & (c - 1)) != 0) {  // combinations of >= 2 of the k pivots
+                  u64 v = 0;
+#pragma unroll
+                  for (int i = 0; i < kOsdG; ++i)
+                    if ((c >> i) & 1) v ^= T[(size_t)(1 << i) * (WR + 1) + w];
+                  T[(size_t)c * (WR + 1) + w] = v;
+                }
+              }
+              __syncthreads();
+              if (cm) {
+                const u64* src = T + (size_t)cm * (WR + 1);
+#pragma unroll
+                for (int q2 = q + 1; q2 < WR; ++q2) row[0][q2] ^= src[q2];
+                sbit[0] ^= (uint32_t)src[WR];
+              }
+              cm = 0;
+              gi = -1;
+              // (T and the slots are rewritten only behind the next group's first barriers)
+            }
+          }
+        }
+        for (int i = tid; i < npiv; i += TB) {
+          const int v = lkk[i];
+          pivrow[i] = v & 2047;
+          pivpos[i] = v >> 11;
+        }
       } else if constexpr (QLDPC_OSD_LEAN && !QLDPC_OSD_1B) {
         // Lean per-pivot loop (round 4): same pivots as the loop below, fewer instructions per
         // wave and step (a pivot step is bound by every wave's own instruction stream: all waves
@@ -1179,7 +1302,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
     // (Register-row mode stages pivpos in LDS first: the trace reads it r times.)
     const int32_t* pp = pivpos;
     if constexpr (kRR) {
-      int32_t* lpp = reinterpret_cast<int32_t*>(smem + A.pbuf_off + (QLDPC_OSD_1B ? 2 * (LB / 64) : 1) * (WR + 1) * 8);
+      int32_t* lpp = reinterpret_cast<int32_t*>(smem + A.pbuf_off + (size_t)osd_prows(LB) * (WR + 1) * 8);
       for (int i = tid; i < r; i += TB) lpp[i] = pivpos[i];
       __syncthreads();
       pp = lpp;
@@ -1886,7 +2009,7 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   G->pbuf_off = (int)(((size_t)G->bits_off + lbits + 15) & ~(size_t)15);
   // register-row mode: pivot-row buffer (QLDPC_OSD_1B: a slot per wave and step parity), then
   // pivpos staged for the swap trace (rank ints)
-  const size_t prows = QLDPC_OSD_1B ? 2 * (size_t)(osd_rr_threads(std::max(2, G->wr)) / 64) : 1;
+  const size_t prows = (size_t)osd_prows(osd_rr_threads(std::max(2, G->wr)));
   G->lds = G->wr ? (size_t)G->pbuf_off + prows * (size_t)(G->wr + 1) * 8 + (size_t)std::max(1, rank) * 4
                  : (size_t)G->bits_off + lbits;
   // panel elimination (register-row mode), opt-in QLDPC_OSD_PNL=1: bit-exact, but the single search
