@@ -184,16 +184,80 @@ class DetectorErrorModel:
     def __str__(self):
         """stim-style text (errors first, then the detector / shift lines in circuit order), with
         exact ``repr`` probabilities."""
-        lines = [f"error({p!r}) " + " ".join([f"D{d}" for d in ds] + [f"L{k}" for k in ks])
-                 for p, ds, ks in zip(self.probs, self.dets, self.obs)]
+        return self.to_text("exact")
+
+    def stim_order(self) -> list:
+        """Mechanism indices in the order stim lists one flush of its error classes: ascending by the
+        target list, detectors before observables, a prefix before its extensions (``error(0.125) D0``,
+        ``error(0.375) D0 D1``, ``error(0.25) D1`` in stim's ``detector_error_model`` docstring)."""
+        return sorted(range(self.num_errors), key=lambda j: (list(self.dets[j]) + [1 << 40 | k for k in self.obs[j]]))
+
+    def to_text(self, style: str = "exact") -> str:
+        """The DEM as the text ``GenFaultHyperGraph`` parses (``str(dem)``, ``src/Simulators_SpaceTime.py:950``):
+        every ``error(p) D.. L..`` line first, then the ``shift_detectors(1) 0`` / ``detector`` lines in
+        circuit order.
+
+        ``style="exact"``: this model's mechanism order, probabilities as ``repr`` (round-trip exact).
+        ``style="stim"``: stim's text as the reference saw it — mechanisms in :meth:`stim_order`, each
+        probability through C++'s default stream format (6 significant digits, ``%g``: exponent
+        notation below 1e-4), detector lines with their coordinate ``detector(0) Dk``.  Against stim
+        itself this rendering is parity unpinned (stim is absent); it is what ``compat=True`` parses."""
+        if style not in ("exact", "stim"):
+            raise ValueError(f"unknown DEM text style {style!r}")
+        order = self.stim_order() if style == "stim" else range(self.num_errors)
+        fmt = (lambda p: format(p, "g")) if style == "stim" else repr
+        lines = [f"error({fmt(self.probs[j])}) " + " ".join([f"D{d}" for d in self.dets[j]] + [f"L{k}" for k in self.obs[j]])
+                 for j in order]
+        det = "detector(0) D{}" if style == "stim" else "detector D{}"
         seg = 0
         for d, s in enumerate(self.det_segment):
             while seg < s:
                 lines.append("shift_detectors(1) 0")
                 seg += 1
-            lines.append(f"detector D{d}")
+            lines.append(det.format(d))
         lines += ["shift_detectors(1) 0"] * (self.num_shifts - seg)
         return "\n".join(lines)
+
+    @classmethod
+    def from_text(cls, text: str, compat: bool = False) -> "DetectorErrorModel":
+        """Parse DEM text the way ``GenFaultHyperGraph`` reads it (``src/Simulators_SpaceTime.py:554-583``):
+        error lines in order, detectors from the ``detector`` lines, segments from the
+        ``shift_detectors(1) 0`` lines.  ``compat=True`` reads each probability with the reference's
+        ``float(re.findall("\\d+\\.\\d+", token)[0])`` (``:575, :642``): a probability printed in
+        exponent notation keeps only its mantissa (``6.67e-05`` -> 6.67) and one printed without a
+        decimal point raises ``IndexError``, as the reference does; ``compat=False`` reads the number
+        exactly."""
+        import re
+
+        items = text.split("\n")
+        dem = cls(0, 0)
+        D = K = seg = 0
+        for it in items:
+            tok = it.split()
+            if not tok:
+                continue
+            if "error" in it:
+                head = tok[0]
+                if compat:
+                    p = float(re.findall(r"\d+\.\d+", head)[0])
+                else:
+                    p = float(head[head.index("(") + 1:head.rindex(")")])
+                ds = sorted(int(t[1:]) for t in tok[1:] if t.startswith("D"))
+                ks = sorted(int(t[1:]) for t in tok[1:] if t.startswith("L"))
+                dem.probs.append(p)
+                dem.dets.append(tuple(ds))
+                dem.obs.append(tuple(ks))
+                K = max([K] + [k + 1 for k in ks])
+                D = max([D] + [d + 1 for d in ds])
+            elif it.strip() == "shift_detectors(1) 0":
+                seg += 1
+            elif "detector" in it and "shift" not in it:
+                d = int(tok[1][1:])
+                while len(dem.det_segment) <= d:
+                    dem.det_segment.append(seg)
+                D = max(D, d + 1)
+        dem.num_detectors, dem.num_observables, dem.num_shifts = D, K, seg
+        return dem
 
 
 _PAULI2 = [(a, b) for a in range(4) for b in range(4) if (a, b) != (0, 0)]  # 0 I, 1 X, 2 Y, 3 Z
@@ -381,10 +445,26 @@ def GenCorrecHyperGraph(detector_error_model: DetectorErrorModel, num_rounds: in
     return Hs % 2
 
 
-def _as_dem(x) -> DetectorErrorModel:
+def _as_dem(x, compat: bool = True) -> DetectorErrorModel:
+    """A DEM object as is; DEM text (``str(...)`` of one, or stim's format) parsed the reference's way
+    (:meth:`DetectorErrorModel.from_text`, the reference's probability regex unless ``compat=False``)."""
     if isinstance(x, DetectorErrorModel):
         return x
-    raise TypeError("expected a DetectorErrorModel (stim is absent; build it with detector_error_model())")
+    if isinstance(x, str):
+        return DetectorErrorModel.from_text(x, compat=compat)
+    raise TypeError("expected a DetectorErrorModel or its text (stim is absent; build it with detector_error_model())")
+
+
+def misparsed_mechanisms(dem: DetectorErrorModel) -> list:
+    """Indices of the mechanisms whose probability the reference's ``\\d+\\.\\d+`` parse of stim's text
+    (6 significant digits, exponent notation below 1e-4) does not read back within that rounding:
+    the ones printed in exponent notation, which it reads as their mantissa (``5.33e-05`` -> 5.33)."""
+    out = []
+    for j, p in enumerate(dem.probs):
+        s = format(p, "g")
+        if "e" in s or "." not in s:
+            out.append(j)
+    return out
 
 
 # ------------------------------------------------------------------- CX schedules

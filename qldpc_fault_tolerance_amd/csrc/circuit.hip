@@ -11,7 +11,8 @@
 //       with the accumulated space correction, decoded by decoder1 on h1; the correction's space
 //       effect (h1_space_cor · c) and logical effect (L1 · c) accumulate (:983-993);
 //   (4) the final m detector rows XOR the accumulated space correction, decoded by decoder2 on h2
-//       (BP, or BP + OSD: GPU OSD for uniform priors, the host OSD stage otherwise);
+//       (BP, or BP + OSD on the GPU: the DEM's non-uniform priors weigh the OSD candidates by
+//       sum log(1 / p_j), osd.hip step 6'; no host round trip);
 //   (5) failure = (final syndrome + h2 · c2 != 0) or (observables + Σ L · c != 0) (:996-1004).
 // State is BIT-SLICED between the stages (word w of row r = row r of samples 64w..64w+63), so the
 // mechanism scatter of (1)-(2) is one wave ballot + one 64-bit atomic xor per (mechanism row, 64
@@ -162,13 +163,11 @@ struct qldpc_circ {
   qldpc_bp* dec1 = nullptr;
   qldpc_bp* dec2 = nullptr;
   qldpc_osd_gpu* osd_gpu = nullptr;
-  const qldpc_osd* osd_host = nullptr;
+  qldpc_osd_gpu* osd_owned = nullptr;  // the GPU OSD built from a host stage (qldpc_circ_set_final_osd)
   int D = 0, K = 0, M = 0, m = 0, n1 = 0, n2 = 0, rounds = 0, reps = 0;
   long long max_batch = 0;
   DevBuf mp, mr, k53, a_rp, a_ci, f_rp, f_ci;  // mechanism rows, thresholds, [Hs; L1], [h2; L2]
   DevBuf DO, acc, failw, synd1, corr1, synd2, corr2, bpcorr2, post2, iters, conv;
-  std::vector<uint8_t> h_synd, h_conv, h_bp, h_out;
-  std::vector<double> h_post;
 };
 
 namespace {
@@ -195,6 +194,8 @@ void stack_csr(const qldpc_graph* A, const qldpc_graph* B, std::vector<int32_t>&
 }
 
 void circ_release(qldpc_circ* c) {
+  if (c->osd_owned) qldpc_osd_gpu_destroy(c->osd_owned);
+  c->osd_owned = nullptr;
   for (DevBuf* b : {&c->mp, &c->mr, &c->k53, &c->a_rp, &c->a_ci, &c->f_rp, &c->f_ci, &c->DO, &c->acc, &c->failw,
                     &c->synd1, &c->corr1, &c->synd2, &c->corr2, &c->bpcorr2, &c->post2, &c->iters, &c->conv})
     b->release();
@@ -299,8 +300,16 @@ int qldpc_circ_set_final_osd(qldpc_circ* c, qldpc_osd_gpu* osd_gpu, const qldpc_
                         (rc = c->bpcorr2.alloc((size_t)c->max_batch * c->n2))))
       return rc;
   }
-  c->osd_gpu = osd_gpu;
-  c->osd_host = osd_host;
+  // a host stage runs on the GPU too (its method, order, rank and soft weights): the launch never
+  // leaves the device
+  qldpc_osd_gpu* own = nullptr;
+  if (osd_host) {
+    const int rc = osd_gpu_from_host(c->dec2->g, osd_host, &own);
+    if (rc) return rc;
+  }
+  if (c->osd_owned) qldpc_osd_gpu_destroy(c->osd_owned);
+  c->osd_owned = own;
+  c->osd_gpu = osd_gpu ? osd_gpu : own;
   return 0;
 }
 
@@ -402,30 +411,14 @@ int qldpc_circ_launch(qldpc_circ* c, uint64_t seed, uint64_t shot_begin, int64_t
     int rc;
     auto* synd2 = static_cast<const uint8_t*>(c->synd2.p);
     auto* corr2 = static_cast<uint8_t*>(c->corr2.p);
-    if (c->osd_gpu || c->osd_host) {  // bposd_decoder: BP, then OSD where BP did not converge
+    if (c->osd_gpu) {  // bposd_decoder: BP, then OSD where BP did not converge (GPU OSD, any priors)
       rc = qldpc_bp_decode_batch_soft(c->dec2, synd2, static_cast<uint8_t*>(c->bpcorr2.p),
                                       static_cast<int32_t*>(c->iters.p), static_cast<uint8_t*>(c->conv.p),
                                       static_cast<double*>(c->post2.p), B, stream);
-      if (!rc && c->osd_gpu) {
+      if (!rc)
         rc = qldpc_osd_gpu_decode(c->osd_gpu, synd2, static_cast<const double*>(c->post2.p),
                                   static_cast<const uint8_t*>(c->conv.p), static_cast<const uint8_t*>(c->bpcorr2.p),
                                   nullptr, corr2, B, stream);
-      } else if (!rc) {  // host OSD stage (non-uniform DEM priors)
-        const size_t nB = (size_t)B;
-        c->h_synd.resize(nB * m);
-        c->h_conv.resize(nB);
-        c->h_bp.resize(nB * c->n2);
-        c->h_out.resize(nB * c->n2);
-        c->h_post.resize(nB * c->n2);
-        QLDPC_HIP(hipMemcpyAsync(c->h_synd.data(), synd2, nB * m, hipMemcpyDeviceToHost, st));
-        QLDPC_HIP(hipMemcpyAsync(c->h_conv.data(), c->conv.p, nB, hipMemcpyDeviceToHost, st));
-        QLDPC_HIP(hipMemcpyAsync(c->h_bp.data(), c->bpcorr2.p, nB * c->n2, hipMemcpyDeviceToHost, st));
-        QLDPC_HIP(hipMemcpyAsync(c->h_post.data(), c->post2.p, nB * c->n2 * 8, hipMemcpyDeviceToHost, st));
-        QLDPC_HIP(hipStreamSynchronize(st));
-        rc = qldpc_osd_decode_batch(c->osd_host, c->h_synd.data(), c->h_post.data(), c->h_conv.data(), c->h_bp.data(),
-                                    nullptr, c->h_out.data(), B, 0);
-        if (!rc) QLDPC_HIP(hipMemcpyAsync(corr2, c->h_out.data(), nB * c->n2, hipMemcpyHostToDevice, st));
-      }
     } else {
       rc = qldpc_bp_decode_batch(c->dec2, synd2, corr2, static_cast<int32_t*>(c->iters.p),
                                  static_cast<uint8_t*>(c->conv.p), B, stream);

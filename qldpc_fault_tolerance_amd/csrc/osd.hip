@@ -330,8 +330,8 @@ int qldpc_osd_decode_batch(const qldpc_osd* osd, const uint8_t* synd, const doub
 }  // extern "C"
 
 // ===========================================================================
-// GPU OSD (uniform priors): one workgroup per syndrome, persistent over the
-// batch.  Same algorithm and outputs as the host stage above, laid out for the
+// GPU OSD: one workgroup per syndrome, persistent over the batch (uniform priors: popcount
+// weights; non-uniform: soft weights summed in column order, candidate step 6').  Same algorithm and outputs as the host stage above, laid out for the
 // GPU: the columns are bitonic-sorted in LDS by (posterior, index) — a stable
 // ascending order — and H is loaded with its columns permuted into that order,
 // word-major (word q of row i at q*m + i) in a per-workgroup HBM slice, so a
@@ -411,6 +411,7 @@ struct OsdGpuArgs {
   const uint8_t* conv;     // [B] or null
   const long long* shot;   // [B] or null: fused-loop capture slots, < 0 = BP converged (skipped)
   const uint8_t* bp_corr;  // [B][n] or null
+  const double* softw;     // [n] log(1 / p_j) for non-uniform priors, or null (uniform: popcount weights)
   uint8_t* out0;           // [B][n] or null
   uint8_t* outw;           // [B][n]
   u64* ws;                 // per workgroup: M [W][m] | X [(1 + nh)][RW]
@@ -509,7 +510,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   uint32_t* sb = used + (m + 31) / 32;                         // [ceil(m/32)] syndrome, reduced
   __shared__ int s_piv[3], s_npiv;  // s_piv triple-buffered by position: reset two columns ahead
   __shared__ uint32_t s_pivx;       // lean loop: (search step << 17) | (0x1FFFF - key), max over the waves
-  __shared__ u64 s_best;
+  __shared__ u64 s_best, s_bestw;
   u64* Mg = A.ws + (size_t)blockIdx.x * A.ws_words;
   u64* X = Mg + (size_t)W * m;  // X[0] = S0, X[1 + j] = x(h_j)
   // matrix: LDS when it fits (at offset 0, over the sort tables, which are copied to the
@@ -1343,18 +1344,19 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
     if (A.method == 1 && w > 0) L = 1ll << w;
     if (A.method == 2 && w >= 0) L = 1 + (long long)k + (long long)w * (w - 1) / 2;
     if (A.method == 0 || A.order == 0 || k == 0) L = 1;
-    u64 best = ~0ull;
-    for (long long c = tid; c < L; c += TB) {
-      int tj[2];
-      int nt = 0;
-      unsigned long long ebits = 0;
+    // candidate c -> its OSD input t: the bits of c (osd_e, natural binary order), or the weight-1
+    // then weight-2 inputs (osd_cs); tj[] = Ht indices
+    auto cand_input = [&](long long c, int* tj, unsigned long long& ebits) -> int {
+      ebits = 0;
       if (A.method == 1) {
         ebits = (unsigned long long)c;
-        nt = __popcll(ebits);
-      } else if (c >= 1 && c <= k) {
+        return __popcll(ebits);
+      }
+      if (c >= 1 && c <= k) {
         tj[0] = (int)(c - 1);
-        nt = 1;
-      } else if (c > k) {
+        return 1;
+      }
+      if (c > k) {
         long long rem = c - 1 - k;
         int i = 0;
         while (rem >= w - 1 - i) {
@@ -1363,8 +1365,79 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
         }
         tj[0] = i;
         tj[1] = i + 1 + (int)rem;
-        nt = 2;
+        return 2;
       }
+      return 0;
+    };
+    if (A.softw) {
+      // 6'. non-uniform priors (qldpc_osd_gpu_create with channel_probs that differ): the soft weight
+      // sum_{j: x_j = 1} log(1 / p_j), added in ascending COLUMN order as the host stage's
+      // soft_weight (and ldpc) adds it, so the candidates go to column space first: Xc[j] = X[j]
+      // with pivot index i moved to its column, one ballot per 64 columns (colpiv: column -> pivot
+      // index or -1); a candidate is then Xc[0] ^ (its Xc[1 + t]) | (its Ht columns), and its weight
+      // one ascending walk over the set bits.  Winner: the lexicographic minimum of (weight, c), i.e.
+      // the first strictly lightest candidate, as the uniform path.
+      int32_t* colpiv = gpos + n;            // [n]
+      u64* Xc = X + (size_t)(1 + nh) * RW;   // [(1 + nh)][W]
+      for (int j = tid; j < n; j += TB) colpiv[j] = -1;
+      __syncthreads();
+      for (int i = tid; i < r; i += TB) colpiv[sidxr[pivpos[i]]] = i;
+      __syncthreads();
+      for (int t = tid >> 6; t < (1 + nh) * W; t += TB >> 6) {  // uniform per wave
+        const int j = t / W, q = t % W;
+        const int col = q * 64 + (tid & 63);
+        bool bitv = false;
+        if (col < n) {
+          const int pi = colpiv[col];
+          if (pi >= 0) bitv = ((X[(size_t)j * RW + (pi >> 6)] >> (pi & 63)) & 1ull) != 0;
+        }
+        const unsigned long long v = __ballot(bitv);
+        if ((tid & 63) == 0) Xc[(size_t)j * W + q] = v;
+      }
+      if (tid == 0) s_bestw = ~0ull;
+      __syncthreads();
+      double bw = __builtin_huge_val();
+      long long bc = -1;
+      for (long long c = tid; c < L; c += TB) {
+        int tj[2];
+        unsigned long long ebits;
+        const int nt = cand_input(c, tj, ebits);
+        double sw = 0.0;
+        for (int q = 0; q < W; ++q) {
+          u64 v = Xc[q];
+          if (A.method == 1) {
+            for (unsigned long long e = ebits; e; e &= e - 1) {
+              const int t = __ffsll((long long)e) - 1;
+              v ^= Xc[(size_t)(1 + t) * W + q];
+              const int hc = sidxr[swp[r + t]];
+              if ((hc >> 6) == q) v |= 1ull << (hc & 63);
+            }
+          } else {
+            for (int a = 0; a < nt; ++a) {
+              v ^= Xc[(size_t)(1 + tj[a]) * W + q];
+              const int hc = sidxr[swp[r + tj[a]]];
+              if ((hc >> 6) == q) v |= 1ull << (hc & 63);
+            }
+          }
+          for (; v; v &= v - 1) sw += A.softw[q * 64 + __ffsll((long long)v) - 1];
+        }
+        if (sw < bw) {  // c ascends per thread: the first of equal weights stays
+          bw = sw;
+          bc = c;
+        }
+      }
+      // non-negative doubles order as their bit patterns
+      const u64 wb = bc >= 0 ? (u64)__double_as_longlong(bw) : ~0ull;
+      if (bc >= 0) atomicMin(&s_bestw, wb);
+      __syncthreads();
+      if (bc >= 0 && wb == s_bestw) atomicMin(&s_best, (u64)bc);
+      __syncthreads();
+    } else {
+    u64 best = ~0ull;
+    for (long long c = tid; c < L; c += TB) {
+      int tj[2];
+      unsigned long long ebits;
+      const int nt = cand_input(c, tj, ebits);
       long long cnt = nt;
       for (int q = 0; q < RWr; ++q) {
         u64 v = X[q];
@@ -1380,6 +1453,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
     }
     if (best != ~0ull) atomicMin(&s_best, best);
     __syncthreads();
+    }
     OSD_ST(4)
     // 7. outputs
     const long long cw = (long long)(s_best & ((1ull << 40) - 1));
@@ -1821,7 +1895,7 @@ struct qldpc_osd_gpu {
   int nsy = 1, syn_lds = 0;  // register-row mode: syndromes per workgroup (osd_rr2_kernel), LDS per syndrome
   size_t lds = 0;
   long long ws_words = 0, iws_ints = 0;
-  qldpc_rt::DevBuf rp, ci, ws, iws;
+  qldpc_rt::DevBuf rp, ci, ws, iws, softw;  // softw: [n] log(1 / p_j) when the priors are not uniform
 };
 
 namespace {
@@ -1963,17 +2037,25 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   int rc = qldpc_osd_create(g->m, g->n, g->row_ptr.data(), g->col_idx.data(), channel_probs, osd_method, osd_order,
                             &O);
   if (rc) return rc;
-  if (!O->uniform) {
-    qldpc_osd_destroy(O);
-    return set_err(QLDPC_ENOTSUP, "GPU OSD needs uniform channel_probs (use the host stage, qldpc_osd_*)");
-  }
-  if (g->n > kOsdMaxN || (osd_method == 1 && osd_order > 24)) {
-    qldpc_osd_destroy(O);
+  rc = qldpc_rt::osd_gpu_from_host(g, O, out);
+  qldpc_osd_destroy(O);
+  return rc;
+}
+
+}  // extern "C"
+
+// The GPU OSD of a host OSD stage built on graph g (same method, order, rank and soft weights
+// log(1 / p_j), copied: no re-derivation from probabilities).  qldpc_osd_gpu_create and the circuit
+// loop (a host stage handed to qldpc_circ_set_final_osd runs on the GPU) both build through here.
+int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_osd_gpu** out) {
+  if (!g || !O || !out) return set_err(QLDPC_EINVAL, "NULL argument");
+  if (!osd_host_matches(O, g)) return set_err(QLDPC_EINVAL, "host OSD stage was built on a different graph");
+  const int osd_method = O->method, osd_order = O->order;
+  int rc = 0;
+  if (g->n > kOsdMaxN || (osd_method == 1 && osd_order > 24))
     return set_err(QLDPC_ENOTSUP, "GPU OSD: n > 8192 or osd_e order > 24");
-  }
   auto* G = new qldpc_osd_gpu();
   G->host = *O;
-  qldpc_osd_destroy(O);
   G->device = g->device;
   const int m = g->m, n = g->n, rank = G->host.rank, k = n - rank;
   const int w = std::min(G->host.order, k);
@@ -2025,15 +2107,18 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   // two syndromes per workgroup (osd_rr2_kernel, the 768-thread register-row kernels): a second LDS
   // area and HBM slice per workgroup; QLDPC_OSD_NSY=1 keeps one
   const char* nsy_env = std::getenv("QLDPC_OSD_NSY");
-  if (G->wr >= 20 && !G->pnl && !QLDPC_OSD_1B && (nsy_env ? std::atoi(nsy_env) : 1) == 2 && osd_rr2_kernel_of(G->wr)) {
+  if (G->wr >= 20 && !G->pnl && !QLDPC_OSD_1B && G->host.uniform && (nsy_env ? std::atoi(nsy_env) : 1) == 2 && osd_rr2_kernel_of(G->wr)) {
     G->nsy = 2;
     G->syn_lds = (int)((G->lds + 15) & ~(size_t)15);
     G->lds = 2 * (size_t)G->syn_lds;
   }
-  G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW;
-  G->iws_ints = 2ll * rank + 3ll * n;
+  // non-uniform priors: the candidates' column-space vectors Xc [(1 + nh)][W] after X, and the
+  // column -> pivot map [n] after the sort maps
+  G->ws_words = (long long)G->W * m + (long long)(1 + G->nh) * G->RW +
+                (G->host.uniform ? 0ll : (long long)(1 + G->nh) * G->W);
+  G->iws_ints = 2ll * rank + 4ll * n;
   auto fail = [&](int code) {
-    G->rp.release(); G->ci.release(); G->ws.release(); G->iws.release();
+    G->rp.release(); G->ci.release(); G->ws.release(); G->iws.release(); G->softw.release();
     delete G;
     return code;
   };
@@ -2054,8 +2139,11 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   const size_t E = g->col_idx.size();
   if ((rc = G->rp.alloc((size_t)(m + 1) * 4)) || (rc = G->ci.alloc(std::max<size_t>(E, 1) * 4)) ||
       (rc = G->ws.alloc((size_t)G->grid * G->nsy * G->ws_words * 8)) ||
-      (rc = G->iws.alloc((size_t)G->grid * G->nsy * G->iws_ints * 4)))
+      (rc = G->iws.alloc((size_t)G->grid * G->nsy * G->iws_ints * 4)) ||
+      (!G->host.uniform && (rc = G->softw.alloc((size_t)n * 8))))
     return fail(rc);
+  if (!G->host.uniform && hipMemcpy(G->softw.p, G->host.w.data(), (size_t)n * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(set_err(QLDPC_EHIP, "upload OSD soft weights"));
   if (hipMemcpy(G->rp.p, g->row_ptr.data(), (size_t)(m + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
       (E && hipMemcpy(G->ci.p, g->col_idx.data(), E * 4, hipMemcpyHostToDevice) != hipSuccess))
     return fail(set_err(QLDPC_EHIP, "upload OSD graph"));
@@ -2063,9 +2151,11 @@ int qldpc_osd_gpu_create(const qldpc_graph* g, const double* channel_probs, int3
   return 0;
 }
 
+extern "C" {
+
 int qldpc_osd_gpu_destroy(qldpc_osd_gpu* osd) {
   if (!osd) return 0;
-  osd->rp.release(); osd->ci.release(); osd->ws.release(); osd->iws.release();
+  osd->rp.release(); osd->ci.release(); osd->ws.release(); osd->iws.release(); osd->softw.release();
   delete osd;
   return 0;
 }
@@ -2095,6 +2185,7 @@ int osd_gpu_decode_slots(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double
   a.rp = static_cast<const int32_t*>(osd->rp.p);
   a.ci = static_cast<const int32_t*>(osd->ci.p);
   a.synd = d_synd; a.post = d_post; a.conv = d_conv; a.shot = d_shot; a.bp_corr = d_bp_corr; a.out0 = d_out0;
+  a.softw = osd->host.uniform ? nullptr : static_cast<const double*>(osd->softw.p);
   a.outw = d_outw;
   a.ws = static_cast<u64*>(osd->ws.p);
   a.iws = static_cast<int32_t*>(osd->iws.p);

@@ -138,6 +138,8 @@ int ps_decode_launch(const qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int
 bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g);
 // host OSD stage built on this graph? (osd.hip; qldpc_circ_set_final_osd checks it)
 bool osd_host_matches(const qldpc_osd* o, const qldpc_graph* g);
+// GPU OSD handle from a host OSD stage on graph g: same method / order / rank / soft weights (osd.hip)
+int osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* host, qldpc_osd_gpu** out);
 // BP+OSD stage of the fused shot loop, one sector (osd.hip)
 int osd_gpu_bposd_stage(qldpc_osd_gpu* osd, const uint8_t* synd, const double* post, const uint8_t* err,
                         const long long* shot, uint8_t* outw, long long ncand, const unsigned long long* lmask, int kw,

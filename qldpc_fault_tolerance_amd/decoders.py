@@ -118,7 +118,8 @@ class BPOSD_Decoder:
         self.decoder = DeviceBP(H, self.channel_probs, max_iter=_int_max_iter(max_iter, H.n), bp_method=bp_method,
                                 ms_scaling_factor=ms_scaling_factor, precision=precision, device=device, soft=True)
         self.osd = HostOSD(H, self.channel_probs, osd_method=osd_method, osd_order=osd_order)
-        # OSD on the GPU for uniform priors (every reference call site); the host stage otherwise
+        # OSD on the GPU (uniform priors: popcount weights; non-uniform: soft weights); the host stage
+        # stays for use_gpu_osd=False and graphs past the GPU kernel's envelope
         self.gpu_osd = (DeviceOSD(self.decoder.graph, self.channel_probs, osd_method, osd_order)
                         if use_gpu_osd and DeviceOSD.supported(H.n, self.channel_probs, osd_method, osd_order)
                         else None)
@@ -311,7 +312,8 @@ class ST_BP_Decoder_Circuit(BPDecoder):
 class ST_BPOSD_Decoder_Circuit(BPOSD_Decoder):
     """``ST_BPOSD_Decoder_Circuit(h, channel_probs, max_iter, bp_method, ms_scaling_factor, osd_method,
     osd_order)`` (``src/Decoders_SpaceTime.py:277-292``): ``bposd_decoder`` on h2; ``decode`` returns
-    ``osdw_decoding``.  DEM priors are non-uniform, so the OSD half runs on the host stage."""
+    ``osdw_decoding``.  DEM priors are non-uniform: the GPU OSD weighs its candidates by
+    sum log(1/p_j) (the host stage's order relation, summed in the same column order)."""
 
 
 class ST_BP_Decoder_Circuit_Class(DecoderClass):

@@ -263,8 +263,9 @@ class HostOSD:
 
 class DeviceOSD:
     """OSD on the GPU (``qldpc_osd_gpu_*``): one workgroup per non-converged syndrome, fed
-    straight from the soft-output BP's device buffers.  Uniform priors only (every
-    reference call site); ``supported`` says whether a graph / prior vector qualifies."""
+    straight from the soft-output BP's device buffers.  Uniform priors weigh candidates by
+    popcount; non-uniform ones (the circuit-level DEM priors) by sum log(1/p_j) in column order,
+    as the host stage.  ``supported`` says whether a graph qualifies (n <= 8192, osd_e order <= 24)."""
 
     MAX_N = 8192
 
@@ -273,7 +274,8 @@ class DeviceOSD:
         p = np.broadcast_to(np.asarray(channel_probs, dtype=np.float64), (n,))
         key = str(osd_method).lower() if not isinstance(osd_method, (int, np.integer)) else None
         meth = OSD_METHODS.get(key, -1) if key is not None else int(osd_method)
-        return n <= DeviceOSD.MAX_N and bool(np.all(p == p[0])) and not (meth == 1 and int(osd_order) > 24)
+        return (n <= DeviceOSD.MAX_N and bool(np.all((p > 0) & (p < 1))) and meth in (0, 1, 2)
+                and not (meth == 1 and int(osd_order) > 24))
 
     def __init__(self, graph: DeviceGraph, channel_probs, osd_method="osd_e", osd_order=10):
         self.graph = graph

@@ -692,7 +692,7 @@ class CodeSimulator_Circuit_SpaceTime:
 
     def __init__(self, code=None, decoder1_z=None, decoder1_x=None, decoder2_z=None, decoder2_x=None, p=0,
                  num_cycles=1, num_rep=1, error_params=None, eval_logical_type="Z", circuit_type="coloration",
-                 rand_scheduling_seed=0, seed=None, max_batch=0):
+                 rand_scheduling_seed=0, seed=None, max_batch=0, compat_dem_text=False):
         import copy as _copy
 
         from . import circuit as _circ
@@ -740,6 +740,10 @@ class CodeSimulator_Circuit_SpaceTime:
         self._dev = None
         self._dev_key = None
         self.last_result = None
+        # True: the hypergraphs are built from the fault DEM rendered as stim's text and parsed with the
+        # reference's regex (circuit.DetectorErrorModel.from_text): stim's mechanism order, 6-digit
+        # probabilities, and mantissa-only reads of probabilities printed in exponent notation
+        self.compat_dem_text = bool(compat_dem_text)
 
     # -- circuits and hypergraphs ---------------------------------------------------
     def _generate_circuit(self):
@@ -753,18 +757,21 @@ class CodeSimulator_Circuit_SpaceTime:
             self.scheduling_Z)
         self.dem = self.circuit.detector_error_model(flatten_loops=True)
         self.detector_sampler = _DetectorSampler(self)
+        self._dev, self._dev_key = None, None  # a cached device loop holds the previous DEM
 
     def _generate_circuit_graph(self):
         """``:942-966``."""
         from . import circuit as _circ
 
         self.fault_dem = self.fault_circuit.detector_error_model(flatten_loops=True)
-        H_list, L_list, P_list = _circ.GenFaultHyperGraph(self.fault_dem, num_rounds=self.num_rounds,
+        src = self.fault_dem.to_text("stim") if self.compat_dem_text else self.fault_dem
+        H_list, L_list, P_list = _circ.GenFaultHyperGraph(src, num_rounds=self.num_rounds,
                                                            num_rep=self.num_rep, num_logicals=self.num_logicals)
         self.circuit_graph = {"h1": H_list[0], "L1": L_list[0], "channel_ps1": P_list[0],
                               "h2": H_list[-1], "L2": L_list[-1], "channel_ps2": P_list[-1]}
-        self.h1_space_cor = _circ.GenCorrecHyperGraph(self.fault_dem, num_rounds=self.num_rounds, num_rep=self.num_rep,
+        self.h1_space_cor = _circ.GenCorrecHyperGraph(src, num_rounds=self.num_rounds, num_rep=self.num_rep,
                                                       num_checks=self.num_checks, num_logicals=self.num_logicals)
+        self._dev, self._dev_key = None, None  # new graphs: rebuild the device loop
 
     # -- reference per-sample path (plugin decoders) -------------------------------
     def _decoding_samples(self, samples):

@@ -7,6 +7,7 @@ Run in the build container only (``/root/reference`` is not on the GPU box):
     python tests/golden/make_golden.py configs  # reference_harness_configs.npz (configs 2-5)
     python tests/golden/make_golden.py fits     # reference_fits.npz (threshold tooling)
     python tests/golden/make_golden.py schedules  # reference_circuit_schedules.npz (CX schedules)
+    python tests/golden/make_golden.py circuit    # reference_circuit.npz (circuit op lists + fault hypergraphs)
 
 The reference modules import third-party packages that are absent here
 (``graph_tools``, ``ldpc``, ``bposd``, ``stim``, …), so empty stub
@@ -552,8 +553,184 @@ def main_schedules():
     print("wrote", path)
 
 
+class _RecTarget:
+    """``stim.target_rec(k)``."""
+
+    def __init__(self, k):
+        self.k = int(k)
+
+
+# gates that never fuse with a neighbour in stim (annotations); every other gate fuses with an
+# immediately preceding instruction of the same gate and arguments (stim's append / parse / +=)
+_STIM_NOFUSE = {"DETECTOR", "OBSERVABLE_INCLUDE", "SHIFT_COORDS", "TICK"}
+_DEM_STYLE = ["exact"]
+
+
+class RecordingCircuit:
+    """A recording stand-in for ``stim.Circuit`` (stim is absent): it keeps the instructions the
+    reference's ``_generate_circuit`` appends (gate, targets, arguments; consecutive same-gate
+    same-argument instructions fused, as stim does), renders them as stim circuit text for
+    ``AddCXError`` (``src/ErrorPlugin.py:11-25``, which rewrites ``str(circuit)``) and parses that
+    text back.  ``detector_error_model`` is the ONE place the engine enters: the recorded op list is
+    handed to ``qldpc_fault_tolerance_amd.circuit.detector_error_model`` and rendered as DEM text
+    (``_DEM_STYLE``), which the reference's own ``GenFaultHyperGraph`` / ``GenCorrecHyperGraph`` then
+    parse unchanged."""
+
+    def __init__(self, text=None):
+        self.ops = []  # [name, targets (int qubit | _RecTarget), args tuple]
+        if text is not None:
+            for line in str(text).split("\n"):
+                line = line.strip()
+                if not line or line in ("{", "}"):
+                    continue
+                head, _, rest = line.partition(" ")
+                if "(" in head:
+                    name = head[:head.index("(")]
+                    args = tuple(float(a) for a in head[head.index("(") + 1:head.rindex(")")].split(","))
+                else:
+                    name, args = head, ()
+                tg = [(_RecTarget(int(t[4:-1])) if t.startswith("rec[") else int(t)) for t in rest.split()]
+                self._push(name, tg, args)
+
+    def _push(self, name, targets, args):
+        name = name.upper()
+        last = self.ops[-1] if self.ops else None
+        if last is not None and name not in _STIM_NOFUSE and last[0] == name and last[2] == args:
+            last[1].extend(targets)
+        else:
+            self.ops.append([name, list(targets), args])
+
+    def append(self, name, targets=(), arg=None):
+        if arg is None:
+            args = ()
+        elif isinstance(arg, (list, tuple)):
+            args = tuple(float(a) for a in arg)
+        else:
+            args = (float(arg),)
+        tg = [t if isinstance(t, _RecTarget) else int(t) for t in (targets if len(targets) else [])]
+        self._push(name, tg, args)
+
+    def __add__(self, other):
+        c = RecordingCircuit()
+        for o in self.ops + other.ops:
+            c._push(o[0], list(o[1]), o[2])
+        return c
+
+    def __mul__(self, k):
+        c = RecordingCircuit()
+        for _ in range(int(k)):
+            for o in self.ops:
+                c.ops.append([o[0], list(o[1]), o[2]])  # flattened REPEAT: no fusion across copies
+        return c
+
+    __rmul__ = __mul__
+
+    def __str__(self):
+        lines = []
+        for name, tg, args in self.ops:
+            a = "(" + ", ".join(repr(x) for x in args) + ")" if args else ""
+            t = " ".join(f"rec[{x.k}]" if isinstance(x, _RecTarget) else str(x) for x in tg)
+            lines.append(f"{name}{a} {t}".rstrip())
+        return "\n".join(lines) + "\n"
+
+    def engine_circuit(self):
+        from qldpc_fault_tolerance_amd import circuit as C
+
+        return C.StimCircuit([C.Op(n, [(x.k if isinstance(x, _RecTarget) else x) for x in tg],
+                                   (args[0] if args else None)) for n, tg, args in self.ops])
+
+    def detector_error_model(self, flatten_loops=True):
+        text = self.engine_circuit().detector_error_model().to_text(_DEM_STYLE[0])
+
+        class _Dem:
+            def __str__(self):
+                return text
+
+        return _Dem()
+
+    def compile_detector_sampler(self):
+        return None
+
+
+def circuit_cases():
+    """(tag, code, p, error_params, num_cycles, num_rep, circuit_type) of the circuit fixtures: the
+    demo (SpaceTimeDecodingDemo.ipynb cell 2), every noise source at the GPU tests' rate with both
+    schedules, distinct rates per source, and a low rate whose mechanisms stim prints in exponent
+    notation (the reference's regex reads their mantissas)."""
+    def ring(d):
+        h = np.zeros((d, d), np.uint8)
+        for i in range(d):
+            h[i, i] = h[i, (i + 1) % d] = 1
+        return h
+
+    tor = codes.hgp(ring(3), ring(3))
+    allp = lambda p: {"p_i": p, "p_state_p": p, "p_m": p, "p_CX": p, "p_idling_gate": p}  # noqa: E731
+    return [
+        ("demo", tor, 1e-3, {"p_i": 0.0, "p_state_p": 0.0, "p_m": 0.0, "p_CX": 1e-3, "p_idling_gate": 0.0}, 13, 3,
+         "coloration"),
+        ("all3c", tor, 3e-3, allp(3e-3), 13, 3, "coloration"),
+        ("all3r", tor, 3e-3, allp(3e-3), 13, 3, "random"),
+        ("mixed", tor, 6e-3, {"p_i": 2e-3, "p_state_p": 3e-3, "p_m": 4e-3, "p_CX": 5e-3, "p_idling_gate": 1e-3}, 5, 2,
+         "random"),
+        ("low", tor, 5e-5, allp(5e-5), 7, 3, "coloration"),
+    ]
+
+
+def _pack_ops(ops):
+    names = np.array([o[0] for o in ops], dtype="<U20")
+    args = np.array([(o[2][0] if o[2] else np.nan) for o in ops], dtype=np.float64)
+    offs = np.cumsum([0] + [len(o[1]) for o in ops]).astype(np.int64)
+    tg = np.array([(x.k if isinstance(x, _RecTarget) else x) for o in ops for x in o[1]], dtype=np.int64)
+    return names, args, offs, tg
+
+
+def main_circuit():
+    """Circuit-level fixtures from the reference's own ``CodeSimulator_Circuit_SpaceTime``
+    (``src/Simulators_SpaceTime.py:672-967``) -> tests/golden/reference_circuit.npz.
+
+    With the stubs of :func:`install_stubs` plus :class:`RecordingCircuit` as ``stim.Circuit``, the
+    reference's ``_generate_circuit`` (:737-940) and ``AddCXError`` run unchanged; the recorded op
+    lists of ``circuit`` / ``fault_circuit`` are stored.  Its ``_generate_circuit_graph`` (:943-967)
+    then runs unchanged on the engine's DEM of the recorded fault circuit, rendered as DEM text twice:
+    ``exact`` (the engine's mechanism order, round-trip probabilities) and ``stim`` (stim's order and
+    6-significant-digit ``%g`` probabilities, which its regex parse reads back).  Stored: h1, L1,
+    channel_ps1, h2, L2, channel_ps2, h1_space_cor of both."""
+    install_stubs()
+    stim = sys.modules["stim"]
+    stim.Circuit = RecordingCircuit
+    stim.target_rec = _RecTarget
+    import Simulators_SpaceTime as SST
+
+    out = {}
+    for tag, code, p, ep, ncyc, nrep, ctype in circuit_cases():
+        sim = SST.CodeSimulator_Circuit_SpaceTime(code=code, p=p, num_cycles=ncyc, num_rep=nrep, error_params=dict(ep),
+                                                  eval_logical_type="Z", circuit_type=ctype)
+        sim._generate_circuit()
+        for which, circ in (("circuit", sim.circuit), ("fault", sim.fault_circuit)):
+            names, args, offs, tg = _pack_ops(circ.ops)
+            out[f"{tag}_{which}_names"], out[f"{tag}_{which}_args"] = names, args
+            out[f"{tag}_{which}_offs"], out[f"{tag}_{which}_targets"] = offs, tg
+        for style in ("exact", "stim"):
+            _DEM_STYLE[0] = style
+            sim._generate_circuit_graph()
+            g = sim.circuit_graph
+            for k in ("h1", "L1", "h2", "L2"):
+                out[f"{tag}_{style}_{k}"] = np.asarray(g[k], dtype=np.uint8)
+            for k in ("channel_ps1", "channel_ps2"):
+                out[f"{tag}_{style}_{k}"] = np.asarray(g[k], dtype=np.float64)
+            out[f"{tag}_{style}_h1_space_cor"] = np.asarray(sim.h1_space_cor, dtype=np.uint8)
+        out[f"{tag}_params"] = np.array([p, ep["p_i"], ep["p_state_p"], ep["p_m"], ep["p_CX"], ep["p_idling_gate"], ncyc,
+                                         nrep, ctype == "random"], dtype=np.float64)
+        print(tag, "h1", out[f"{tag}_exact_h1"].shape, "h2", out[f"{tag}_exact_h2"].shape, flush=True)
+    path = os.path.join(HERE, "reference_circuit.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, len(out), "arrays")
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "schedules":
+    if len(sys.argv) > 1 and sys.argv[1] == "circuit":
+        main_circuit()
+    elif len(sys.argv) > 1 and sys.argv[1] == "schedules":
         main_schedules()
     elif len(sys.argv) > 1 and sys.argv[1] == "notebook":
         main_notebook()

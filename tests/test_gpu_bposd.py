@@ -170,7 +170,63 @@ def test_gpu_osd_matches_host_osd(gpu, monkeypatch, name, t0, method, order, mod
     assert np.array_equal(o0, h0)
     assert np.array_equal(ow, hw)
     assert np.array_equal((H.astype(np.int64) @ ow.T.astype(np.int64) % 2).T, synd)
-    assert DeviceOSD.supported(n, p, method, order) and not DeviceOSD.supported(n, np.linspace(.01, .1, n), method, 1)
+    assert DeviceOSD.supported(n, p, method, order) and DeviceOSD.supported(n, np.linspace(.01, .1, n), method, 1)
+
+
+@pytest.mark.parametrize("name,method,order,mode", [
+    ("hgp_34_n225", "osd_e", 10, "default"), ("hgp_34_n225", "osd_cs", 8, "default"), ("hgp_34_n225", "osd_0", 0, "default"),
+    ("hgp_34_n1600", "osd_e", 10, "default"), ("hgp_34_n225", "osd_e", 10, "lds"), ("hgp_34_n225", "osd_e", 8, "hbm"),
+    ("circuit_h2_all3c", "osd_e", 10, "default"), ("circuit_h2_demo", "osd_e", 10, "default"),
+    ("circuit_h1_all3r", "osd_cs", 6, "default")])
+def test_gpu_osd_nonuniform_priors_matches_oracle(gpu, oracle, monkeypatch, name, method, order, mode):
+    """GPU OSD with NON-uniform channel_probs (the circuit-level final round
+    ST_BPOSD_Decoder_Circuit(h2, channel_ps2, ...), src/Decoders_SpaceTime.py:277-292): candidates
+    weighed by sum log(1/p_j) in ascending column order (osd.hip step 6') == the oracle's literal OSD
+    (oracle.osd_decode: Neal LU, per-candidate solve, soft weight summed in index order) and the
+    native host stage, per syndrome.  Graphs: codes with drawn priors, and the reference-generated
+    circuit hypergraphs with their DEM priors (tests/golden/reference_circuit.npz)."""
+    from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceOSD, HostOSD
+
+    for k, v in _OSD_MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    if name.startswith("circuit_"):
+        import os
+
+        _, h, tag = name.split("_")
+        z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_circuit.npz"))
+        H = z[f"{tag}_exact_{h}"].astype(np.uint8)
+        probs = z[f"{tag}_exact_channel_ps{h[1]}"].astype(np.float64)
+        # circuit-level rates are tiny; scale the error draw up so BP leaves non-converged syndromes
+        rng = np.random.default_rng(order + len(name))
+        e = (rng.random((256, H.shape[1])) < np.minimum(0.25, 40 * probs)).astype(np.uint8)
+        synd = (e.astype(np.int64) @ H.T.astype(np.int64) % 2).astype(np.uint8)
+        mi = 2
+    else:
+        code = codes.get_code(name)
+        H = code.hz
+        n = H.shape[1]
+        rng = np.random.default_rng(11 + order)
+        probs = rng.uniform(0.02, 0.12, n)
+        probs[::7] = probs[3]  # some equal priors: tied soft weights occur
+        synd, _ = _sample(H, 0.08 if n < 1000 else 0.055, 192, seed=order + 5)
+        mi = int(n / 10)
+    n = H.shape[1]
+    assert DeviceOSD.supported(n, probs, method, order)
+    bp = DeviceBP(H, probs, max_iter=mi, ms_scaling_factor=0.625, precision=64, soft=True)
+    osd = DeviceOSD(bp.graph, probs, method, order)
+    ow, o0, corr, iters, conv, post = osd.bposd_batch(bp, synd)
+    assert (~conv).sum() > 0
+    h0, hw = HostOSD(H, probs, method, order).decode_batch(synd, post, conv, corr)
+    assert np.array_equal(o0, h0) and np.array_equal(ow, hw)
+    idx = np.flatnonzero(~conv)[:48]
+    if n < 1000:  # the literal numpy restatement
+        for b in idx:
+            r0, rw = oracle.osd_decode(H, probs, synd[b], post[b], method, order)
+            assert np.array_equal(ow[b], rw) and np.array_equal(o0[b], r0), b
+    else:  # its C restatement (the same algorithm step for step), fast enough for n1600
+        r0, rw = oracle.osd_decode_batch(H, probs, synd[idx], post[idx], method, order)
+        assert np.array_equal(ow[idx], rw) and np.array_equal(o0[idx], r0)
+    assert np.array_equal((H.astype(np.int64) @ ow.T.astype(np.int64) % 2).T, synd)
 
 
 def test_bposd_decoder_host_and_gpu_osd_agree(gpu):
@@ -180,6 +236,11 @@ def test_bposd_decoder_host_and_gpu_osd_agree(gpu):
     synd, _ = _sample(code.hx, 0.1, 128, seed=3)
     a = BPOSD_Decoder(code.hx, 0.1 * np.ones(code.N), 22, "minimum_sum", 0.625, "osd_e", 10)
     b = BPOSD_Decoder(code.hx, 0.1 * np.ones(code.N), 22, "minimum_sum", 0.625, "osd_e", 10, use_gpu_osd=False)
+    assert a.gpu_osd is not None and b.gpu_osd is None
+    assert np.array_equal(a.decode_batch(synd), b.decode_batch(synd))
+    pr = np.random.default_rng(5).uniform(0.03, 0.15, code.N)  # non-uniform priors: the GPU OSD too
+    a = BPOSD_Decoder(code.hx, pr, 22, "minimum_sum", 0.625, "osd_e", 10)
+    b = BPOSD_Decoder(code.hx, pr, 22, "minimum_sum", 0.625, "osd_e", 10, use_gpu_osd=False)
     assert a.gpu_osd is not None and b.gpu_osd is None
     assert np.array_equal(a.decode_batch(synd), b.decode_batch(synd))
 

@@ -3,9 +3,11 @@
 * The DEM sampler (``qldpc_circ_sample``) == the oracle's Philox draws of every mechanism, and the
   detector / observable bits the fused launch decodes are the same draws.
 * The fused shot loop (``qldpc_circ_launch``: rounds of decoder1 on h1, space / logical
-  corrections, decoder2 BP+OSD on h2 through the host OSD stage, failure check) == the oracle's
-  restatement of ``CodeSimulator_Circuit_SpaceTime._decoding_samples`` per sample
-  (``oracle/circuit_oracle.py``), bit for bit.
+  corrections, decoder2 BP+OSD on h2, failure check) == the oracle's restatement of
+  ``CodeSimulator_Circuit_SpaceTime._decoding_samples`` per sample (``oracle/circuit_oracle.py``), bit
+  for bit, with decoders and oracle built from the REFERENCE-generated hypergraphs
+  (``tests/golden/reference_circuit.npz``: the reference's own ``_generate_circuit_graph`` on this
+  engine's DEM text).
 * The reference's per-sample plugin path (``_decoding_samples`` with foreign decoders) == the fused
   path on the same samples.
 * The demo (``SpaceTimeDecodingDemo.ipynb`` cells 2-3: d3 toric, p = 1e-3, CX noise only,
@@ -14,6 +16,7 @@
   only stim-era output the reference holds; everything else here is parity-unpinned against stim.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -30,7 +33,24 @@ def _ring(d):
     return h
 
 
-def _sim(p, ep_scale, num_cycles=13, num_rep=3, osd=True, max_iter_ratio=10, circuit_type="coloration", seed=7):
+REF_CIRCUIT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_circuit.npz")
+
+
+def _reference_graphs(tag):
+    """The reference's own fault hypergraphs (tests/golden/reference_circuit.npz, made by running
+    src/Simulators_SpaceTime.py:943-967 unchanged on this engine's DEM text; make_golden.py circuit)."""
+    z = np.load(REF_CIRCUIT)
+    g = {k: z[f"{tag}_exact_{k}"].astype(np.float64) for k in ("h1", "L1", "h2", "L2")}
+    g["channel_ps1"] = list(z[f"{tag}_exact_channel_ps1"])
+    g["channel_ps2"] = list(z[f"{tag}_exact_channel_ps2"])
+    return g, z[f"{tag}_exact_h1_space_cor"].astype(np.float64)
+
+
+def _sim(p, ep_scale, num_cycles=13, num_rep=3, osd=True, max_iter_ratio=10, circuit_type="coloration", seed=7,
+         ref_tag=None):
+    """The simulator with its decoders; with ``ref_tag`` the hypergraphs, channel probabilities and
+    space-correction matrix are the REFERENCE-generated fixture's (after checking the engine's own
+    equal them), so the decoders and the oracle below are built from the reference's graphs."""
     from qldpc_fault_tolerance_amd.decoders import ST_BP_Decoder_Circuit, ST_BPOSD_Decoder_Circuit
     from qldpc_fault_tolerance_amd.simulators import CodeSimulator_Circuit_SpaceTime
 
@@ -40,6 +60,12 @@ def _sim(p, ep_scale, num_cycles=13, num_rep=3, osd=True, max_iter_ratio=10, cir
                                           eval_logical_type="Z", circuit_type=circuit_type, seed=seed)
     sim._generate_circuit()
     sim._generate_circuit_graph()
+    if ref_tag is not None:
+        g_ref, cor_ref = _reference_graphs(ref_tag)
+        for k in ("h1", "L1", "h2", "L2"):
+            assert np.array_equal(np.asarray(sim.circuit_graph[k]), g_ref[k]), k
+        assert np.array_equal(np.asarray(sim.h1_space_cor), cor_ref)
+        sim.circuit_graph, sim.h1_space_cor = g_ref, cor_ref
     g = sim.circuit_graph
     mi = int(code.N / max_iter_ratio)
     sim.decoder1_z = ST_BP_Decoder_Circuit(g["h1"], g["channel_ps1"], mi, "minimum_sum", 0.625)
@@ -70,7 +96,8 @@ def test_dem_sampler_matches_oracle_draws(gpu):
 def test_fused_circuit_loop_matches_oracle_per_sample(gpu, osd, ratio, ctype):
     import circuit_oracle
 
-    sim, mi = _sim(3e-3, ALL_NOISE, osd=osd, max_iter_ratio=ratio, circuit_type=ctype)
+    sim, mi = _sim(3e-3, ALL_NOISE, osd=osd, max_iter_ratio=ratio, circuit_type=ctype,
+                   ref_tag="all3c" if ctype == "coloration" else "all3r")
     g = sim.circuit_graph
     dev = sim._device()
     S, b0 = 1500, 4242
@@ -116,18 +143,26 @@ def test_plugin_path_equals_fused_path(gpu):
 def test_demo_wer_against_printed(gpu):
     """SpaceTimeDecodingDemo.ipynb cell 3: WordErrorRate(10000) = 0.00019299501269032238, i.e. 50
     failures in 10,000 samples (inverted through the per-cycle WER formula, K = 2, 13 cycles; the
-    inversion is exact).  Measured (round 4, 2e6 samples): the engine fails 0.00794 of the samples,
-    79.4 per 10,000; the printed 50 lies below the central 99.9 % band [52, 110] of Binomial(10000,
-    0.00794) (one-sided p ~ 5e-4).  DOCUMENTED DISCREPANCY, unresolved: the CPU
-    oracle of the same model agrees with the engine per sample, the DEM column order does not change
-    a single outcome (OSD ties), every mechanism probability is >= 5.3e-4 (so the reference's
-    ``\d+\.\d+`` parse of stim's text cannot have mangled one), and the CX schedules are the
-    reference's own.  What remains unpinnable here is stim itself and ldpc / bposd.  This test
-    guards the engine's rate (regression band: 5 sigma of the 2e6-sample estimate) and reports the
-    printed value's position."""
+    inversion is exact).  The engine (2e6 samples, the demo's circuit, decoders and parameters) fails
+    0.00794 of the samples (round 4: 79.4 per 10,000).
+
+    This is NOT a parity test, for two recorded reasons:
+    * provenance: the WER cell ran at ``In [47]``, BEFORE its setup cell (cell 2, ``In [48]``); the
+      printed number came from a simulator an earlier execution of cell 2 built, whose parameters the
+      notebook does not show;
+    * sampling: the reference draws every sample from ONE stim detector sampler compiled in
+      ``_generate_circuit`` and fans ``_single_run`` out through ``parmap`` over ``mp.cpu_count()``
+      forked workers (src/Simulators_SpaceTime.py:940, :1036, :40-56; Python 3.7 forks), so every
+      worker replays the SAME sample stream: the count is ~ P x (failures in the first 10,000 / P
+      samples), with P times the binomial variance, and tends to a multiple of P (50 = 5 x 10).
+      Under that model the printed 50 is unremarkable for any P in 4..16 (one-sided p 0.04-0.27),
+      where a plain Binomial(10000, p) band would put it at p ~ 3e-4.
+    The test guards the engine's rate (regression band: 5 sigma of the 2e6-sample estimate) and
+    asserts the printed count inside the duplicated-stream model's central 99.9 % band for every
+    plausible worker count."""
     from scipy import stats
 
-    sim, _ = _sim(1e-3, DEMO)
+    sim, _ = _sim(1e-3, DEMO, ref_tag="demo")
     assert sim.num_rounds == 4 and sim.K == 2
     S = 2_000_000
     res = sim.fused_counts(S)
@@ -138,9 +173,14 @@ def test_demo_wer_against_printed(gpu):
     k = round(printed_ler * 10000)
     assert abs(printed_ler * 10000 - k) < 1e-6 and k == 50  # an integer count: the inversion is exact
     lo, hi = stats.binom.ppf([0.0005, 0.9995], 10000, ler)
-    p_low = stats.binom.cdf(k, 10000, ler)
-    print(f"engine LER {ler:.5g} ({res.failures}/{S}); printed count {k}/10000; 99.9% band [{lo}, {hi}]; "
-          f"P(X <= {k}) = {p_low:.3g}")
+    print(f"engine LER {ler:.5g} ({res.failures}/{S}); printed count {k}/10000; plain binomial 99.9% band "
+          f"[{lo}, {hi}], P(X <= {k}) = {stats.binom.cdf(k, 10000, ler):.3g}")
+    for P in range(4, 17):  # duplicated-stream model: count = P x Binomial(10000 // P, LER)
+        c = 10000 // P
+        lo_p, hi_p = stats.binom.ppf([0.0005, 0.9995], c, ler)
+        p_low = stats.binom.cdf(k // P, c, ler)
+        print(f"  P={P:2d} workers: band [{P * lo_p:.0f}, {P * hi_p:.0f}], P(count <= {k}) = {p_low:.3f}")
+        assert P * lo_p <= k <= P * hi_p, (P, lo_p, hi_p)
     sd = math.sqrt(0.00794 * (1 - 0.00794) / S)
     assert abs(ler - 0.00794) < 5 * sd, ler
     wer, _ = sim.WordErrorRate(10000)
