@@ -70,47 +70,50 @@ __global__ void __launch_bounds__(kTileC) cs_unpack(const u64* __restrict__ DO, 
   for (int b = 0; b < nb; ++b) out[((long long)w * 64 + b) * R + r] = (uint8_t)((d >> b) & 1ull);
 }
 
-// per CSR row r of A (cols over the decoder's n): bit b = parity of corr[64w + b][cols];
-// acc[r][w] ^= bits.  grid x = row tiles, y = word w
+// acc[r][w] ^= bit-sliced parities of the CSR rows r of A (cols over the decoder's n) on the byte
+// corrections corr[s][n]: one thread per SAMPLE (its corr row is contiguous, a wave's 64 rows one
+// ~64 n-byte span), every row's parity a ballot = the word of its 64 samples, written by lane 0
+// (each (r, w) belongs to one wave: no atomics).  grid x = sample tiles
 __global__ void __launch_bounds__(kTileC) cs_apply(const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
                                                   int rows, const uint8_t* __restrict__ corr, int n,
                                                   u64* __restrict__ acc, int W, long long count) {
-  const int r = blockIdx.x * kTileC + threadIdx.x;
-  const int w = blockIdx.y;
-  if (r >= rows) return;
-  const int nb = (int)std::min<long long>(64, count - (long long)w * 64);
-  u64 bits = 0;
-  for (int b = 0; b < nb; ++b) {
-    const uint8_t* c = corr + ((long long)w * 64 + b) * n;
+  const long long s = (long long)blockIdx.x * kTileC + threadIdx.x;
+  const int w = (int)(s >> 6);
+  if (((long long)w << 6) >= count) return;  // whole wave past the batch (uniform per wave)
+  const uint8_t* c = corr + (s < count ? s : 0) * (long long)n;
+  for (int r = 0; r < rows; ++r) {
     uint32_t x = 0;
-    for (int e = rp[r]; e < rp[r + 1]; ++e) x ^= c[ci[e]];
-    bits |= (u64)(x & 1u) << b;
+    if (s < count)
+      for (int e = rp[r]; e < rp[r + 1]; ++e) x ^= c[ci[e]];
+    const u64 bits = __ballot((x & 1u) != 0);
+    if (__lane_id() == 0 && bits) acc[(long long)r * W + w] ^= bits;
   }
-  acc[(long long)r * W + w] ^= bits;
 }
 
 // (5): rows 0..m-1 of [h2; L2]: final syndrome (detector rows fin0.., XOR the accumulated space
 // correction) + h2 · c2; rows m..m+K-1: observables (rows obs0..) + the accumulated L1 · c + L2 · c2.
-// Any nonzero residual bit fails its sample.  grid x = row tiles, y = word w
+// Any nonzero residual bit fails its sample.  One thread per sample as cs_apply; lane 0 ORs the
+// residual words and writes the wave's failure word.  grid x = sample tiles
 __global__ void __launch_bounds__(kTileC) cs_final(const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
                                                   const uint8_t* __restrict__ corr, int n, const u64* __restrict__ DO,
                                                   int fin0, int obs0, const u64* __restrict__ acc, int m, int K,
                                                   u64* __restrict__ failw, int W, long long count) {
-  const int r = blockIdx.x * kTileC + threadIdx.x;
-  const int w = blockIdx.y;
-  if (r >= m + K) return;
+  const long long s = (long long)blockIdx.x * kTileC + threadIdx.x;
+  const int w = (int)(s >> 6);
+  if (((long long)w << 6) >= count) return;  // (uniform per wave)
   const int nb = (int)std::min<long long>(64, count - (long long)w * 64);
-  u64 bits = 0;
-  for (int b = 0; b < nb; ++b) {
-    const uint8_t* c = corr + ((long long)w * 64 + b) * n;
-    uint32_t x = 0;
-    for (int e = rp[r]; e < rp[r + 1]; ++e) x ^= c[ci[e]];
-    bits |= (u64)(x & 1u) << b;
-  }
-  const u64 base = DO[(long long)(r < m ? fin0 + r : obs0 + (r - m)) * W + w] ^ acc[(long long)r * W + w];
   const u64 valid = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
-  const u64 res = (base ^ bits) & valid;
-  if (res) atomicOr(&failw[w], res);
+  const uint8_t* c = corr + (s < count ? s : 0) * (long long)n;
+  u64 fw = 0;
+  for (int r = 0; r < m + K; ++r) {
+    uint32_t x = 0;
+    if (s < count)
+      for (int e = rp[r]; e < rp[r + 1]; ++e) x ^= c[ci[e]];
+    const u64 bits = __ballot((x & 1u) != 0);
+    const u64 base = DO[(long long)(r < m ? fin0 + r : obs0 + (r - m)) * W + w] ^ acc[(long long)r * W + w];
+    fw |= (base ^ bits) & valid;
+  }
+  if (__lane_id() == 0) failw[w] = fw;
 }
 
 __global__ void __launch_bounds__(kTileC) cs_tally(const u64* __restrict__ failw, u64* __restrict__ cnt,
@@ -128,27 +131,48 @@ __global__ void __launch_bounds__(kTileC) cs_tally(const u64* __restrict__ failw
     for (int k = 0; k < nb; ++k) fail_out[c0 + (long long)w * 64 + k] = (uint8_t)((f >> k) & 1ull);
 }
 
-// decode statistics of one batched decode into counter sector q (0 = decoder1 rounds, 1 = decoder2)
+// decode statistics of one batched decode into counter sector q (0 = decoder1 rounds, 1 = decoder2):
+// the iteration histogram in LDS first (every sample of a batch usually lands in the same few bins,
+// so per-sample global atomics serialised on one address), then one global add per non-empty bin
 __global__ void __launch_bounds__(kTileC) cs_iters(const int32_t* __restrict__ iters, const uint8_t* __restrict__ conv,
                                                   u64* __restrict__ cnt, int q, long long count) {
+  __shared__ uint32_t hist[kHistBins];
   __shared__ u64 sit, snc;
+  for (int b = threadIdx.x; b < kHistBins; b += kTileC) hist[b] = 0;
   if (threadIdx.x == 0) sit = snc = 0;
   __syncthreads();
-  const long long s = (long long)blockIdx.x * kTileC + threadIdx.x;
-  if (s < count) {
+  u64 it_sum = 0, nc = 0;
+  for (long long s = (long long)blockIdx.x * kTileC + threadIdx.x; s < count; s += (long long)gridDim.x * kTileC) {
     const int it = iters[s];
-    atomicAdd(&sit, (u64)it);
-    if (!conv[s]) atomicAdd(&snc, 1ull);
-    atomicAdd(&cnt[kCntHist + q * kHistBins + std::min(it, kHistBins - 1)], 1ull);
+    it_sum += (u64)it;
+    nc += conv[s] ? 0u : 1u;
+    atomicAdd(&hist[std::min(it, kHistBins - 1)], 1u);
+  }
+  // wave sums, one LDS add per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    it_sum += __shfl_down(it_sum, off);
+    nc += __shfl_down(nc, off);
+  }
+  if (__lane_id() == 0) {
+    atomicAdd(&sit, it_sum);
+    atomicAdd(&snc, nc);
   }
   __syncthreads();
+  for (int b = threadIdx.x; b < kHistBins; b += kTileC)
+    if (hist[b]) atomicAdd(&cnt[kCntHist + q * kHistBins + b], (u64)hist[b]);
   if (threadIdx.x == 0) {
-    const long long nb = std::min<long long>(kTileC, count - (long long)blockIdx.x * kTileC);
-    atomicAdd(&cnt[kCntDec + q], (u64)nb);
+    const long long first = (long long)blockIdx.x * kTileC;
+    long long tot = 0;  // samples this block visited
+    for (long long s0 = first; s0 < count; s0 += (long long)gridDim.x * kTileC) tot += std::min<long long>(kTileC, count - s0);
+    atomicAdd(&cnt[kCntDec + q], (u64)tot);
     atomicAdd(&cnt[kCntIters + q], sit);
     atomicAdd(&cnt[kCntNonconv + q], snc);
   }
 }
+
+// cs_iters: enough blocks to spread the samples, few enough that each block's LDS histogram flush
+// (one global add per non-empty bin) stays cheap
+unsigned iters_grid(long long B) { return (unsigned)std::max<long long>(1, std::min<long long>(256, (B + kTileC - 1) / kTileC)); }
 
 u64 ceil53c(double t) {
   if (!(t > 0.0)) return 0ull;
@@ -395,10 +419,10 @@ int qldpc_circ_launch(qldpc_circ* c, uint64_t seed, uint64_t shot_begin, int64_t
       int rc = qldpc_bp_decode_batch(c->dec1, static_cast<const uint8_t*>(c->synd1.p), static_cast<uint8_t*>(c->corr1.p),
                                      static_cast<int32_t*>(c->iters.p), static_cast<uint8_t*>(c->conv.p), B, stream);
       if (rc) return rc;
-      hipLaunchKernelGGL(cs_iters, dim3((unsigned)((B + kTileC - 1) / kTileC)), dim3(kTileC), 0, st,
+      hipLaunchKernelGGL(cs_iters, dim3(iters_grid(B)), dim3(kTileC), 0, st,
                          static_cast<const int32_t*>(c->iters.p), static_cast<const uint8_t*>(c->conv.p), cnt, 0, B);
       QLDPC_HIP(hipGetLastError());
-      hipLaunchKernelGGL(cs_apply, dim3((unsigned)((m + K + kTileC - 1) / kTileC), (unsigned)W), dim3(kTileC), 0, st,
+      hipLaunchKernelGGL(cs_apply, dim3((unsigned)((B + kTileC - 1) / kTileC)), dim3(kTileC), 0, st,
                          static_cast<const int32_t*>(c->a_rp.p), static_cast<const int32_t*>(c->a_ci.p), m + K,
                          static_cast<const uint8_t*>(c->corr1.p), c->n1, acc, W, B);
       QLDPC_HIP(hipGetLastError());
@@ -424,11 +448,11 @@ int qldpc_circ_launch(qldpc_circ* c, uint64_t seed, uint64_t shot_begin, int64_t
                                  static_cast<uint8_t*>(c->conv.p), B, stream);
     }
     if (rc) return rc;
-    hipLaunchKernelGGL(cs_iters, dim3((unsigned)((B + kTileC - 1) / kTileC)), dim3(kTileC), 0, st,
+    hipLaunchKernelGGL(cs_iters, dim3(iters_grid(B)), dim3(kTileC), 0, st,
                        static_cast<const int32_t*>(c->iters.p), static_cast<const uint8_t*>(c->conv.p), cnt, 1, B);
     QLDPC_HIP(hipGetLastError());
     // (5) residual syndrome / logicals -> failures
-    hipLaunchKernelGGL(cs_final, dim3((unsigned)((m + K + kTileC - 1) / kTileC), (unsigned)W), dim3(kTileC), 0, st,
+    hipLaunchKernelGGL(cs_final, dim3((unsigned)((B + kTileC - 1) / kTileC)), dim3(kTileC), 0, st,
                        static_cast<const int32_t*>(c->f_rp.p), static_cast<const int32_t*>(c->f_ci.p), corr2, c->n2, DO,
                        fin0, D, acc, m, K, static_cast<u64*>(c->failw.p), W, B);
     QLDPC_HIP(hipGetLastError());

@@ -41,6 +41,19 @@ def engine_counts(gpu):
     return {cell: cell_counts(cell, MULT, 0x5EED, 64, log=lambda s: None, hyp=nbp.ADOPTED[cell]) for cell in (16, 20, 25)}
 
 
+@pytest.fixture(scope="module")
+def heldout_counts(gpu):
+    """A fresh 25x sample under the ADOPTED hypotheses at notebook_pin.HELDOUT_SEED (round 5)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from notebook_pin_run import cell_counts
+
+    return {cell: cell_counts(cell, MULT, nbp.HELDOUT_SEED, 64, log=lambda s: None, hyp=nbp.ADOPTED[cell])
+            for cell in (16, 20, 25)}
+
+
 def _pct(cell, counts, formula="current"):
     """Mid-rank percentile of each printed (A, p_c) in the bootstrap distribution, plus the bands."""
     P = nbp.cell_p_list(cell)
@@ -63,11 +76,34 @@ def test_printed_fits_uniform_in_engine_distribution(engine_counts):
     A = nbp.uniformity([e["A_pct"] for _, _, e in pts])
     print("p_c percentiles:", [(cell, R, round(e["p_c_pct"], 3)) for cell, R, e in pts])
     print("p_c uniformity:", pc, "A uniformity:", A)
-    # round 4 measured (profiles/r04/pin/): p_c KS p = 0.51, Fisher p = 0.105; A KS p = 0.18
+    # round 4 measured (profiles/r04/pin/): p_c KS p = 0.51, Fisher p = 0.105; A KS p = 0.18.  ADOPTED
+    # was selected on THIS seed from 36 hypothesis combinations: the Bonferroni-corrected values are
+    # the honest ones for this run (the held-out seed below carries the pre-registered test)
+    print("Bonferroni x", nbp.HYPOTHESIS_COMBINATIONS, ": p_c KS", nbp.bonferroni(pc["ks_p"]), "Fisher",
+          nbp.bonferroni(pc["fisher_p"]), "; A KS", nbp.bonferroni(A["ks_p"]), "Fisher", nbp.bonferroni(A["fisher_p"]))
     assert pc["ks_p"] > 0.05 and pc["fisher_p"] > 0.05, pc
     assert A["ks_p"] > 0.05, A
     # fits that failed inside the bootstrap stay rare (the notebook's fit itself succeeded every time)
     assert all(e["failed"] <= DRAWS // 20 for _, _, e in pts)
+
+
+def test_heldout_seed_uniform(heldout_counts):
+    """The pre-registered check: the ADOPTED hypotheses on a fresh 25x sample
+    (notebook_pin.HELDOUT_SEED, never used for selection).  p_c: KS and Fisher p > 0.05; A: KS p > 0.05.
+    A's Fisher test is reported, not asserted: Fisher's method assumes 15 independent p-values, but A
+    and p_c come from one joint fit per point and a cell's fits share the same engine rates, so A's
+    per-point tails are correlated with p_c's and across rounds (two extreme A's of one cell were what
+    failed it at the selection seed, r04 Fisher p = 0.012); KS, which bounds the whole distribution,
+    is the A criterion."""
+    res = {cell: _pct(cell, heldout_counts[cell]) for cell in (16, 20, 25)}
+    pts = [(cell, R, e) for cell, d in res.items() for R, e in d.items()]
+    assert len(pts) == 15
+    pc = nbp.uniformity([e["p_c_pct"] for _, _, e in pts])
+    A = nbp.uniformity([e["A_pct"] for _, _, e in pts])
+    print("held-out seed", hex(nbp.HELDOUT_SEED), "p_c percentiles:", [(cell, R, round(e["p_c_pct"], 3)) for cell, R, e in pts])
+    print("held-out p_c uniformity:", pc, "A uniformity:", A)
+    assert pc["ks_p"] > 0.05 and pc["fisher_p"] > 0.05, pc
+    assert A["ks_p"] > 0.05, A
 
 
 def test_fit_at_engine_rates_tracks_printed(engine_counts):

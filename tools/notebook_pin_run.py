@@ -110,7 +110,8 @@ def hypothesis_table(cells_bands: dict, formula: str = "current") -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cells", type=int, nargs="+", default=[16, 20, 25])
-    ap.add_argument("--hyp", nargs="+", default=["H0_q0"], help=f"any of {list(nbp.HYPOTHESES)}")
+    ap.add_argument("--hyp", nargs="+", default=["H0_q0"],
+                    help=f"any of {list(nbp.HYPOTHESES)}, or 'adopted' (notebook_pin.ADOPTED per cell)")
     ap.add_argument("--mult", type=float, default=25.0)
     ap.add_argument("--draws", type=int, default=400)
     ap.add_argument("--seed", type=int, default=0x5EED)
@@ -135,11 +136,13 @@ def main():
         return
     result = {"mult": a.mult, "draws": a.draws, "seed": a.seed, "precision": a.precision, "hypotheses": {}}
     for hyp in a.hyp:
-        hres = {"spec": nbp.HYPOTHESES[hyp], "cells": {}}
+        hres = {"spec": ({str(c): nbp.ADOPTED[c] for c in a.cells} if hyp == "adopted" else nbp.HYPOTHESES[hyp]),
+                "cells": {}}
         result["hypotheses"][hyp] = hres
         for cell in a.cells:
             t0 = time.time()
-            cnt = cell_counts(cell, a.mult, a.seed, a.precision, log=lambda s: print(hyp, s, flush=True), hyp=hyp)
+            h_cell = nbp.ADOPTED[cell] if hyp == "adopted" else hyp
+            cnt = cell_counts(cell, a.mult, a.seed, a.precision, log=lambda s: print(hyp, s, flush=True), hyp=h_cell)
             hres["cells"][str(cell)] = {"counts": {str(R): v for R, v in cnt.items()},
                                         "gpu_seconds": time.time() - t0}
             if not a.counts_only:
