@@ -492,12 +492,15 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
     // bank pair (slot mod 32), per 16-lane store group the same over slot mod 16; objective = reads
     // + ws * stores, temperature T0 falling linearly to 0 (round 4; tools/dev/place_opt3.cpp is the
     // offline study: 20 M moves take the n1600 hz model from 362 / 715 to 327 / 442 cycles).
-    // default 4000 moves per edge (n1600: 21.5 M moves, ~3 s on one host core; measured +3.1 %:
-    // 1.221 M vs 1.184 M shots/s, bank-conflict share 0.338 -> 0.276, profiles/r04/passd/); the
-    // result is memoised per process for the same graph, lane map and layout (decoders for other
-    // error rates of one code reuse it)
+    // default 4000 moves per edge, capped at 2^25 moves (~6 s on one host core; n1600: 21.5 M moves,
+    // ~3.9 s; measured +3.1 %: 1.221 M vs 1.184 M shots/s, bank-conflict share 0.338 -> 0.276,
+    // profiles/r04/passd/); QLDPC_M2S_ANNEAL=<moves> or DeviceBP(anneal_iters=...) overrides it (0 =
+    // the greedy placement only, for short runs).  The result is memoised per process for the same
+    // graph, lane map and layout (decoders for other error rates of one code reuse it); the memo keeps
+    // at most kAnnealMemo placements (a sweep over many codes does not grow it without bound)
     const int iters_env = anneal_iters >= 0 ? anneal_iters : env_int("QLDPC_M2S_ANNEAL", -1);
-    const int iters = iters_env >= 0 ? iters_env : (int)std::min<long long>(4000LL * g->nnz, 1LL << 30);
+    const int iters = iters_env >= 0 ? iters_env : (int)std::min<long long>(4000LL * g->nnz, 1LL << 25);
+    constexpr size_t kAnnealMemo = 16;
     static std::mutex memo_mu;
     static std::map<uint64_t, std::vector<int>> memo;
     uint64_t key = 0xcbf29ce484222325ull;
@@ -596,6 +599,7 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
         }
       }
       std::lock_guard<std::mutex> lk(memo_mu);
+      if (memo.size() >= kAnnealMemo) memo.clear();
       memo[key] = lslot;
     }
   }
@@ -1636,7 +1640,13 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     a.work = nullptr;
     if (bp->engine >= 3 && env_int("QLDPC_DYN", 1) != 0) {  // chunk queue, ~64 chunks per workgroup
       if (!bp->work.p && bp->work.alloc(16)) return QLDPC_ENOMEM;
+      // at most kMaxQueuePops pops of the one queue counter per launch: small graphs run many
+      // workgroups per CU and decode a syndrome in microseconds, and 65,536 one-syndrome pops of one
+      // address serialised at ~12 ns each (0.8 ms per launch whatever max_iter; round 5 probe,
+      // tools/dev/probe_small_dec.py)
+      constexpr long long kMaxQueuePops = 8192;
       a.chunk = (int)std::max<long long>(1, std::min<long long>(kChunkMax, B / (cap * std::max(1, env_int("QLDPC_DYN_PER", 64)))));
+      a.chunk = (int)std::min<long long>(kChunkMax, std::max<long long>(a.chunk, (B + kMaxQueuePops - 1) / kMaxQueuePops));
       QLDPC_HIP(hipMemsetAsync(bp->work.p, 0, 4, (hipStream_t)stream));
       a.work = static_cast<unsigned int*>(bp->work.p);
     }

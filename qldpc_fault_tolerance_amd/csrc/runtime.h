@@ -81,10 +81,10 @@ struct qldpc_bp {
   std::vector<int32_t> slot_var;
   qldpc_rt::DevBuf perm;
   qldpc_rt::DevBuf rperm;  // engine 3: original check of each check label (label_checks)
-  int gather_conf[2] = {0, 0};
+  int gather_conf[2] = {0, 0};  // engine 3: extra gather cycles per pass before / after labelling
   // engine-3 fp64 variable phase, static LDS model per workgroup-iteration (qldpc_bp_lds_model):
   // CS gather cycles / extra, V-slot read cycles / extra, v2c store group-cycles / extra
-  int64_t lds_model[6] = {0, 0, 0, 0, 0, 0};  // engine 3: extra gather cycles per pass before / after labelling
+  int64_t lds_model[6] = {0, 0, 0, 0, 0, 0};
   int d3k = 0;
   int d2k = 0;  // byte-F family: compile-time degree-2 slot count (slots of the measurement variables)
   int ea_shift = 0;  // engine 3: 2 = dword-scaled LDS addresses in the edge words (images > 64 KiB)

@@ -7,6 +7,7 @@ the hand-written kernels.  No CPU fallback exists (``_native`` raises).
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -73,11 +74,28 @@ class DeviceGraph:
 
 
 class DeviceBP:
-    """``ldpc.bp_decoder`` equivalent on the GPU (``qldpc_bp_create``)."""
+    """``ldpc.bp_decoder`` equivalent on the GPU (``qldpc_bp_create``).
+
+    ``anneal_iters``: moves of the annealed V-slot placement the fp64 engine-3 families run at
+    creation (host time, one core: ~0.18 us per move; default 4000 per edge capped at 2^25, memoised
+    per process for the same graph).  0 keeps the greedy placement (decodes identically; the placement
+    only moves LDS bank conflicts), for short runs over many codes."""
 
     def __init__(self, H, channel_probs, max_iter: int = 0, bp_method="minimum_sum", ms_scaling_factor=0.625,
                  precision: int = 64, vars_per_thread: int = 0, device: int | None = None, graph: DeviceGraph | None = None,
-                 min_col_slots: int = 0, soft: bool = False, hbm: bool = False):
+                 min_col_slots: int = 0, soft: bool = False, hbm: bool = False, anneal_iters: int | None = None):
+        if anneal_iters is not None:  # read by qldpc_bp_create (QLDPC_M2S_ANNEAL) at creation only
+            old = os.environ.get("QLDPC_M2S_ANNEAL")
+            os.environ["QLDPC_M2S_ANNEAL"] = str(int(anneal_iters))
+            try:
+                self.__init__(H, channel_probs, max_iter, bp_method, ms_scaling_factor, precision, vars_per_thread,
+                              device, graph, min_col_slots, soft, hbm, None)
+            finally:
+                if old is None:
+                    os.environ.pop("QLDPC_M2S_ANNEAL", None)
+                else:
+                    os.environ["QLDPC_M2S_ANNEAL"] = old
+            return
         self.graph = graph if graph is not None else DeviceGraph(H, device=device)
         n = self.graph.n
         probs = np.asarray(channel_probs, dtype=np.float64)
