@@ -52,9 +52,10 @@ LDS_MIX = {
             "(3 x b128 + tail b64) + CS / argmin-slot stores (2 x b64) = 96 cycles"),
     "m2s8": (8, {"ds_read_b64": 16, "ds_read_b128": 4, "ds_write_b64": 10}, "m2s8_row_mix",
              "m2s8 row of 8 (engine ids 10103 / 10203): 8 x (b64 + b64 + store b64) + 4 x b128 + 2 x store b64 = 108 cycles"),
-    "st64": (9, {"ds_read_b64": 1, "ds_read_b128": 13, "ds_write_b64": 9, "ds_write_b128": 1}, None,
-             "fp64 two-word tail row of 9 (engine ids 1013 / 101013): 9 x (CS gather b128 + v2c store b64) + the row "
-             "(4 x b128 + tail b64) + the CS store (b128) = 121 cycles"),
+    "st64": (9, {"ds_read_b64": 10, "ds_read_b128": 13, "ds_write_b64": 9, "ds_write_b128": 1}, None,
+             "fp64 two-word tail row of 9 (engine ids 1013 / 101013; 1024-thread workgroups, 128-VGPR budget: the "
+             "own previous v2c is re-read from LDS, bp_reg.h RState::kKeepV false): 9 x (CS gather b128 + own V-slot "
+             "read b64 + v2c store b64) + the row (4 x b128 + tail b64) + the CS store (b128) = 139 cycles"),
 }
 
 

@@ -145,10 +145,11 @@ int qldpc_osd_decode_batch(const qldpc_osd *osd, const uint8_t *synd, const doub
                            int32_t threads);
 
 /*
- * GPU OSD (uniform channel_probs, n <= 8192): the same outputs as
- * qldpc_osd_decode_batch, one workgroup per syndrome; all pointers are DEVICE
- * pointers (d_post from qldpc_bp_decode_batch_soft).  Non-uniform priors
- * return QLDPC_ENOTSUP (use the host stage).
+ * GPU OSD (n <= 8192, osd_e order <= 24): the same outputs as qldpc_osd_decode_batch, one
+ * workgroup per syndrome; all pointers are DEVICE pointers (d_post from
+ * qldpc_bp_decode_batch_soft).  Uniform channel_probs weigh candidates by popcount; non-uniform
+ * ones (the circuit-level DEM priors) by sum log(1/p_j), added in ascending column order as the
+ * host stage does.
  */
 typedef struct qldpc_osd_gpu qldpc_osd_gpu;
 int qldpc_osd_gpu_create(const qldpc_graph *g, const double *channel_probs, int32_t osd_method, int32_t osd_order,
@@ -358,8 +359,8 @@ int qldpc_mc_run_sharded(qldpc_mc **mcs, qldpc_comm **comms, int32_t ndev, doubl
  * Sample s draws mechanism j when Philox4x32-10(key = seed, ctr = (j, shot, 0x51D50003)) as a
  * 53-bit uniform is < probs[j] (shot = shot_begin + s).  Counters: shots, failures, sector 0 =
  * decoder1 decodes (num_rounds per sample), sector 1 = decoder2 decodes.  d_fail [S] (or NULL),
- * d_detobs [S][D + K] sampled detector and observable bits (or NULL).  Async on `stream` except
- * with a host OSD stage (synchronous per batch).  dec1 = dec2 = NULL (and NULL h1_space_cor / L1 /
+ * d_detobs [S][D + K] sampled detector and observable bits (or NULL).  Asynchronous on `stream`
+ * (no host round trip, BP+OSD included).  dec1 = dec2 = NULL (and NULL h1_space_cor / L1 /
  * L2) makes a sampler-only handle for qldpc_circ_sample (decoders outside the engine).
  */
 typedef struct qldpc_circ qldpc_circ;
@@ -367,7 +368,8 @@ int qldpc_circ_create(const qldpc_graph *dem, const qldpc_graph *dem_obs, const 
                       const qldpc_graph *h1_space_cor, const qldpc_graph *L1, qldpc_bp *dec2, const qldpc_graph *L2,
                       int32_t num_rounds, int32_t num_rep, int64_t max_batch, qldpc_circ **out);
 /* decoder2 as bposd_decoder (ST_BPOSD_Decoder_Circuit, src/Decoders_SpaceTime.py:277-292): dec2 from
- * qldpc_bp_create_soft and ONE of a GPU OSD (uniform priors) or a host OSD stage on h2. */
+ * qldpc_bp_create_soft and ONE of a GPU OSD or a host OSD stage on h2; a host stage is turned into a
+ * GPU OSD with its method, order, rank and soft weights, so the launch never leaves the device. */
 int qldpc_circ_set_final_osd(qldpc_circ *circ, qldpc_osd_gpu *osd_gpu, const qldpc_osd *osd_host);
 int qldpc_circ_info(const qldpc_circ *circ, int32_t *detectors, int32_t *observables, int32_t *mechanisms);
 int qldpc_circ_launch(qldpc_circ *circ, uint64_t seed, uint64_t shot_begin, int64_t shot_count, void *d_counters,

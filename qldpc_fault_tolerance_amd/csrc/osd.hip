@@ -354,7 +354,7 @@ constexpr int kOsdThreadsLds = 1024;  // LDS-resident image: one workgroup per C
 // workgroup: [0] sort, [1] H load, [2] Gauss-Jordan, [3] swaps + bit-vectors, [4] candidates,
 // [5] outputs, [6] syndromes, [7] positions visited, [8] of [2]: pivot searches + their barrier,
 // [9] of [2] (register rows): pivot-row publication + its barrier
-__device__ unsigned long long g_osd_stamps[10];
+__device__ unsigned long long g_osd_stamps[16];
 __device__ inline unsigned long long osd_stamp() {
 #if QLDPC_STAMPS
   unsigned long long t;
@@ -397,11 +397,22 @@ constexpr int kOsdXB = QLDPC_OSD_XB;
 #define QLDPC_OSD_G 4
 #endif
 constexpr bool kOsdM4R = QLDPC_OSD_M4R && !QLDPC_OSD_1B;
+// blocked mode (PNL 3): byte offset of the Four-Russians tables in the panel area (after the
+// half-words and masks [m] u32, pk [32], pidx [m]) and the area's size with them ([8][16][WR + 1] u64)
+__host__ __device__ inline size_t osd_blk_tab_off(int m) { return ((size_t)12 * m + 128 + 15) & ~(size_t)15; }
+inline size_t osd_blk_bytes(int m, int wr) { return osd_blk_tab_off(m) + (size_t)8 * 16 * (wr + 1) * 8; }
+
 constexpr int kOsdG = QLDPC_OSD_G;
 // rows of (WR + 1) words in the register-row pivot area: the pivot row (1), the one-barrier build's
 // per-wave slots, or the Four-Russians table (2^G rows) and its per-pivot slots (4 rows)
 constexpr int osd_prows(int lb) { return QLDPC_OSD_1B ? 2 * (lb / 64) : kOsdM4R ? (1 << kOsdG) + 4 : 1; }
 
+
+// calls f(integral_constant<int, Q>) for Q = 0, 1, ... while it returns true (compile-time word index)
+template <int... Q, class F>
+__device__ __attribute__((always_inline)) inline void osd_for_words(std::integer_sequence<int, Q...>, F&& f) {
+  (void)(f(std::integral_constant<int, Q>{}) && ...);
+}
 
 struct OsdGpuArgs {
   const int32_t* rp;
@@ -529,7 +540,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   const int w = A.order < k ? A.order : k;
   const int nh = A.method == 2 ? k : w;
 
-  unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t0 = osd_stamp(), t1;
 #define OSD_ST(k)              \
   if (QLDPC_STAMPS) {          \
@@ -621,7 +632,241 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
       u64* pbuf = reinterpret_cast<u64*>(smem + A.pbuf_off);  // [WR] pivot row, [WR] its syndrome bit
       OSD_ST(1)
       int npiv = 0;   // uniform
-      if constexpr (PNL) {
+      if constexpr (PNL == 3) {
+        // Blocked elimination (round 5; the default for register rows): the
+        // per-pivot loops below cost every wave two barriers and a pivot-row round trip per pivot
+        // (~2,100 cycles per pivot at n1600, 0.62 of wave cycles parked, profiles/r04/passt/).  Here
+        // the pivots of a 32-column panel (half a row word) are found by ONE search wave with no
+        // barrier per pivot: it holds every row's panel half-word (rows s * 64 + lane, SM slots) and
+        // a 32-bit combination mask per row (which of the panel's pivot rows, in their panel-start
+        // state, the row has absorbed); a pivot step is a wave minimum over the unused rows' first
+        // set bits (the lexicographic minimum of (column, row): the greedy scan's pivot and its lowest
+        // row, as the loops below pick it), two readlanes and a masked xor per slot.  Then the panel's
+        // pivot rows publish their panel-start words q.. (+ syndrome bit) as the single entries of
+        // 4-pivot Four-Russians tables (16 combinations per group), the workgroup fills the tables,
+        // and every row xors in ONE table entry per group for everything past the panel.  Exact: the
+        // same pivots, pivot rows and reduced rows as the per-pivot elimination (an unused row is zero
+        // before the scan position, so the pivot rows' earlier words are zero and the words < q never
+        // change).  Four barriers per panel instead of two per pivot.
+        static_assert(RPT == 1, "blocked mode: one row per thread");
+        constexpr int SM = LB / 64;  // row slots per lane of the search wave
+        constexpr u64 kLo = 0xFFFFFFFFull, kHi = ~kLo;
+        constexpr int TS = WR + 1;   // table entry stride: words of a start row + its syndrome bit
+        uint32_t* pw = reinterpret_cast<uint32_t*>(smem + A.pnl_off);  // [m] panel half-words
+        uint32_t* pmsk = pw + m;                                       // [m] combination masks
+        int* pk = reinterpret_cast<int*>(pmsk + m);                    // [32] the panel's pivot rows
+        int* pidx = pk + 32;                                           // [m] panel index of a pivot row
+        u64* T = reinterpret_cast<u64*>(smem + A.pnl_off + osd_blk_tab_off(m));  // [8 groups][16][TS]
+        int32_t* lkk = reinterpret_cast<int32_t*>(smem);  // pivots (position << 11) | row, over the dead sort keys
+        __shared__ int s_P;
+        uint32_t usedm = 0;  // search wave: bit s = row s * 64 + lane is used (rows >= m: always)
+        if (tid < 64) {
+#pragma unroll
+          for (int s2 = 0; s2 < SM; ++s2)
+            if (s2 * 64 + tid >= m) usedm |= 1u << s2;
+        }
+        // one compile-time word q per call (every row word stays in a VGPR; a runtime q would index
+        // the row array and demote it to scratch)
+        auto blk_word = [&](auto qc) __attribute__((always_inline)) -> bool {
+          constexpr int q = decltype(qc)::value;
+          if (q * 64 >= n || npiv >= rank) return false;  // uniform
+          for (int h = 0; h < 2; ++h) {
+            if (q * 64 + h * 32 >= n || npiv >= rank) break;  // uniform
+            // 1. every row's panel half-word (every earlier panel applied)
+            unsigned long long tb0 = QLDPC_STAMPS ? osd_stamp() : 0ull;
+            if (tid < m) pw[tid] = (uint32_t)(row[0][q] >> (32 * h));
+            __syncthreads();
+            if (QLDPC_STAMPS) {  // [11]: step 1 + its barrier
+              const unsigned long long t = osd_stamp();
+              st[11] += t - tb0;
+              tb0 = t;
+            }
+            // 2. the search wave: the panel's greedy pivots, its rows' final half-words and masks
+            if (tid < 64) {
+              // a lone wave is latency-bound: the pivot step keeps its dependent chains short (unused
+              // masks as VGPRs, a min3 tree over the slots, a 4-level select tree for the pivot row's
+              // half-word and mask, the pivot list in one VGPR written after the panel)
+              uint32_t wv[SM], cm[SM];
+              uint32_t ub = ~usedm;  // bit s: row s * 64 + lane is a candidate (unused, < m)
+#pragma unroll
+              for (int s2 = 0; s2 < SM; ++s2) {
+                wv[s2] = s2 * 64 + tid < m ? pw[s2 * 64 + tid] : 0u;
+                cm[s2] = 0u;
+              }
+              uint32_t pkv = 0;  // lane k: (position << 11) | row of the panel's pivot k
+              int P = 0, np = npiv;
+              while (np < rank) {  // uniform
+                // key = (first set bit << 11) | row over the unused rows; none: >= 0xFFFFF800
+                uint32_t kk[SM];
+#pragma unroll
+                for (int s2 = 0; s2 < SM; ++s2) {
+                  const uint32_t um = (uint32_t)__builtin_amdgcn_sbfe((int)ub, s2, 1);
+                  kk[s2] = (ffbl_u32(wv[s2] & um) << 11) | (uint32_t)(s2 * 64 + tid);
+                }
+                // min3 tree over the slots (compile-time shapes: SM <= 16 -> at most 3 levels)
+                constexpr int N1 = (SM + 2) / 3, N2 = (N1 + 2) / 3, N3 = (N2 + 2) / 3;
+                auto mn = [](uint32_t a, uint32_t b) { return a < b ? a : b; };
+                uint32_t l1[N1], l2[N2];
+#pragma unroll
+                for (int i = 0; i < N1; ++i)
+                  l1[i] = mn(kk[3 * i], mn(3 * i + 1 < SM ? kk[3 * i + 1 < SM ? 3 * i + 1 : 0] : ~0u,
+                                           3 * i + 2 < SM ? kk[3 * i + 2 < SM ? 3 * i + 2 : 0] : ~0u));
+#pragma unroll
+                for (int i = 0; i < N2; ++i)
+                  l2[i] = mn(l1[3 * i], mn(3 * i + 1 < N1 ? l1[3 * i + 1 < N1 ? 3 * i + 1 : 0] : ~0u,
+                                           3 * i + 2 < N1 ? l1[3 * i + 2 < N1 ? 3 * i + 2 : 0] : ~0u));
+                static_assert(N3 == 1, "search wave: at most 27 row slots");
+                const uint32_t key = wave_min_u32_bc(mn(l2[0], mn(N2 > 1 ? l2[N2 > 1 ? 1 : 0] : ~0u,
+                                                                  N2 > 2 ? l2[N2 > 2 ? 2 : 0] : ~0u)));
+                if (key > 0x1FFFFu) break;  // no pivot left in this panel (uniform)
+                const int fb = (int)(key >> 11), r = (int)(key & 2047u), sr = r >> 6, lr = r & 63;
+                // the pivot row's half-word and mask: a select tree on sr's bits (levels of halving
+                // arrays, short live ranges), then one readlane each
+                constexpr int H1 = (SM + 1) / 2, H2 = (H1 + 1) / 2, H3 = (H2 + 1) / 2;
+                uint32_t aw[H1], ac[H1];
+                {
+                  // bitwise selects (a select of two array loads would become a load at a selected
+                  // index: a dynamically indexed array, demoted to scratch)
+                  const uint32_t msk = (sr & 1) ? ~0u : 0u;  // uniform
+#pragma unroll
+                  for (int i = 0; i < H1; ++i) {
+                    aw[i] = wv[2 * i] ^ ((wv[2 * i] ^ wv[2 * i + 1 < SM ? 2 * i + 1 : 2 * i]) & msk);
+                    ac[i] = cm[2 * i] ^ ((cm[2 * i] ^ cm[2 * i + 1 < SM ? 2 * i + 1 : 2 * i]) & msk);
+                  }
+                }
+                uint32_t bw[H2], bc[H2];
+                {
+                  const uint32_t msk = (sr & 2) ? ~0u : 0u;
+#pragma unroll
+                  for (int i = 0; i < H2; ++i) {
+                    bw[i] = aw[2 * i] ^ ((aw[2 * i] ^ aw[2 * i + 1 < H1 ? 2 * i + 1 : 2 * i]) & msk);
+                    bc[i] = ac[2 * i] ^ ((ac[2 * i] ^ ac[2 * i + 1 < H1 ? 2 * i + 1 : 2 * i]) & msk);
+                  }
+                }
+                uint32_t cw[H3], cc[H3];
+                {
+                  const uint32_t msk = (sr & 4) ? ~0u : 0u;
+#pragma unroll
+                  for (int i = 0; i < H3; ++i) {
+                    cw[i] = bw[2 * i] ^ ((bw[2 * i] ^ bw[2 * i + 1 < H2 ? 2 * i + 1 : 2 * i]) & msk);
+                    cc[i] = bc[2 * i] ^ ((bc[2 * i] ^ bc[2 * i + 1 < H2 ? 2 * i + 1 : 2 * i]) & msk);
+                  }
+                }
+                uint32_t dw = cw[0], dc = cc[0];
+                if constexpr (H3 > 1) {
+                  const uint32_t msk = (sr & 8) ? ~0u : 0u;
+                  dw = cw[0] ^ ((cw[0] ^ cw[H3 > 1 ? 1 : 0]) & msk);
+                  dc = cc[0] ^ ((cc[0] ^ cc[H3 > 1 ? 1 : 0]) & msk);
+                }
+                static_assert(SM <= 16, "search wave: at most 16 row slots");
+                const uint32_t pwv = (uint32_t)__builtin_amdgcn_readlane((int)dw, lr);
+                const uint32_t pmv = (uint32_t)__builtin_amdgcn_readlane((int)dc, lr);
+                const uint32_t add = pmv | (1u << P);
+                const bool me = tid == lr;
+#pragma unroll
+                for (int s2 = 0; s2 < SM; ++s2) {
+                  const uint32_t sel = (uint32_t)__builtin_amdgcn_sbfe((int)wv[s2], fb, 1);  // -(bit fb)
+                  const bool pr = me && s2 == sr;  // the pivot row keeps its word and mask
+                  wv[s2] = pr ? pwv : wv[s2] ^ (pwv & sel);
+                  cm[s2] = pr ? pmv : cm[s2] ^ (add & sel);
+                }
+                ub = me ? (ub & ~(1u << sr)) : ub;  // the pivot row leaves the candidates
+                pkv = tid == P ? (uint32_t)(((q * 64 + h * 32 + fb) << 11) | r) : pkv;
+                ++P;
+                ++np;
+              }
+              if (tid < P) {
+                lkk[npiv + tid] = (int32_t)pkv;
+                pk[tid] = (int)(pkv & 2047u);
+                pidx[pkv & 2047u] = tid;
+              }
+#pragma unroll
+              for (int s2 = 0; s2 < SM; ++s2)
+                if (s2 * 64 + tid < m) {
+                  pw[s2 * 64 + tid] = wv[s2];
+                  pmsk[s2 * 64 + tid] = cm[s2];
+                }
+              usedm = ~ub;
+              if (tid == 0) {
+                s_P = P;
+                s_npiv = np;
+              }
+              if (QLDPC_STAMPS) {  // [8]: the search, [7]: its pivots
+                const unsigned long long t = osd_stamp();
+                st[8] += t - tb0;
+                st[7] += (unsigned long long)P;
+                tb0 = t;
+              }
+            }
+            __syncthreads();
+            const int P = s_P;
+            npiv = s_npiv;
+            // 3. the panel's pivot rows publish their panel-start rows (words q.., syndrome bit) as
+            // the single entries of their group's table; every row takes its final half-word and mask
+            uint32_t cmk = 0, fw = 0;
+            if (tid < m) {
+              cmk = pmsk[tid];
+              fw = pw[tid];
+              const int kx = pidx[tid];
+              if (kx >= 0 && kx < P && pk[kx] == tid) {  // (stale entries of earlier panels fail the check)
+                used_r[0] = true;
+                u64* d = T + (size_t)((kx >> 2) * 16 + (1 << (kx & 3))) * TS;
+#pragma unroll
+                for (int q2 = q; q2 < WR; ++q2) d[q2] = row[0][q2];
+                d[WR] = sbit[0];
+              }
+            }
+            __syncthreads();
+            // 4. every group's entries of >= 2 pivots: the xor of its single entries
+            const int ng = (P + 3) >> 2;
+            constexpr int nw = WR + 1 - q;  // words q..WR-1 and the syndrome entry
+            for (int t = tid; t < ng * 16 * nw; t += TB) {
+              const int gc = t / nw, c = gc & 15;
+              const int wd = q + t % nw;
+              if (c & (c - 1)) {
+                const u64* g0 = T + (size_t)(gc - c) * TS + wd;
+                u64 v = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                  if ((c >> i) & 1) v ^= g0[(size_t)(1 << i) * TS];
+                T[(size_t)gc * TS + wd] = v;
+              }
+            }
+            __syncthreads();
+            if (QLDPC_STAMPS) {  // [9]: the search barrier, the single entries and the table fill
+              const unsigned long long t = osd_stamp();
+              st[9] += t - tb0;
+              tb0 = t;
+            }
+            // 5. every row: one table entry per group into everything past the panel (the high half
+            // of word q when the panel is its low half, words q + 1.., the syndrome bit); the panel
+            // half-word is the search's final value
+            if (tid < m) {
+              u64 accq = 0;
+              for (int g = 0; g < ng; ++g) {  // uniform bound
+                const uint32_t c = (cmk >> (4 * g)) & 15u;
+                if (c) {
+                  const u64* src = T + (size_t)(g * 16 + (int)c) * TS;
+                  accq ^= src[q];
+#pragma unroll
+                  for (int q2 = q + 1; q2 < WR; ++q2) row[0][q2] ^= src[q2];
+                  sbit[0] ^= (uint32_t)src[WR];
+                }
+              }
+              row[0][q] = h ? ((row[0][q] & kLo) | ((u64)fw << 32)) : (((row[0][q] ^ accq) & kHi) | (u64)fw);
+            }
+            if (QLDPC_STAMPS) st[10] += osd_stamp() - tb0;  // [10]: the row updates
+            // (pw is rewritten by the next panel's step 1 after these reads; T behind its first two barriers)
+          }
+          return true;
+        };
+        osd_for_words(std::make_integer_sequence<int, WR>{}, blk_word);
+        for (int i = tid; i < npiv; i += TB) {
+          const int v = lkk[i];
+          pivrow[i] = v & 2047;
+          pivpos[i] = v >> 11;
+        }
+      } else if constexpr (PNL) {
         static_assert(RPT == 1, "panel mode: one row per thread");
         constexpr int SM = LB / 64;  // row slots per lane of the search wave (rows s * 64 + lane)
         constexpr u64 kLo = 0xFFFFFFFFull, kHi = ~kLo;
@@ -1507,15 +1752,10 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   }
 #undef OSD_ST
   if (QLDPC_STAMPS && tid == 0)
-    for (int k2 = 0; k2 < 10; ++k2) atomicAdd(&g_osd_stamps[k2], st[k2]);
+    for (int k2 = 0; k2 < 16; ++k2) atomicAdd(&g_osd_stamps[k2], st[k2]);
 }
 
 #if QLDPC_EXPERIMENTAL
-// calls f(integral_constant<int, Q>) for Q = 0, 1, ... while it returns true (compile-time word index)
-template <int... Q, class F>
-__device__ __attribute__((always_inline)) inline void osd_for_words(std::integer_sequence<int, Q...>, F&& f) {
-  (void)(f(std::integral_constant<int, Q>{}) && ...);
-}
 
 // Two syndromes per workgroup (register-row mode, 768 threads, m <= 768; round 4, VERDICT r03 item
 // 5).  The Gauss-Jordan of one syndrome is a chain of ~780 dependent steps (wave minimum, LDS
@@ -1979,7 +2219,8 @@ OsdKern osd_rr_kernel_t(int wr) {
   }
 }
 OsdKern osd_rr_kernel(int wr, int pnl) {
-  return pnl == 2 ? osd_rr_kernel_t<2>(wr) : pnl ? osd_rr_kernel_t<1>(wr) : osd_rr_kernel_t<0>(wr);
+  return pnl == 3 ? osd_rr_kernel_t<3>(wr) : pnl == 2 ? osd_rr_kernel_t<2>(wr) : pnl ? osd_rr_kernel_t<1>(wr)
+                                                                                   : osd_rr_kernel_t<0>(wr);
 }
 OsdKern osd_rr2_kernel_of(int wr) {
 #if QLDPC_EXPERIMENTAL
@@ -2100,9 +2341,10 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
   // (profiles/r03/bposd_pnl/)
   const char* pnl_env = std::getenv("QLDPC_OSD_PNL");
   if (G->wr && pnl_env && std::atoi(pnl_env) != 0) {
-    G->pnl = std::atoi(pnl_env) == 2 ? 2 : 1;  // 2: the distributed panel search (one barrier per pivot)
+    const int pv = std::atoi(pnl_env);
+    G->pnl = pv == 3 ? 3 : pv == 2 ? 2 : 1;  // 2: the distributed panel search (one barrier per pivot); 3: blocked
     G->pnl_off = (int)((G->lds + 15) & ~(size_t)15);
-    G->lds = (size_t)G->pnl_off + osd_pnl_bytes(m, G->wr);
+    G->lds = (size_t)G->pnl_off + (G->pnl == 3 ? osd_blk_bytes(m, G->wr) : osd_pnl_bytes(m, G->wr));
   }
   // two syndromes per workgroup (osd_rr2_kernel, the 768-thread register-row kernels): a second LDS
   // area and HBM slice per workgroup; QLDPC_OSD_NSY=1 keeps one
@@ -2163,10 +2405,10 @@ int qldpc_osd_gpu_destroy(qldpc_osd_gpu* osd) {
 #if QLDPC_STAMPS
 // diagnostic builds only: read and clear osd_gpu_kernel's step-cycle sums
 int qldpc_debug_osd_stamps(unsigned long long* out) {
-  unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(out, HIP_SYMBOL(g_osd_stamps), 80) != hipSuccess)
+  unsigned long long z[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(out, HIP_SYMBOL(g_osd_stamps), 128) != hipSuccess)
     return -1;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_osd_stamps), z, 80) == hipSuccess ? 0 : -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_osd_stamps), z, 128) == hipSuccess ? 0 : -1;
 }
 #endif
 

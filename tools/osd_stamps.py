@@ -25,7 +25,7 @@ cls = BPOSD_Decoder_Class(10, "minimum_sum", 0.625, "osd_e", 10, precision=prec)
 dx, dz = cls.GetDecoder({"h": code.hz, "p_data": p}), cls.GetDecoder({"h": code.hx, "p_data": p})
 sim = CodeSimulator_DataError(code, dx, dz, [p / 2] * 3, "Total", seed=5)
 lib = ctypes.CDLL(_native.LIB_PATH)
-out = (ctypes.c_ulonglong * 10)()
+out = (ctypes.c_ulonglong * 16)()
 sim.bposd_counts(S)  # warm-up
 assert lib.qldpc_debug_osd_stamps(out) == 0
 f, c, o = sim.bposd_counts(S)
@@ -43,3 +43,7 @@ else:
     print(f"positions per syndrome {v[7] / max(1, v[6]):.0f}; per position: {v[2] / max(1, v[7]):.0f} clk, "
           f"of which search + barrier {v[8] / max(1, v[7]):.0f}, pivot-row publication + barrier (register rows) "
           f"{v[9] / max(1, v[7]):.0f}")
+if os.environ.get("QLDPC_OSD_PNL", "0") == "3":  # blocked: [7] pivots, [8] searches, [9] tables, [10] row updates, [11] step 1
+    pv = max(1, v[7])
+    print(f"blocked: pivots per syndrome {v[7] / max(1, v[6]):.0f}; per pivot: search {v[8] / pv:.0f} clk, tables {v[9] / pv:.0f}, "
+          f"row updates {v[10] / pv:.0f}, panel-word exchange {v[11] / pv:.0f} (Gauss-Jordan {v[2] / pv:.0f})")
