@@ -157,6 +157,12 @@ int qldpc_osd_gpu_create(const qldpc_graph *g, const double *channel_probs, int3
 int qldpc_osd_gpu_destroy(qldpc_osd_gpu *osd);
 int qldpc_osd_gpu_decode(qldpc_osd_gpu *osd, const uint8_t *d_synd, const double *d_post, const uint8_t *d_conv,
                          const uint8_t *d_bp_corr, uint8_t *d_out0, uint8_t *d_outw, int64_t B, void *stream);
+/* Elimination geometry the handle chose (no reference counterpart; tests and DESIGN.md §4):
+ * row_words = 64-bit words per register row (0: LDS / HBM image), window_words = the column
+ * window's row words (0: none; its overruns are redone at full width), threads = per workgroup,
+ * workgroups = the launch's persistent grid (the window launch's when there is one). */
+int qldpc_osd_gpu_geometry(const qldpc_osd_gpu *osd, int32_t *row_words, int32_t *window_words, int32_t *threads,
+                           int32_t *workgroups);
 
 /*
  * Fused Monte Carlo shot loop = CodeSimulator_DataError._single_run

@@ -367,6 +367,12 @@ __device__ inline unsigned long long osd_stamp() {
 #endif
 }
 constexpr int kOsdMaxN = 8192;
+// column-window launch: the mark a syndrome whose elimination overran the window leaves in its
+// outw[0] for the full-width redo launch (outputs are 0 / 1 bytes otherwise)
+constexpr uint8_t kOsdRedo = 0xFF;
+// column window: positions past rank + nh the window words cover (dependent positions allowed
+// before the rank is reached)
+constexpr int kOsdWinSlack = 64;
 // register-row mode: pivot-row words read per batch ahead of their xors
 #ifndef QLDPC_OSD_XB
 #define QLDPC_OSD_XB 8
@@ -434,6 +440,9 @@ struct OsdGpuArgs {
   int pbuf_off;  // register-row mode: LDS byte offset of the pivot-row broadcast buffer
   int pnl_off;   // panel mode: LDS byte offset of the panel area (words, masks, pivot rows, indices)
   int syn_lds;   // two-syndrome register-row kernel: LDS bytes per syndrome area
+  int win;       // 1: column-window launch (rows hold the first WR words only; a syndrome whose
+                 // elimination overruns them is marked for the redo launch), 2: the redo launch,
+                 // 3: test hook (QLDPC_OSD_WIN_REDO=1): a window launch that also marks every odd b
   long long ws_words, iws_ints;
 };
 
@@ -509,8 +518,11 @@ __device__ inline u64 ord_key(double x) {
 // the rows its mask names (uniform loop, broadcast LDS reads).  Same pivots (the lexicographic
 // minimum of (first set bit >= scan position, row) over unused rows, on up-to-date words) and the
 // same reduced rows as the per-pivot elimination; three barriers per panel instead of two per pivot.
-template <int LB, int WR = 0, int RPT = 1, int PNL = 0>
-__global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
+// WPE: minimum waves per SIMD the VGPR budget is pinned to (two workgroups per CU: the
+// column-window kernels, 2 x 12 waves; the two-rows-per-thread blocked kernels, 2 x 6 waves).
+template <int LB, int WR = 0, int RPT = 1, int PNL = 0, int WPE = 1>
+__global__ void __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(RPT == 2 ? 3 : WPE)))
+osd_gpu_kernel(OsdGpuArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, TB = blockDim.x;
   const int m = A.m, n = A.n, W = A.W, RW = A.RW, NP = A.NP, rank = A.rank;
@@ -551,6 +563,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
   for (long long b = blockIdx.x; b < A.B; b += gridDim.x) {
     uint8_t* ow = A.outw + b * (long long)n;
     uint8_t* o0 = A.out0 ? A.out0 + b * (long long)n : nullptr;
+    if (A.win == 2 && ow[0] != kOsdRedo) continue;  // redo launch: only the window's overruns (uniform)
     if (A.shot && A.shot[b] < 0) continue;  // captured decode that converged at max_iter: no OSD
     if (A.conv && A.conv[b]) {  // BP converged: bposd_decoder returns the BP decoding
       for (int j = tid; j < n; j += TB) {
@@ -633,7 +646,8 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
       OSD_ST(1)
       int npiv = 0;   // uniform
       if constexpr (PNL == 3) {
-        // Blocked elimination (round 5; the default for register rows): the
+        // Blocked elimination (round 5; opt-in QLDPC_OSD_PNL=3, measured
+        // slower than the lean loop): the
         // per-pivot loops below cost every wave two barriers and a pivot-row round trip per pivot
         // (~2,100 cycles per pivot at n1600, 0.62 of wave cycles parked, profiles/r04/passt/).  Here
         // the pivots of a 32-column panel (half a row word) are found by ONE search wave with no
@@ -648,8 +662,7 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
         // same pivots, pivot rows and reduced rows as the per-pivot elimination (an unused row is zero
         // before the scan position, so the pivot rows' earlier words are zero and the words < q never
         // change).  Four barriers per panel instead of two per pivot.
-        static_assert(RPT == 1, "blocked mode: one row per thread");
-        constexpr int SM = LB / 64;  // row slots per lane of the search wave
+        constexpr int SM = (LB * RPT) / 64;  // row slots per lane of the search wave (rows s * 64 + lane)
         constexpr u64 kLo = 0xFFFFFFFFull, kHi = ~kLo;
         constexpr int TS = WR + 1;   // table entry stride: words of a start row + its syndrome bit
         uint32_t* pw = reinterpret_cast<uint32_t*>(smem + A.pnl_off);  // [m] panel half-words
@@ -674,7 +687,9 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
             if (q * 64 + h * 32 >= n || npiv >= rank) break;  // uniform
             // 1. every row's panel half-word (every earlier panel applied)
             unsigned long long tb0 = QLDPC_STAMPS ? osd_stamp() : 0ull;
-            if (tid < m) pw[tid] = (uint32_t)(row[0][q] >> (32 * h));
+#pragma unroll
+            for (int j = 0; j < RPT; ++j)
+              if (tid + j * TB < m) pw[tid + j * TB] = (uint32_t)(row[j][q] >> (32 * h));
             __syncthreads();
             if (QLDPC_STAMPS) {  // [11]: step 1 + its barrier
               const unsigned long long t = osd_stamp();
@@ -803,17 +818,23 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
             npiv = s_npiv;
             // 3. the panel's pivot rows publish their panel-start rows (words q.., syndrome bit) as
             // the single entries of their group's table; every row takes its final half-word and mask
-            uint32_t cmk = 0, fw = 0;
-            if (tid < m) {
-              cmk = pmsk[tid];
-              fw = pw[tid];
-              const int kx = pidx[tid];
-              if (kx >= 0 && kx < P && pk[kx] == tid) {  // (stale entries of earlier panels fail the check)
-                used_r[0] = true;
-                u64* d = T + (size_t)((kx >> 2) * 16 + (1 << (kx & 3))) * TS;
+            uint32_t cmk[RPT], fw[RPT];
 #pragma unroll
-                for (int q2 = q; q2 < WR; ++q2) d[q2] = row[0][q2];
-                d[WR] = sbit[0];
+            for (int j = 0; j < RPT; ++j) {
+              const int i = tid + j * TB;
+              cmk[j] = 0;
+              fw[j] = 0;
+              if (i < m) {
+                cmk[j] = pmsk[i];
+                fw[j] = pw[i];
+                const int kx = pidx[i];
+                if (kx >= 0 && kx < P && pk[kx] == i) {  // (stale entries of earlier panels fail the check)
+                  used_r[j] = true;
+                  u64* d = T + (size_t)((kx >> 2) * 16 + (1 << (kx & 3))) * TS;
+#pragma unroll
+                  for (int q2 = q; q2 < WR; ++q2) d[q2] = row[j][q2];
+                  d[WR] = sbit[j];
+                }
               }
             }
             __syncthreads();
@@ -841,19 +862,22 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
             // 5. every row: one table entry per group into everything past the panel (the high half
             // of word q when the panel is its low half, words q + 1.., the syndrome bit); the panel
             // half-word is the search's final value
-            if (tid < m) {
-              u64 accq = 0;
-              for (int g = 0; g < ng; ++g) {  // uniform bound
-                const uint32_t c = (cmk >> (4 * g)) & 15u;
-                if (c) {
-                  const u64* src = T + (size_t)(g * 16 + (int)c) * TS;
-                  accq ^= src[q];
 #pragma unroll
-                  for (int q2 = q + 1; q2 < WR; ++q2) row[0][q2] ^= src[q2];
-                  sbit[0] ^= (uint32_t)src[WR];
+            for (int j = 0; j < RPT; ++j) {
+              if (tid + j * TB < m) {
+                u64 accq = 0;
+                for (int g = 0; g < ng; ++g) {  // uniform bound
+                  const uint32_t c = (cmk[j] >> (4 * g)) & 15u;
+                  if (c) {
+                    const u64* src = T + (size_t)(g * 16 + (int)c) * TS;
+                    accq ^= src[q];
+#pragma unroll
+                    for (int q2 = q + 1; q2 < WR; ++q2) row[j][q2] ^= src[q2];
+                    sbit[j] ^= (uint32_t)src[WR];
+                  }
                 }
+                row[j][q] = h ? ((row[j][q] & kLo) | ((u64)fw[j] << 32)) : (((row[j][q] ^ accq) & kHi) | (u64)fw[j]);
               }
-              row[0][q] = h ? ((row[0][q] & kLo) | ((u64)fw << 32)) : (((row[0][q] ^ accq) & kHi) | (u64)fw);
             }
             if (QLDPC_STAMPS) st[10] += osd_stamp() - tb0;  // [10]: the row updates
             // (pw is rewritten by the next panel's step 1 after these reads; T behind its first two barriers)
@@ -1414,6 +1438,12 @@ __global__ void __launch_bounds__(LB) osd_gpu_kernel(OsdGpuArgs A) {
         }
       }
       }  // per-pivot elimination
+      if ((A.win == 1 || A.win == 3) && (npiv < rank || (A.win == 3 && (b & 1)))) {
+        // the pivots run past the column window (uniform): redo at full width
+        if (tid == 0) ow[0] = kOsdRedo;
+        __syncthreads();
+        continue;
+      }
       // reduced rows -> the HBM slice (word-major), syndrome bits -> sb
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
@@ -2133,6 +2163,7 @@ struct qldpc_osd_gpu {
   int rr_tb = 0;             // register-row mode: threads per workgroup = m rounded up to waves
   int pnl = 0, pnl_off = 0;  // register-row mode: panel elimination (QLDPC_OSD_PNL), its LDS area
   int nsy = 1, syn_lds = 0;  // register-row mode: syndromes per workgroup (osd_rr2_kernel), LDS per syndrome
+  int win_wr = 0, win_grid = 0;  // column window (osd_win_kernel): row words held, workgroups
   size_t lds = 0;
   long long ws_words = 0, iws_ints = 0;
   qldpc_rt::DevBuf rp, ci, ws, iws, softw;  // softw: [n] log(1 / p_j) when the priors are not uniform
@@ -2198,11 +2229,20 @@ namespace {
 // per thread: 2 or 3 rows per thread in 384 / 256 threads (fewer waves reading each broadcast
 // pivot word) measured 16 % / 26 % slower on n1600 (the per-pivot chain is latency-bound).
 constexpr int kOsdWR[] = {2, 4, 8, 12, 16, 20, 25};
-constexpr int osd_rpt(int) { return 1; }
-inline int osd_rr_threads(int wr) { return wr <= 16 ? 1024 : 768; }
+// rows per thread: 1, or 2 for the blocked elimination of the 20-25-word rows with QLDPC_OSD_RPT=2
+// (384-thread workgroups, two syndromes per CU, VGPRs pinned to 3 waves per SIMD).  MEASURED AND NOT
+// KEPT (opt-in): bit-exact (blk GPU tests), but the pinned budget spills 46 VGPRs and the n1600 BP+OSD
+// rate drops to 521 k shots/s vs 588 k with one row per thread (profiles/r05/osd_notkept/rpt2_*)
+inline int osd_rpt(int wr, int pnl) {
+  const char* e = std::getenv("QLDPC_OSD_RPT");
+  return (pnl == 3 && wr >= 20 && e && std::atoi(e) == 2) ? 2 : 1;
+}
+inline int osd_rr_threads(int wr, int pnl = 0) { return wr <= 16 ? 1024 : 768 / osd_rpt(wr, pnl); }
 using OsdKern = void (*)(OsdGpuArgs);
 template <int WR, int PNL>
-OsdKern osd_rr_wide(int) {
+OsdKern osd_rr_wide(int rpt) {
+  if constexpr (PNL == 3)  // blocked: two rows per thread, 384 threads, two syndromes per CU
+    if (rpt == 2) return &osd_gpu_kernel<384, WR, 2, 3>;
   return &osd_gpu_kernel<768, WR, 1, PNL>;
 }
 template <int PNL>
@@ -2213,14 +2253,32 @@ OsdKern osd_rr_kernel_t(int wr) {
     case 8: return &osd_gpu_kernel<1024, 8, 1, PNL>;
     case 12: return &osd_gpu_kernel<1024, 12, 1, PNL>;
     case 16: return &osd_gpu_kernel<1024, 16, 1, PNL>;
-    case 20: return osd_rr_wide<20, PNL>(osd_rpt(wr));
-    case 25: return osd_rr_wide<25, PNL>(osd_rpt(wr));
+    case 20: return osd_rr_wide<20, PNL>(osd_rpt(wr, PNL));
+    case 25: return osd_rr_wide<25, PNL>(osd_rpt(wr, PNL));
     default: return nullptr;
   }
 }
 OsdKern osd_rr_kernel(int wr, int pnl) {
   return pnl == 3 ? osd_rr_kernel_t<3>(wr) : pnl == 2 ? osd_rr_kernel_t<2>(wr) : pnl ? osd_rr_kernel_t<1>(wr)
                                                                                    : osd_rr_kernel_t<0>(wr);
+}
+// column-window kernels (register rows, m <= 768, no panel modes): the first WR row words only and
+// a VGPR budget of 6 waves per SIMD, i.e. two 768-thread workgroups per CU
+// (QLDPC_OSD_WPE=3: one workgroup per CU, no VGPR pinning -- A/B)
+constexpr int kOsdWinWR[] = {8, 12, 14, 16};
+template <int WPE>
+OsdKern osd_win_kernel_t(int wr) {
+  switch (wr) {
+    case 8: return &osd_gpu_kernel<768, 8, 1, 0, WPE>;
+    case 12: return &osd_gpu_kernel<768, 12, 1, 0, WPE>;
+    case 14: return &osd_gpu_kernel<768, 14, 1, 0, WPE>;
+    case 16: return &osd_gpu_kernel<768, 16, 1, 0, WPE>;
+    default: return nullptr;
+  }
+}
+OsdKern osd_win_kernel(int wr) {
+  const char* e = std::getenv("QLDPC_OSD_WPE");
+  return (e && std::atoi(e) == 3) ? osd_win_kernel_t<3>(wr) : osd_win_kernel_t<6>(wr);
 }
 OsdKern osd_rr2_kernel_of(int wr) {
 #if QLDPC_EXPERIMENTAL
@@ -2317,11 +2375,13 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
   // register-row mode (one row per thread of a 1024-thread workgroup, row words in VGPRs) when
   // m <= 1024 and n <= 2048; QLDPC_OSD_RR=0 keeps the LDS / HBM image
   const char* rr_env = std::getenv("QLDPC_OSD_RR");
+  const char* pnl_env = std::getenv("QLDPC_OSD_PNL");
+  const int want_pnl = pnl_env ? std::atoi(pnl_env) : 0;
   if (!rr_env || std::atoi(rr_env) != 0)
     for (int wr : kOsdWR)
       if (wr >= G->W) {
-        const int rpt = osd_rpt(wr);
-        if (m <= osd_rr_threads(wr) * rpt) {
+        const int rpt = osd_rpt(wr, want_pnl == 3 ? 3 : 0);
+        if (m <= osd_rr_threads(wr, want_pnl == 3 ? 3 : 0) * rpt) {
           G->wr = wr;
           G->rr_tb = std::max(64, ((m + rpt - 1) / rpt + 63) / 64 * 64);  // RPT rows per thread, no idle waves
         }
@@ -2339,9 +2399,8 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
   // wave's per-pivot chain (one wave alone issues a VALU op every 4 cycles) is longer than the two
   // barriers it saves: n1600 OSD-E(10) 6.66 vs 3.08 us per syndrome, BP+OSD 257k vs 490k shots/s
   // (profiles/r03/bposd_pnl/)
-  const char* pnl_env = std::getenv("QLDPC_OSD_PNL");
-  if (G->wr && pnl_env && std::atoi(pnl_env) != 0) {
-    const int pv = std::atoi(pnl_env);
+  if (G->wr && want_pnl != 0) {
+    const int pv = want_pnl;
     G->pnl = pv == 3 ? 3 : pv == 2 ? 2 : 1;  // 2: the distributed panel search (one barrier per pivot); 3: blocked
     G->pnl_off = (int)((G->lds + 15) & ~(size_t)15);
     G->lds = (size_t)G->pnl_off + (G->pnl == 3 ? osd_blk_bytes(m, G->wr) : osd_pnl_bytes(m, G->wr));
@@ -2353,6 +2412,29 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
     G->nsy = 2;
     G->syn_lds = (int)((G->lds + 15) & ~(size_t)15);
     G->lds = 2 * (size_t)G->syn_lds;
+  }
+  // column window (register rows, one syndrome per workgroup, the lean loop): the elimination
+  // stops once rank pivots are found, and only the positions < rank + nh are read after it (the
+  // pivots and the non-pivot columns Ht[0..nh)), so the rows need only the first words that
+  // cover rank + nh + kOsdWinSlack positions; a syndrome whose pivots run past them (more than
+  // ~kOsdWinSlack dependent positions before the rank) is redone at full width by a second
+  // launch.  Opt-in: QLDPC_OSD_WIN=1 picks the width, =<words> forces one.  MEASURED AND NOT KEPT:
+  // bit-exact (64 BP+OSD GPU tests), but on the reference codes the rank is reached only near
+  // the END of the reliability order (hgp_34_n1600 at p = 0.04: last pivot at position 1419-1538
+  // of 1600, tools/dev/osd_last_pivot.py), so nearly every syndrome overruns a 14-word window and
+  // pays twice: 491 k BP+OSD shots/s vs 615 k at full width (profiles/r05/osd_notkept/window_*).
+  const char* win_env = std::getenv("QLDPC_OSD_WIN");
+  const int win_force = win_env ? std::atoi(win_env) : 0;
+  if (G->wr && !G->pnl && G->nsy == 1 && m <= 768 && win_force > 0 && QLDPC_OSD_LEAN && !kOsdM4R && !QLDPC_OSD_1B) {
+    const long long need = (long long)rank + G->nh;
+    for (int ww : kOsdWinWR) {
+      const bool fits = win_force > 1 ? ww == win_force && (long long)ww * 64 >= need
+                                      : (long long)ww * 64 >= need + kOsdWinSlack;
+      if (fits) {
+        if (ww < G->wr) G->win_wr = ww;
+        break;
+      }
+    }
   }
   // non-uniform priors: the candidates' column-space vectors Xc [(1 + nh)][W] after X, and the
   // column -> pivot map [n] after the sort maps
@@ -2378,10 +2460,18 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
                                                    G->lds) != hipSuccess || nb <= 0)
     nb = 1;
   G->grid = cus * nb;
+  if (G->win_wr) {
+    int nbw = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbw, reinterpret_cast<const void*>(osd_win_kernel(G->win_wr)),
+                                                     G->rr_tb, G->lds) != hipSuccess || nbw <= 0)
+      nbw = 1;
+    G->win_grid = cus * nbw;
+  }
+  const int slices = std::max(G->grid, G->win_grid);
   const size_t E = g->col_idx.size();
   if ((rc = G->rp.alloc((size_t)(m + 1) * 4)) || (rc = G->ci.alloc(std::max<size_t>(E, 1) * 4)) ||
-      (rc = G->ws.alloc((size_t)G->grid * G->nsy * G->ws_words * 8)) ||
-      (rc = G->iws.alloc((size_t)G->grid * G->nsy * G->iws_ints * 4)) ||
+      (rc = G->ws.alloc((size_t)slices * G->nsy * G->ws_words * 8)) ||
+      (rc = G->iws.alloc((size_t)slices * G->nsy * G->iws_ints * 4)) ||
       (!G->host.uniform && (rc = G->softw.alloc((size_t)n * 8))))
     return fail(rc);
   if (!G->host.uniform && hipMemcpy(G->softw.p, G->host.w.data(), (size_t)n * 8, hipMemcpyHostToDevice) != hipSuccess)
@@ -2394,6 +2484,16 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
 }
 
 extern "C" {
+
+int qldpc_osd_gpu_geometry(const qldpc_osd_gpu* osd, int32_t* row_words, int32_t* window_words, int32_t* threads,
+                           int32_t* workgroups) {
+  if (!osd || !row_words || !window_words || !threads || !workgroups) return set_err(QLDPC_EINVAL, "NULL argument");
+  *row_words = osd->wr;
+  *window_words = osd->win_wr;
+  *threads = osd->wr ? osd->rr_tb : osd->m_lds ? kOsdThreadsLds : kOsdThreads;
+  *workgroups = osd->win_wr ? osd->win_grid : osd->grid;
+  return 0;
+}
 
 int qldpc_osd_gpu_destroy(qldpc_osd_gpu* osd) {
   if (!osd) return 0;
@@ -2438,8 +2538,17 @@ int osd_gpu_decode_slots(qldpc_osd_gpu* osd, const uint8_t* d_synd, const double
   a.pnl_off = osd->pnl_off;
   a.syn_lds = osd->syn_lds;
   a.ws_words = osd->ws_words; a.iws_ints = osd->iws_ints;
+  a.win = 0;
   const int grid = (int)std::min<long long>((B + osd->nsy - 1) / osd->nsy, osd->grid);
-  if (osd->nsy == 2)
+  if (osd->win_wr) {  // the column window, then the full-width redo of its overruns
+    const char* tr = std::getenv("QLDPC_OSD_WIN_REDO");
+    a.win = (tr && std::atoi(tr) == 1) ? 3 : 1;
+    hipLaunchKernelGGL(osd_win_kernel(osd->win_wr), dim3((int)std::min<long long>(B, osd->win_grid)), dim3(osd->rr_tb),
+                       osd->lds, (hipStream_t)stream, a);
+    QLDPC_HIP(hipGetLastError());
+    a.win = 2;
+    hipLaunchKernelGGL(osd_rr_kernel(osd->wr, 0), dim3(grid), dim3(osd->rr_tb), osd->lds, (hipStream_t)stream, a);
+  } else if (osd->nsy == 2)
     hipLaunchKernelGGL(osd_rr2_kernel_of(osd->wr), dim3(grid), dim3(osd->rr_tb), osd->lds, (hipStream_t)stream, a);
   else if (osd->wr)
     hipLaunchKernelGGL(osd_rr_kernel(osd->wr, osd->pnl), dim3(grid), dim3(osd->rr_tb), osd->lds, (hipStream_t)stream, a);

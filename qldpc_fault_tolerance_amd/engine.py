@@ -311,6 +311,14 @@ class DeviceOSD:
                       "qldpc_osd_gpu_create")
         self.handle = h
 
+    def geometry(self) -> dict:
+        """The elimination layout the handle chose: register-row words, column-window words (0 =
+        none), threads per workgroup and the persistent grid."""
+        v = [ctypes.c_int32() for _ in range(4)]
+        _native.check(_native.lib().qldpc_osd_gpu_geometry(self.handle, *[ctypes.byref(x) for x in v]),
+                      "qldpc_osd_gpu_geometry")
+        return dict(zip(("row_words", "window_words", "threads", "workgroups"), (x.value for x in v)))
+
     def decode_device(self, synd_dev, post_dev, conv_dev, corr_dev, out0_dev, outw_dev, stream=None):
         torch = _torch()
         B = int(synd_dev.shape[0])

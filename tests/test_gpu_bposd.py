@@ -137,7 +137,14 @@ def test_bposd_shot_loop_matches_oracle_per_shot(gpu, oracle):
 # and the opt-in panel eliminations of the register rows (QLDPC_OSD_PNL=1: one search wave; 2: every
 # thread searches its own row, one barrier per pivot; both measured slower)
 _OSD_MODES = {"default": {}, "lds": {"QLDPC_OSD_RR": "0"}, "hbm": {"QLDPC_OSD_RR": "0", "QLDPC_OSD_LDS": "0"},
-              "pnl1": {"QLDPC_OSD_PNL": "1"}, "pnl2": {"QLDPC_OSD_PNL": "2"}, "blk": {"QLDPC_OSD_PNL": "3"}}
+              "pnl1": {"QLDPC_OSD_PNL": "1"}, "pnl2": {"QLDPC_OSD_PNL": "2"}, "blk": {"QLDPC_OSD_PNL": "3"},
+              "blk2": {"QLDPC_OSD_PNL": "3", "QLDPC_OSD_RPT": "2"},
+              # the opt-in column window (measured slower): its own width (rank + nh
+              # + 64 positions), forced to 8 words, its full-width redo exercised on every odd
+              # syndrome, and the one-workgroup-per-CU build of the window kernel
+              "win": {"QLDPC_OSD_WIN": "1"}, "win8": {"QLDPC_OSD_WIN": "8"},
+              "winredo": {"QLDPC_OSD_WIN": "1", "QLDPC_OSD_WIN_REDO": "1"},
+              "wpe3": {"QLDPC_OSD_WIN": "1", "QLDPC_OSD_WPE": "3"}}
 
 
 @pytest.mark.parametrize("name,t0,method,order,mode", [
@@ -148,7 +155,13 @@ _OSD_MODES = {"default": {}, "lds": {"QLDPC_OSD_RR": "0"}, "hbm": {"QLDPC_OSD_RR
     ("hgp_34_n1600", 0, "osd_e", 10, "pnl1"), ("hgp_34_n225", 3, "osd_e", 8, "pnl1"),
     ("hgp_34_n225", 0, "osd_cs", 8, "pnl2"), ("hgp_34_n1600", 0, "osd_e", 10, "pnl2"), ("hgp_34_n225", 3, "osd_e", 8, "pnl2"),
     ("hgp_34_n225", 0, "osd_e", 10, "blk"), ("hgp_34_n225", 0, "osd_cs", 8, "blk"), ("hgp_34_n1600", 0, "osd_e", 10, "blk"),
-    ("hgp_34_n1600", 0, "osd_cs", 6, "blk"), ("hgp_34_n225", 3, "osd_e", 8, "blk"), ("LP_Matg8_L30_Dmin20", 0, "osd_e", 10, "blk")])
+    ("hgp_34_n1600", 0, "osd_cs", 6, "blk"), ("hgp_34_n225", 3, "osd_e", 8, "blk"), ("LP_Matg8_L30_Dmin20", 0, "osd_e", 10, "blk"),
+    ("hgp_34_n1600", 0, "osd_e", 10, "win"), ("hgp_34_n1600", 0, "osd_e", 10, "winredo"),
+    ("hgp_34_n1600", 0, "osd_e", 10, "blk2"),
+    ("hgp_34_n1600", 0, "osd_e", 10, "wpe3"), ("hgp_34_n1600", 0, "osd_0", 0, "win"),
+    ("LP_Matg8_L30_Dmin20", 0, "osd_e", 10, "win"), ("LP_Matg8_L30_Dmin20", 0, "osd_e", 10, "win8"),
+    ("LP_Matg8_L30_Dmin20", 0, "osd_e", 20, "winredo"), ("hgp_34_n225", 3, "osd_e", 8, "winredo"),
+    ("hgp_34_n225", 3, "osd_0", 0, "win8")])
 def test_gpu_osd_matches_host_osd(gpu, monkeypatch, name, t0, method, order, mode):
     """GPU OSD kernel == native host OSD stage (itself pinned to the oracle in
     tests/test_osd_cpu.py) on GPU soft-BP posteriors, incl. a rank-deficient space-time graph
@@ -166,6 +179,13 @@ def test_gpu_osd_matches_host_osd(gpu, monkeypatch, name, t0, method, order, mod
     synd, _ = _sample(H, p, 192, seed=len(method) + order)
     bp = DeviceBP(H, p, max_iter=max(1, int(code.N / 10)), ms_scaling_factor=0.625, precision=64, soft=True)
     osd = DeviceOSD(bp.graph, np.full(n, p), method, order)
+    geo = osd.geometry()
+    if mode == "win8":
+        assert geo["window_words"] == 8
+    elif mode not in ("win", "winredo", "wpe3") or method == "osd_cs" or n < 500:
+        assert geo["window_words"] == 0
+    else:  # rank + nh + 64 positions fit fewer words than the rows
+        assert 0 < geo["window_words"] < geo["row_words"], geo
     ow, o0, corr, iters, conv, post = osd.bposd_batch(bp, synd)
     assert (~conv).sum() > 0
     h0, hw = HostOSD(H, np.full(n, p), method, order).decode_batch(synd, post, conv, corr)
@@ -180,7 +200,8 @@ def test_gpu_osd_matches_host_osd(gpu, monkeypatch, name, t0, method, order, mod
     ("hgp_34_n1600", "osd_e", 10, "default"), ("hgp_34_n225", "osd_e", 10, "lds"), ("hgp_34_n225", "osd_e", 8, "hbm"),
     ("circuit_h2_all3c", "osd_e", 10, "default"), ("circuit_h2_demo", "osd_e", 10, "default"),
     ("hgp_34_n1600", "osd_e", 10, "blk"), ("circuit_h1_all3r", "osd_cs", 6, "blk"),
-    ("circuit_h1_all3r", "osd_cs", 6, "default")])
+    ("circuit_h1_all3r", "osd_cs", 6, "default"), ("hgp_34_n1600", "osd_e", 10, "winredo"),
+    ("hgp_34_n1600", "osd_e", 10, "win")])
 def test_gpu_osd_nonuniform_priors_matches_oracle(gpu, oracle, monkeypatch, name, method, order, mode):
     """GPU OSD with NON-uniform channel_probs (the circuit-level final round
     ST_BPOSD_Decoder_Circuit(h2, channel_ps2, ...), src/Decoders_SpaceTime.py:277-292): candidates
