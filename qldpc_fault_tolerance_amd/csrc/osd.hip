@@ -890,6 +890,117 @@ osd_gpu_kernel(OsdGpuArgs A) {
           pivrow[i] = v & 2047;
           pivpos[i] = v >> 11;
         }
+      } else if constexpr (PNL == 4) {
+        // Lagged one-barrier loop (round 5; QLDPC_OSD_PNL=4).  The lean loop below walks two
+        // barriers and four dependent LDS round trips per pivot (search max, barrier, winner read,
+        // publication, barrier, pivot-row reads).  Here only the pivot WORD q is applied at once:
+        // before the search barrier every wave's best candidate row also leaves its word q in a
+        // per-wave slot, so after the barrier each row reads the winner and the winning wave's
+        // slot and updates its word q -- the next search reads nothing else.  The pivot's other
+        // words (and syndrome bit) are published by its owner after that barrier and applied one
+        // step later, after the next barrier (the owner of the next pivot applies them before it
+        // publishes its own row); at a word's end, and when the rank is reached, one extra barrier
+        // flushes the pending row.  Same pivots and the same reduced rows as the lean loop; one
+        // barrier per pivot.  Slots, winner words and pivot-row buffers are double-buffered by
+        // step / pivot parity: a buffer is rewritten two barriers after it was read.
+        // MEASURED AND NOT KEPT (opt-in): bit-exact (10 GPU tests incl. non-uniform priors and
+        // circuit graphs), but n1600 BP+OSD-E(10) 578 k vs 616 k shots/s with the lean loop
+        // (profiles/r05/osd_notkept/lag_*): the pending row xor and the slot round trip stay on
+        // every wave's path between two barriers, so halving the barriers shortens nothing.
+        static_assert(RPT == 1, "lagged loop: one row per thread");
+        __shared__ uint32_t s_pv[2];        // per step parity: (step << 17) | (0x1FFFF - key), max over waves
+        __shared__ u64 s_slot[2][LB / 64];  // per step parity and wave: word q of the wave's best row
+        int32_t* lkk = reinterpret_cast<int32_t*>(smem);  // pivots over the dead sort keys, as the lean loop
+        const uint32_t pv_a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&s_pv[0]);
+        if (tid < 2) s_pv[tid] = 0u;
+        __syncthreads();
+        uint32_t step = 0;  // uniform
+        uint32_t um = used_r[0] ? 0u : ~0u;
+        const int wv = tid >> 6;
+        bool pend = false;  // uniform: a pivot row waits in pbuf half pp
+        int pp = 0;
+        bool phb = false;   // this row takes the pending pivot row (it had the pivot bit, not its owner)
+#pragma unroll
+        for (int q = 0; q < WR; ++q) {
+          if (q * 64 >= n || npiv >= rank) break;  // uniform
+          const int bend = n - q * 64 < 64 ? n - q * 64 : 64;
+          const u64 wmask = bend < 64 ? (1ull << bend) - 1ull : ~0ull;
+          // the pending pivot row's words q+1.. and syndrome bit (published before the last barrier)
+          auto apply_pending = [&]() __attribute__((always_inline)) {
+            if (pend) {  // uniform
+              const u64* pr = pbuf + (size_t)pp * (WR + 1);
+              if (phb) {
+                constexpr int XB = kOsdXB;
+                u64 buf[XB];
+#pragma unroll
+                for (int u = 0; u < XB; ++u)
+                  if (q + 1 + u < WR) buf[u] = pr[q + 1 + u];
+                const uint32_t ps = (uint32_t)pr[WR];
+#pragma unroll
+                for (int q2 = q + 1; q2 < WR; ++q2) {
+                  const u64 pv = buf[(q2 - q - 1) % XB];
+                  if (q2 + XB < WR) buf[(q2 - q - 1) % XB] = pr[q2 + XB];
+                  row[0][q2] ^= pv;
+                }
+                sbit[0] ^= ps;
+              }
+              pend = false;
+            }
+          };
+          int b = 0;
+          for (;;) {  // uniform
+            ++step;
+            asm volatile("" : "+s"(step));
+            const int par = (int)(step & 1u);
+            if (QLDPC_STAMPS) st[7] += 1;
+            const u64 lowm = (~0ull << b) & wmask;
+            const uint32_t ml = (uint32_t)row[0][q] & (uint32_t)lowm & um;
+            const uint32_t mh = (uint32_t)(row[0][q] >> 32) & (uint32_t)(lowm >> 32) & um;
+            const uint32_t fl = ffbl_u32(ml), fh = ffbl_u32(mh) | 32u;
+            const uint32_t f = fl < fh ? fl : fh;
+            const uint32_t key0 = (f << 11) | (uint32_t)tid;
+            const uint32_t key = wave_min_u32_bc(key0);
+            if (key <= 0x1FFFFu) {  // uniform per wave
+              if (key0 == key) s_slot[par][wv] = row[0][q];
+              if ((tid & 63) == 0) lds_max_u32_sync(pv_a + 4u * (uint32_t)par, (step << 17) | (0x1FFFFu - key));
+            }
+            __syncthreads();
+            const uint32_t vx = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_pv[par]);  // uniform
+            apply_pending();
+            if ((vx >> 17) != step) break;  // no pivot left in this word (uniform; nothing pending)
+            const uint32_t kk = 0x1FFFFu - (vx & 0x1FFFFu);
+            const int fb = (int)(kk >> 11), r = (int)(kk & 2047u);
+            const u64 pw = s_slot[par][r >> 6];
+            const bool hb = ((row[0][q] >> fb) & 1ull) != 0;
+            const bool own = tid == r;
+            if (hb && !own) row[0][q] ^= pw;
+            if (own) {
+              used_r[0] = true;
+              um = 0u;
+              u64* pr = pbuf + (size_t)(npiv & 1) * (WR + 1);
+#pragma unroll
+              for (int q2 = q + 1; q2 < WR; ++q2) pr[q2] = row[0][q2];
+              pr[WR] = sbit[0];
+              lkk[npiv] = ((q * 64 + fb) << 11) | r;
+            }
+            pend = true;
+            pp = npiv & 1;
+            phb = hb && !own;
+            ++npiv;
+            b = fb + 1;
+            if (b >= bend || npiv >= rank) {  // uniform: flush the pending row before the next word
+              __syncthreads();
+              apply_pending();
+              break;
+            }
+          }
+        }
+        // the pivot list -> pivrow / pivpos (every lkk write precedes one of the loop's barriers)
+        for (int i = tid; i < npiv; i += TB) {
+          const int v = lkk[i];
+          pivrow[i] = v & 2047;
+          pivpos[i] = v >> 11;
+        }
       } else if constexpr (PNL) {
         static_assert(RPT == 1, "panel mode: one row per thread");
         constexpr int SM = LB / 64;  // row slots per lane of the search wave (rows s * 64 + lane)
@@ -1578,7 +1689,7 @@ osd_gpu_kernel(OsdGpuArgs A) {
     // (Register-row mode stages pivpos in LDS first: the trace reads it r times.)
     const int32_t* pp = pivpos;
     if constexpr (kRR) {
-      int32_t* lpp = reinterpret_cast<int32_t*>(smem + A.pbuf_off + (size_t)osd_prows(LB) * (WR + 1) * 8);
+      int32_t* lpp = reinterpret_cast<int32_t*>(smem + A.pbuf_off + (size_t)(osd_prows(LB) + (PNL == 4 ? 1 : 0)) * (WR + 1) * 8);
       for (int i = tid; i < r; i += TB) lpp[i] = pivpos[i];
       __syncthreads();
       pp = lpp;
@@ -2259,7 +2370,7 @@ OsdKern osd_rr_kernel_t(int wr) {
   }
 }
 OsdKern osd_rr_kernel(int wr, int pnl) {
-  return pnl == 3 ? osd_rr_kernel_t<3>(wr) : pnl == 2 ? osd_rr_kernel_t<2>(wr) : pnl ? osd_rr_kernel_t<1>(wr)
+  return pnl == 4 ? osd_rr_kernel_t<4>(wr) : pnl == 3 ? osd_rr_kernel_t<3>(wr) : pnl == 2 ? osd_rr_kernel_t<2>(wr) : pnl ? osd_rr_kernel_t<1>(wr)
                                                                                    : osd_rr_kernel_t<0>(wr);
 }
 // column-window kernels (register rows, m <= 768, no panel modes): the first WR row words only and
@@ -2401,9 +2512,12 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
   // (profiles/r03/bposd_pnl/)
   if (G->wr && want_pnl != 0) {
     const int pv = want_pnl;
-    G->pnl = pv == 3 ? 3 : pv == 2 ? 2 : 1;  // 2: the distributed panel search (one barrier per pivot); 3: blocked
+    G->pnl = pv == 4 ? 4 : pv == 3 ? 3 : pv == 2 ? 2 : 1;  // 2: the distributed panel search (one barrier per pivot); 3: blocked
     G->pnl_off = (int)((G->lds + 15) & ~(size_t)15);
-    G->lds = (size_t)G->pnl_off + (G->pnl == 3 ? osd_blk_bytes(m, G->wr) : osd_pnl_bytes(m, G->wr));
+    if (G->pnl == 4)  // the lagged loop: a second pivot-row buffer (the pivpos staging moves behind it)
+      G->lds += (size_t)(G->wr + 1) * 8;
+    else
+      G->lds = (size_t)G->pnl_off + (G->pnl == 3 ? osd_blk_bytes(m, G->wr) : osd_pnl_bytes(m, G->wr));
   }
   // two syndromes per workgroup (osd_rr2_kernel, the 768-thread register-row kernels): a second LDS
   // area and HBM slice per workgroup; QLDPC_OSD_NSY=1 keeps one
