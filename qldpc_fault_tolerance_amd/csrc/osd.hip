@@ -373,6 +373,15 @@ constexpr uint8_t kOsdRedo = 0xFF;
 // column window: positions past rank + nh the window words cover (dependent positions allowed
 // before the rank is reached)
 constexpr int kOsdWinSlack = 64;
+// forward elimination (PNL 5): bytes of the compaction staging area (64 rows in, 64 out)
+__host__ __device__ inline size_t osd_fwd_stg_bytes(int wr) { return 2 * ((size_t)wr * 64 * 8 + 64 * 4); }
+// forward elimination: U words of pivot row k over pivot block B >= k / 64, packed upper-triangular
+// by blocks (block b's 64 rows hold RW - b words each)
+__host__ __device__ inline int osd_ul_at(int k, int B, int RW) {
+  const int b = k >> 6;
+  return 64 * (b * RW - (b * (b - 1)) / 2 + (B - b)) + (k & 63);
+}
+__host__ __device__ inline int osd_ul_words(int RW) { return 64 * (RW * (RW + 1) / 2); }
 // register-row mode: pivot-row words read per batch ahead of their xors
 #ifndef QLDPC_OSD_XB
 #define QLDPC_OSD_XB 8
@@ -403,6 +412,11 @@ constexpr int kOsdXB = QLDPC_OSD_XB;
 #define QLDPC_OSD_G 4
 #endif
 constexpr bool kOsdM4R = QLDPC_OSD_M4R && !QLDPC_OSD_1B;
+// diagnostic A/B build: the lean loop's row xors done three times (same rows): the step's
+// sensitivity to its row-update VALU work
+#ifndef QLDPC_OSD_XOR3
+#define QLDPC_OSD_XOR3 0
+#endif
 // blocked mode (PNL 3): byte offset of the Four-Russians tables in the panel area (after the
 // half-words and masks [m] u32, pk [32], pidx [m]) and the area's size with them ([8][16][WR + 1] u64)
 __host__ __device__ inline size_t osd_blk_tab_off(int m) { return ((size_t)12 * m + 128 + 15) & ~(size_t)15; }
@@ -889,6 +903,164 @@ osd_gpu_kernel(OsdGpuArgs A) {
           const int v = lkk[i];
           pivrow[i] = v & 2047;
           pivpos[i] = v >> 11;
+        }
+      } else if constexpr (PNL == 5) {
+        // Forward elimination with compaction (round 5; QLDPC_OSD_PNL=5, osd_0 / osd_e).  A pivot
+        // step costs every wave its search and its row xors (the step is VALU-bound: xoring the
+        // pivot row three times instead of once made the lean loop's OSD 47 % slower,
+        // profiles/r05/osd_notkept/xor3_*).  Gauss-Jordan xors the pivot row into EVERY row that has
+        // the bit; plain forward elimination only into the unused rows, and every 64 pivots the
+        // unused rows are packed into the leading waves (words q.. through an LDS staging area), so
+        // the trailing waves drop out of the search and the xors: about half of both.  A pivot row
+        // is final when chosen; the rows stay in registers (a compaction swaps the <= 64 rows used
+        // since the last one out of the leading slots against the unused rows behind them, through
+        // a 64-row LDS staging area) and go to the HBM slice once at the end, as row (pivot
+        // index) -- a per-pivot global store would hold its wave at every barrier.  The rows' U
+        // bits (bit p_k of pivot row i, k > i) are taken as the pivots come (a frozen row's bit
+        // at the pivot position) and kept in LDS by blocks of 64 pivots (osd_ul_at).  The
+        // Jordan half is done afterwards on the (1 + nh)-bit right-hand sides only (syndrome bit,
+        // the nh non-pivot columns Ht): U x = b by blocks of 64 pivots (after step 4 below).  Same
+        // pivots (lexicographic minimum of (first bit, ORIGINAL row)), same S0 / x(h_j).
+        static_assert(RPT == 1, "forward elimination: one row per thread");
+        int32_t* lkk = reinterpret_cast<int32_t*>(smem);  // pivots: (sbit << 24) | (position << 11) | row
+        u64* stgA = reinterpret_cast<u64*>(smem + A.pnl_off);  // [WR][64] words of the rows moving in
+        u64* stgB = stgA + (size_t)WR * 64;                     // [WR][64] words of the rows moving out
+        uint32_t* siA = reinterpret_cast<uint32_t*>(stgB + (size_t)WR * 64);  // [64] row | sbit << 11 | (pivot + 1) << 12
+        uint32_t* siB = siA + 64;
+        u64* Ul = reinterpret_cast<u64*>(smem + A.pnl_off + osd_fwd_stg_bytes(WR));  // U words, osd_ul_at
+        __shared__ u64 s_bal[LB / 64];
+        const uint32_t pivx_a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(&s_pivx);
+        uint32_t step = 0;  // uniform
+        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
+        int rid = tid < m ? tid : 2047;       // original row of the slot
+        uint32_t um = used_r[0] ? 0u : ~0u;   // ~0 while the slot holds an unused row
+        int pk = -1;                          // pivot index of the slot's row (-1: not a pivot row)
+        u64 cu = 0;                           // the row's U bits over the pivots of block fl
+        int fl = 0;                           // uniform: U blocks flushed
+        int nact = ((m < TB ? m : TB) + 63) >> 6;  // uniform: waves that may hold unused rows
+        int ncomp = 64;                       // uniform: next compaction at npiv == ncomp
+        // one compile-time word q per call (a runtime q would index the row registers and put
+        // them in scratch; the body is too large for the unroller); false = stop
+        auto fwd_word = [&](auto qc) __attribute__((always_inline)) -> bool {
+          constexpr int q = decltype(qc)::value;
+          if (q * 64 >= n || npiv >= rank) return false;  // uniform
+          const int bend = n - q * 64 < 64 ? n - q * 64 : 64;
+          const u64 wmask = bend < 64 ? (1ull << bend) - 1ull : ~0ull;
+          int b = 0;
+          for (;;) {  // uniform
+            if (npiv >= ncomp) {  // uniform: permute the slots, unused rows first (stable)
+              const unsigned long long tc0 = QLDPC_STAMPS ? osd_stamp() : 0ull;
+              ncomp += 64;
+              if (pk >= 0) Ul[osd_ul_at(pk, fl, RW)] = cu;  // block fl of the U bits is complete
+              cu = 0;
+              ++fl;
+              const bool u = um != 0u;
+              const unsigned long long bal = __ballot(u);
+              if ((tid & 63) == 0) s_bal[wv] = bal;
+              __syncthreads();
+              // lane l reads wave l's ballot (one LDS round trip); sums by readlane (SALU adds)
+              const int ln = tid & 63;
+              const unsigned long long bl = ln < (TB >> 6) ? s_bal[ln] : 0ull;
+              const int cl = (int)__popcll(bl);
+              int base = 0, tot = 0;  // unused rows in slots before this wave's / in all
+#pragma unroll
+              for (int w2 = 0; w2 < LB / 64; ++w2) {
+                const int cw = __builtin_amdgcn_readlane(cl, w2);
+                base += w2 < wv ? cw : 0;
+                tot += cw;
+              }
+              const int tw = tot >> 6;
+              const int ul = ln < tw ? cl : (ln == tw ? (int)__popcll(bl & ((1ull << (tot & 63)) - 1ull)) : 0);
+              int Ut = 0;  // unused rows in slots < tot (uniform)
+#pragma unroll
+              for (int w2 = 0; w2 < LB / 64; ++w2) Ut += __builtin_amdgcn_readlane(ul, w2);
+              const int Us = base + (int)__popcll(bal & ((1ull << (tid & 63)) - 1ull));
+              // holes: used rows in slots < tot; movers: unused rows in slots >= tot (as many)
+              const bool hole = !u && tid < tot, mover = u && tid >= tot;
+              const int hi = hole ? tid - Us : Us - Ut;
+              if (hole || mover) {
+                u64* dp = hole ? stgB : stgA;
+#pragma unroll
+                for (int q2 = 0; q2 < WR; ++q2) dp[(size_t)q2 * 64 + hi] = row[0][q2];
+                (hole ? siB : siA)[hi] = (uint32_t)rid | (sbit[0] << 11) | ((uint32_t)(pk + 1) << 12);
+              }
+              __syncthreads();  // (the staging is next written 64 pivots = 128 barriers later)
+              if (hole || mover) {
+                const u64* sp = hole ? stgA : stgB;
+#pragma unroll
+                for (int q2 = 0; q2 < WR; ++q2) row[0][q2] = sp[(size_t)q2 * 64 + hi];
+                const uint32_t v = (hole ? siA : siB)[hi];
+                rid = (int)(v & 2047u);
+                sbit[0] = (v >> 11) & 1u;
+                pk = (int)(v >> 12) - 1;
+                um = hole ? ~0u : 0u;
+              }
+              nact = __builtin_amdgcn_readfirstlane((tot + 63) >> 6);
+              if (QLDPC_STAMPS) st[15] += osd_stamp() - tc0;
+            }
+            ++step;
+            if (QLDPC_STAMPS) st[7] += 1;
+            if (wv < nact) {  // uniform per wave
+              const u64 lowm = (~0ull << b) & wmask;
+              const uint32_t ml = (uint32_t)row[0][q] & (uint32_t)lowm & um;
+              const uint32_t mh = (uint32_t)(row[0][q] >> 32) & (uint32_t)(lowm >> 32) & um;
+              const uint32_t fl = ffbl_u32(ml), fh = ffbl_u32(mh) | 32u;
+              const uint32_t f = fl < fh ? fl : fh;
+              const uint32_t key = wave_min_u32_bc((f << 11) | (uint32_t)rid);
+              if ((tid & 63) == 0 && key <= 0x1FFFFu) lds_max_u32_sync(pivx_a, (step << 17) | (0x1FFFFu - key));
+            }
+            __syncthreads();
+            const uint32_t vx = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_pivx);  // uniform
+            if ((vx >> 17) != step) break;  // no pivot left in this word (uniform)
+            const uint32_t kk = 0x1FFFFu - (vx & 0x1FFFFu);
+            const int fb = (int)(kk >> 11), r = (int)(kk & 2047u);
+            const bool hbit = ((row[0][q] >> fb) & 1ull) != 0;
+            const bool upd = um != 0u && hbit && rid != r;
+            if (pk >= 0 && hbit) cu |= 1ull << (npiv & 63);  // a frozen pivot row: U bit
+            if (um != 0u && rid == r) {  // the pivot's owner: publish and record
+              um = 0u;
+              pk = npiv;
+#pragma unroll
+              for (int q2 = q; q2 < WR; ++q2) pbuf[q2] = row[0][q2];
+              pbuf[WR] = sbit[0];
+              lkk[npiv] = (int)((sbit[0] << 24) | ((uint32_t)(q * 64 + fb) << 11) | (uint32_t)r);
+            }
+            ++npiv;
+            __syncthreads();
+            if (upd) {  // pivot-row words through the rolling buffer, as the lean loop
+              constexpr int XB = kOsdXB;
+              u64 buf[XB];
+#pragma unroll
+              for (int u2 = 0; u2 < XB; ++u2)
+                if (q + u2 < WR) buf[u2] = pbuf[q + u2];
+              const uint32_t ps = (uint32_t)pbuf[WR];
+#pragma unroll
+              for (int q2 = q; q2 < WR; ++q2) {
+                const u64 pv = buf[(q2 - q) % XB];
+                if (q2 + XB < WR) buf[(q2 - q) % XB] = pbuf[q2 + XB];
+                row[0][q2] ^= pv;
+              }
+              sbit[0] ^= ps;
+            }
+            b = fb + 1;
+            if (b >= bend || npiv >= rank) break;  // uniform
+          }
+          return true;
+        };
+        osd_for_words(std::make_integer_sequence<int, WR>{}, fwd_word);
+        if (pk >= 0 && npiv > fl * 64) Ul[osd_ul_at(pk, fl, RW)] = cu;  // the last block's U bits
+        if (pk >= 0) {  // the pivot rows -> the HBM slice, row = pivot index
+          u64* mrow = Mg + pk;
+          asm volatile("" : "+v"(mrow));
+#pragma unroll
+          for (int q2 = 0; q2 < WR; ++q2)
+            if (q2 < W) mrow[(size_t)q2 * m] = row[0][q2];
+        }
+        // the pivot list -> pivrow / pivpos (every lkk write precedes one of the loop's barriers)
+        for (int i = tid; i < npiv; i += TB) {
+          const int v = lkk[i];
+          pivrow[i] = v & 2047;
+          pivpos[i] = (v >> 11) & 0x1FFF;
         }
       } else if constexpr (PNL == 4) {
         // Lagged one-barrier loop (round 5; QLDPC_OSD_PNL=4).  The lean loop below walks two
@@ -1418,7 +1590,16 @@ osd_gpu_kernel(OsdGpuArgs A) {
                 const u64 pv = buf[(q2 - q) % XB];
                 if (q2 + XB < WR) buf[(q2 - q) % XB] = pbuf[q2 + XB];
 #pragma unroll
-                for (int j = 0; j < RPT; ++j) row[j][q2] ^= upd[j] ? pv : 0ull;
+                for (int j = 0; j < RPT; ++j) {
+                  u64 t = upd[j] ? pv : 0ull;
+                  row[j][q2] ^= t;
+                  if (QLDPC_OSD_XOR3) {  // diagnostic: the same xor twice more (same result, 3x the work)
+                    asm volatile("" : "+v"(t));
+                    row[j][q2] ^= t;
+                    asm volatile("" : "+v"(t));
+                    row[j][q2] ^= t;
+                  }
+                }
               }
 #pragma unroll
               for (int j = 0; j < RPT; ++j) sbit[j] ^= upd[j] ? ps : 0u;
@@ -1555,9 +1736,10 @@ osd_gpu_kernel(OsdGpuArgs A) {
         __syncthreads();
         continue;
       }
-      // reduced rows -> the HBM slice (word-major), syndrome bits -> sb
+      // reduced rows -> the HBM slice (word-major), syndrome bits -> sb (forward elimination: the
+      // pivot rows are there already, in pivot order)
 #pragma unroll
-      for (int j = 0; j < RPT; ++j) {
+      for (int j = 0; j < RPT && PNL != 5; ++j) {
         const int i = tid + j * TB;
         if (i < m) {
           // opaque row pointer: the compiler otherwise hoists the WR word addresses out of the
@@ -1706,6 +1888,73 @@ osd_gpu_kernel(OsdGpuArgs A) {
     // 5. S0 and x(h_j) as bit-vectors over the pivot index: one wave per 64-bit word, lane c
     // forms bit c (pivot q*64 + c) and a ballot packs the word
     const int RWr = (r + 63) / 64;
+    if constexpr (kRR && PNL == 5) {
+      // 5'. (forward elimination) the Jordan half on the right-hand sides: thread k holds pivot row
+      // k (final since it was chosen, HBM slice row k) and b_k = (syndrome bit, bits Ht[j] of the
+      // row) as bits 0, 1 + j; U_kj = bit p_j of row k for pivots j > k (upper unitriangular in
+      // pivot order, the pivots being found in ascending position; its words were taken during
+      // the elimination).  Back substitution U x = b by blocks of 64 pivots from the last: the
+      // block's wave solves it lane by lane (readlane of the finished lane's x, xor into the lanes
+      // whose U bit names it), publishes x as 1 + nh ballot words, and every earlier row takes
+      // parity(U_k,block & x) per right-hand side.
+      const int32_t* lk = reinterpret_cast<const int32_t*>(smem);
+      const u64* Ul = reinterpret_cast<const u64*>(smem + A.pnl_off + osd_fwd_stg_bytes(WR));
+      u64* xv = const_cast<u64*>(Ul) + osd_ul_words(RW);      // [1 + nh][RWr] x as bit-vectors
+      uint32_t bk = 0;
+      {
+        u64 rw[WR];
+        const u64* mrow = Mg + tid;
+        asm volatile("" : "+v"(mrow));
+#pragma unroll
+        for (int Q = 0; Q < WR; ++Q) rw[Q] = (tid < r && Q < W) ? mrow[(size_t)Q * m] : 0ull;
+        if (tid < r) bk = ((uint32_t)lk[tid] >> 24) & 1u;
+        for (int j = 0; j < nh; ++j) {  // uniform
+          const int hp = swp[r + j];
+          const int hq = hp >> 6;
+          u64 wsel = 0;
+          osd_for_words(std::make_integer_sequence<int, WR>{}, [&](auto Qc) __attribute__((always_inline)) {
+            constexpr int Q = decltype(Qc)::value;
+            if (Q == hq) wsel = rw[Q];
+            return true;
+          });
+          bk |= (uint32_t)((wsel >> (hp & 63)) & 1ull) << (1 + j);
+        }
+      }
+      unsigned long long tj0 = QLDPC_STAMPS ? osd_stamp() : 0ull;
+      const int B0 = __builtin_amdgcn_readfirstlane(tid >> 6);  // this wave's pivot block (uniform)
+      for (int B = RWr - 1; B >= 0; --B) {  // uniform
+        if (B0 == B) {
+          // U bits name later pivots only (bit t of lane l: t > l), lanes past r hold zeros
+          const u64 uo = tid < r ? Ul[osd_ul_at(tid, B, RW)] : 0ull;
+          const uint32_t ulo = (uint32_t)uo, uhi = (uint32_t)(uo >> 32);
+#pragma unroll
+          for (int t = 63; t > 0; --t) {  // lane t is final: x_t (constant lanes, no hazards)
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)bk, t);
+            const uint32_t bit = ((t < 32 ? ulo : uhi) >> (t & 31)) & 1u;
+            bk ^= x & (0u - bit);
+          }
+#pragma unroll
+          for (int j = 0; j < 32; ++j) {
+            if (j > nh) break;  // uniform
+            const unsigned long long bal = __ballot(tid < r && ((bk >> j) & 1u));
+            if ((tid & 63) == 0) xv[(size_t)j * RWr + B] = bal;
+          }
+        }
+        __syncthreads();
+        if (B0 < B) {  // uniform per wave; lanes past r: uB = 0
+          const u64 uB = tid < r ? Ul[osd_ul_at(tid, B, RW)] : 0ull;
+          uint32_t acc = 0;
+#pragma unroll
+          for (int j = 0; j < 32; ++j) {
+            if (j > nh) break;  // uniform
+            acc |= (uint32_t)(__popcll(uB & xv[(size_t)j * RWr + B]) & 1) << j;
+          }
+          bk ^= acc;
+        }
+      }
+      if (QLDPC_STAMPS) st[13] += osd_stamp() - tj0;
+      for (int t = tid; t < (1 + nh) * RWr; t += TB) X[(size_t)(t / RWr) * RW + t % RWr] = xv[t];
+    } else
     for (int t = tid >> 6; t < (1 + nh) * RWr; t += TB >> 6) {  // uniform per wave
       const int j = t / RWr, q = t % RWr;
       const int c = tid & 63, i = q * 64 + c;
@@ -2370,7 +2619,7 @@ OsdKern osd_rr_kernel_t(int wr) {
   }
 }
 OsdKern osd_rr_kernel(int wr, int pnl) {
-  return pnl == 4 ? osd_rr_kernel_t<4>(wr) : pnl == 3 ? osd_rr_kernel_t<3>(wr) : pnl == 2 ? osd_rr_kernel_t<2>(wr) : pnl ? osd_rr_kernel_t<1>(wr)
+  return pnl == 5 ? osd_rr_kernel_t<5>(wr) : pnl == 4 ? osd_rr_kernel_t<4>(wr) : pnl == 3 ? osd_rr_kernel_t<3>(wr) : pnl == 2 ? osd_rr_kernel_t<2>(wr) : pnl ? osd_rr_kernel_t<1>(wr)
                                                                                    : osd_rr_kernel_t<0>(wr);
 }
 // column-window kernels (register rows, m <= 768, no panel modes): the first WR row words only and
@@ -2512,9 +2761,17 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
   // (profiles/r03/bposd_pnl/)
   if (G->wr && want_pnl != 0) {
     const int pv = want_pnl;
-    G->pnl = pv == 4 ? 4 : pv == 3 ? 3 : pv == 2 ? 2 : 1;  // 2: the distributed panel search (one barrier per pivot); 3: blocked
+    G->pnl = pv == 5 ? 5 : pv == 4 ? 4 : pv == 3 ? 3 : pv == 2 ? 2 : 1;  // 2: the distributed panel search (one barrier per pivot); 3: blocked
+    if (G->pnl == 5 && (G->host.method == 2 || G->nh > 31)) G->pnl = 0;  // forward elimination: <= 31 Ht columns
     G->pnl_off = (int)((G->lds + 15) & ~(size_t)15);
-    if (G->pnl == 4)  // the lagged loop: a second pivot-row buffer (the pivpos staging moves behind it)
+    if (G->pnl == 0) {
+      G->pnl_off = 0;
+    } else if (G->pnl == 5) {  // compaction staging, then (aliased) U words, x bit-vectors, word starts
+      const size_t tb = (size_t)G->rr_tb, rw = (size_t)G->RW;
+      (void)tb;
+      G->lds = (size_t)G->pnl_off + osd_fwd_stg_bytes(G->wr) + (size_t)osd_ul_words((int)rw) * 8 +
+               (size_t)(1 + G->nh) * rw * 8;
+    } else if (G->pnl == 4)  // the lagged loop: a second pivot-row buffer (the pivpos staging moves behind it)
       G->lds += (size_t)(G->wr + 1) * 8;
     else
       G->lds = (size_t)G->pnl_off + (G->pnl == 3 ? osd_blk_bytes(m, G->wr) : osd_pnl_bytes(m, G->wr));

@@ -47,3 +47,6 @@ if os.environ.get("QLDPC_OSD_PNL", "0") == "3":  # blocked: [7] pivots, [8] sear
     pv = max(1, v[7])
     print(f"blocked: pivots per syndrome {v[7] / max(1, v[6]):.0f}; per pivot: search {v[8] / pv:.0f} clk, tables {v[9] / pv:.0f}, "
           f"row updates {v[10] / pv:.0f}, panel-word exchange {v[11] / pv:.0f} (Gauss-Jordan {v[2] / pv:.0f})")
+if os.environ.get("QLDPC_OSD_PNL", "0") == "5":  # forward: [15] compactions, [13] back substitution (wave 0's view)
+    print(f"forward: compactions {v[15] / max(1, v[6]):.0f} clk per syndrome, "
+          f"back substitution {v[13] / max(1, v[6]):.0f} clk per syndrome")
