@@ -921,6 +921,12 @@ osd_gpu_kernel(OsdGpuArgs A) {
         // Jordan half is done afterwards on the (1 + nh)-bit right-hand sides only (syndrome bit,
         // the nh non-pivot columns Ht): U x = b by blocks of 64 pivots (after step 4 below).  Same
         // pivots (lexicographic minimum of (first bit, ORIGINAL row)), same S0 / x(h_j).
+        // MEASURED AND NOT KEPT (opt-in): bit-exact (11 GPU tests incl. non-uniform priors and the
+        // circuit graphs), the elimination itself ~15 % shorter (1.21 M vs 1.41 M cycles per n1600
+        // syndrome, stamps), but the compactions (46 k) and the back substitution (63 k) take most
+        // of that back and the extra per-step bookkeeping the rest: n1600 BP+OSD-E(10) 581 k vs
+        // 617 k shots/s (profiles/r05/osd_notkept/fwd_*).  What the halved VALU does not touch is
+        // the step's latency chain (two barriers, four LDS round trips), ~1,100 of its ~1,800 cycles.
         static_assert(RPT == 1, "forward elimination: one row per thread");
         int32_t* lkk = reinterpret_cast<int32_t*>(smem);  // pivots: (sbit << 24) | (position << 11) | row
         u64* stgA = reinterpret_cast<u64*>(smem + A.pnl_off);  // [WR][64] words of the rows moving in
