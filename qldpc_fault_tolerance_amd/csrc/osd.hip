@@ -2595,20 +2595,22 @@ namespace {
 // per thread: 2 or 3 rows per thread in 384 / 256 threads (fewer waves reading each broadcast
 // pivot word) measured 16 % / 26 % slower on n1600 (the per-pivot chain is latency-bound).
 constexpr int kOsdWR[] = {2, 4, 8, 12, 16, 20, 25};
-// rows per thread: 1, or 2 for the blocked elimination of the 20-25-word rows with QLDPC_OSD_RPT=2
-// (384-thread workgroups, two syndromes per CU, VGPRs pinned to 3 waves per SIMD).  MEASURED AND NOT
-// KEPT (opt-in): bit-exact (blk GPU tests), but the pinned budget spills 46 VGPRs and the n1600 BP+OSD
-// rate drops to 521 k shots/s vs 588 k with one row per thread (profiles/r05/osd_notkept/rpt2_*)
+// rows per thread: 1, or 2 for the lean loop / blocked elimination of the 20-25-word rows with
+// QLDPC_OSD_RPT=2 (384-thread workgroups, two syndromes per CU, VGPRs pinned to 3 waves per SIMD).
+// MEASURED AND NOT KEPT (opt-in): bit-exact (GPU tests), but n1600 BP+OSD 521 k vs 588 k shots/s for
+// the blocked elimination (46 VGPRs spilled) and 499 k vs 614 k for the lean loop (spills outside
+// the pivot loop only): two half-size syndromes per CU cost more than one full-size
+// (profiles/r05/osd_notkept/rpt2_*, lean_rpt2_*)
 inline int osd_rpt(int wr, int pnl) {
   const char* e = std::getenv("QLDPC_OSD_RPT");
-  return (pnl == 3 && wr >= 20 && e && std::atoi(e) == 2) ? 2 : 1;
+  return ((pnl == 3 || pnl == 0) && wr >= 20 && e && std::atoi(e) == 2) ? 2 : 1;
 }
 inline int osd_rr_threads(int wr, int pnl = 0) { return wr <= 16 ? 1024 : 768 / osd_rpt(wr, pnl); }
 using OsdKern = void (*)(OsdGpuArgs);
 template <int WR, int PNL>
 OsdKern osd_rr_wide(int rpt) {
-  if constexpr (PNL == 3)  // blocked: two rows per thread, 384 threads, two syndromes per CU
-    if (rpt == 2) return &osd_gpu_kernel<384, WR, 2, 3>;
+  if constexpr (PNL == 3 || PNL == 0)  // two rows per thread, 384 threads, two syndromes per CU
+    if (rpt == 2) return &osd_gpu_kernel<384, WR, 2, PNL>;
   return &osd_gpu_kernel<768, WR, 1, PNL>;
 }
 template <int PNL>

@@ -143,6 +143,8 @@ _OSD_MODES = {"default": {}, "lds": {"QLDPC_OSD_RR": "0"}, "hbm": {"QLDPC_OSD_RR
               "lag": {"QLDPC_OSD_PNL": "4"},
               # forward elimination with compaction + blocked back substitution (osd_cs: lean loop)
               "fwd": {"QLDPC_OSD_PNL": "5"},
+              # the lean loop with two rows per thread (384-thread workgroups, two per CU)
+              "rpt2": {"QLDPC_OSD_RPT": "2"},
               # the opt-in column window (measured slower): its own width (rank + nh
               # + 64 positions), forced to 8 words, its full-width redo exercised on every odd
               # syndrome, and the one-workgroup-per-CU build of the window kernel
@@ -171,7 +173,8 @@ _OSD_MODES = {"default": {}, "lds": {"QLDPC_OSD_RR": "0"}, "hbm": {"QLDPC_OSD_RR
     ("LP_Matg8_L30_Dmin20", 0, "osd_e", 10, "lag"),
     ("hgp_34_n225", 0, "osd_e", 10, "fwd"), ("hgp_34_n225", 0, "osd_0", 0, "fwd"), ("hgp_34_n1600", 0, "osd_e", 10, "fwd"),
     ("hgp_34_n1600", 0, "osd_0", 0, "fwd"), ("hgp_34_n225", 3, "osd_e", 8, "fwd"), ("LP_Matg8_L30_Dmin20", 0, "osd_e", 10, "fwd"),
-    ("LP_Matg8_L30_Dmin20", 0, "osd_e", 20, "fwd"), ("hgp_34_n1600", 0, "osd_cs", 6, "fwd")])
+    ("LP_Matg8_L30_Dmin20", 0, "osd_e", 20, "fwd"), ("hgp_34_n1600", 0, "osd_cs", 6, "fwd"),
+    ("hgp_34_n1600", 0, "osd_e", 10, "rpt2"), ("hgp_34_n1600", 0, "osd_cs", 6, "rpt2"), ("hgp_34_n1600", 0, "osd_0", 0, "rpt2")])
 def test_gpu_osd_matches_host_osd(gpu, monkeypatch, name, t0, method, order, mode):
     """GPU OSD kernel == native host OSD stage (itself pinned to the oracle in
     tests/test_osd_cpu.py) on GPU soft-BP posteriors, incl. a rank-deficient space-time graph
@@ -213,7 +216,8 @@ def test_gpu_osd_matches_host_osd(gpu, monkeypatch, name, t0, method, order, mod
     ("circuit_h1_all3r", "osd_cs", 6, "default"), ("hgp_34_n1600", "osd_e", 10, "winredo"),
     ("hgp_34_n1600", "osd_e", 10, "win"), ("hgp_34_n1600", "osd_e", 10, "lag"),
     ("circuit_h2_demo", "osd_e", 10, "lag"), ("circuit_h1_all3r", "osd_cs", 6, "lag"),
-    ("hgp_34_n1600", "osd_e", 10, "fwd"), ("circuit_h2_demo", "osd_e", 10, "fwd"), ("circuit_h2_all3c", "osd_e", 10, "fwd")])
+    ("hgp_34_n1600", "osd_e", 10, "fwd"), ("circuit_h2_demo", "osd_e", 10, "fwd"), ("circuit_h2_all3c", "osd_e", 10, "fwd"),
+    ("hgp_34_n1600", "osd_e", 10, "rpt2")])
 def test_gpu_osd_nonuniform_priors_matches_oracle(gpu, oracle, monkeypatch, name, method, order, mode):
     """GPU OSD with NON-uniform channel_probs (the circuit-level final round
     ST_BPOSD_Decoder_Circuit(h2, channel_ps2, ...), src/Decoders_SpaceTime.py:277-292): candidates
