@@ -157,6 +157,24 @@ int qldpc_osd_gpu_create(const qldpc_graph *g, const double *channel_probs, int3
 int qldpc_osd_gpu_destroy(qldpc_osd_gpu *osd);
 int qldpc_osd_gpu_decode(qldpc_osd_gpu *osd, const uint8_t *d_synd, const double *d_post, const uint8_t *d_conv,
                          const uint8_t *d_bp_corr, uint8_t *d_out0, uint8_t *d_outw, int64_t B, void *stream);
+/*
+ * FirstMinBPDecoder (src/Decoders.py:49-74) on the device: one-iteration min-sum BP (ldpc
+ * bp_decoder, max_iter = 1, bp_method "minimum_sum") repeated on the running syndrome while the
+ * residual syndrome weight does not grow, at most max_iter accepted steps; the corrections are the
+ * xor of the accepted steps' decisions.  One workgroup per syndrome, the whole loop on the device.
+ *   create : graph g, channel_probs [n] in (0, 1), max_iter, ms_scaling_factor (0 = ldpc's
+ *            1 - 2^-iter schedule at iter 1), precision 64 (ldpc's double) or 32; 2 (m + n) <= 64 KiB.
+ *   decode : device pointers d_synd [B][m] u8 -> d_corr [B][n] u8, d_steps [B] i32 (accepted
+ *            steps, or NULL), on `stream`.
+ * Replaces the Python loop of FirstMinBPDecoder.decode (Decoders.py:60-74).
+ */
+typedef struct qldpc_firstmin qldpc_firstmin;
+int qldpc_firstmin_create(const qldpc_graph *g, const double *channel_probs, int32_t max_iter,
+                          double ms_scaling_factor, int32_t precision, qldpc_firstmin **out);
+int qldpc_firstmin_destroy(qldpc_firstmin *fm);
+int qldpc_firstmin_decode(qldpc_firstmin *fm, const uint8_t *d_synd, uint8_t *d_corr, int32_t *d_steps, int64_t B,
+                          void *stream);
+
 /* Elimination geometry the handle chose (no reference counterpart; tests and DESIGN.md §4):
  * row_words = 64-bit words per register row (0: LDS / HBM image), window_words = the column
  * window's row words (0: none; its overruns are redone at full width), threads = per workgroup,

@@ -22,7 +22,8 @@ EXPORTED = [
     "qldpc_bp_geometry", "qldpc_bp_engine", "qldpc_phenl_create", "qldpc_phenl_destroy",
     "qldpc_phenl_trace_len", "qldpc_phenl_launch", "qldpc_bp_degree3_slots", "qldpc_bp_create_soft",
     "qldpc_bp_decode_batch_soft", "qldpc_osd_create", "qldpc_osd_destroy", "qldpc_osd_rank",
-    "qldpc_osd_decode_batch", "qldpc_osd_gpu_create", "qldpc_osd_gpu_destroy", "qldpc_osd_gpu_decode", "qldpc_osd_gpu_geometry", "qldpc_phenl_set_final_osd",
+    "qldpc_osd_decode_batch", "qldpc_osd_gpu_create", "qldpc_osd_gpu_destroy", "qldpc_osd_gpu_decode", "qldpc_osd_gpu_geometry",
+    "qldpc_firstmin_create", "qldpc_firstmin_destroy", "qldpc_firstmin_decode", "qldpc_phenl_set_final_osd",
     "qldpc_bp_bank_stats", "qldpc_bp_create_hbm", "qldpc_mc_set_osd", "qldpc_comm_unique_id",
     "qldpc_comm_init_rank", "qldpc_comm_init_all", "qldpc_comm_rank", "qldpc_comm_allreduce_counters",
     "qldpc_comm_allreduce_counters_group", "qldpc_comm_destroy", "qldpc_mc_run_sharded", "qldpc_sample_errors",
@@ -109,6 +110,12 @@ def _declare(L):
     L.qldpc_osd_gpu_destroy.argtypes = [_vp]
     L.qldpc_osd_gpu_decode.restype = ctypes.c_int
     L.qldpc_osd_gpu_geometry.restype = ctypes.c_int
+    L.qldpc_firstmin_create.restype = ctypes.c_int
+    L.qldpc_firstmin_create.argtypes = [_vp, _vp, _i32, ctypes.c_double, _i32, _vp]
+    L.qldpc_firstmin_destroy.restype = ctypes.c_int
+    L.qldpc_firstmin_destroy.argtypes = [_vp]
+    L.qldpc_firstmin_decode.restype = ctypes.c_int
+    L.qldpc_firstmin_decode.argtypes = [_vp, _vp, _vp, _vp, _i64, _vp]
     L.qldpc_osd_gpu_geometry.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 4
     L.qldpc_osd_gpu_decode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]
     L.qldpc_phenl_set_final_osd.restype = ctypes.c_int

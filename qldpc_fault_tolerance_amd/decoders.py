@@ -60,19 +60,41 @@ class BPDecoder:
 
 
 class FirstMinBPDecoder:
-    """Repeated one-iteration BP while the syndrome weight does not grow (``src/Decoders.py:49-74``)."""
+    """Repeated one-iteration BP while the syndrome weight does not grow (``src/Decoders.py:49-74``).
+
+    ``minimum_sum`` (every reference call site) runs the whole loop on the GPU in one kernel
+    (:class:`~.engine.DeviceFirstMin`, ``qldpc_firstmin_*``); ``product_sum`` steps the engine's
+    one-iteration BP from the host (one launch per first-min step for all active syndromes)."""
 
     def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, precision: int = 64,
                  device: int | None = None):
+        from .engine import DeviceFirstMin, bp_method_code
+
         self.h = np.asarray(h)
         self.max_iter = max_iter
-        self._bp = BPDecoder(h, channel_probs, 1, bp_method, ms_scaling_factor, precision=precision, device=device)
         self._H = CSR.from_dense(self.h)
+        self._fm = None
+        self._bp = None
+        if bp_method_code(bp_method) == 1:
+            n = self._H.n
+            probs = np.asarray(channel_probs, dtype=np.float64)
+            self._fm = DeviceFirstMin(self._H, np.full(n, float(probs)) if probs.ndim == 0 else probs,
+                                      int(max_iter), ms_scaling_factor, precision=precision, device=device)
+        else:
+            self._bp = BPDecoder(h, channel_probs, 1, bp_method, ms_scaling_factor, precision=precision, device=device)
+        self.steps_batch = None
 
     def decode(self, synd):
         return self.decode_batch(np.asarray(synd).reshape(1, -1))[0]
 
     def decode_batch(self, synd):
+        """[B, m] syndromes -> [B, n] corrections (int64); ``steps_batch`` = accepted steps."""
+        if self._fm is not None:
+            corr, self.steps_batch = self._fm.decode_batch(synd)
+            return corr
+        return self._decode_batch_stepped(synd)
+
+    def _decode_batch_stepped(self, synd):
         S = (np.atleast_2d(np.asarray(synd)).astype(np.int64) % 2).astype(np.uint8)
         B = S.shape[0]
         correction = np.zeros((B, self._H.n), dtype=np.int64)

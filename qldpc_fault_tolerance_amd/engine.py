@@ -363,6 +363,56 @@ class DeviceOSD:
             self.handle = None
 
 
+class DeviceFirstMin:
+    """``FirstMinBPDecoder`` (``src/Decoders.py:49-74``) on the GPU (``qldpc_firstmin_*``): one-iteration
+    min-sum BP repeated on the running syndrome while its weight does not grow, at most
+    ``max_iter`` accepted steps, the whole loop in one kernel (one workgroup per syndrome)."""
+
+    def __init__(self, H, channel_probs, max_iter: int, ms_scaling_factor=0.625, precision: int = 64,
+                 device: int | None = None, graph: DeviceGraph | None = None):
+        self.graph = graph if graph is not None else DeviceGraph(H, device=device)
+        n = self.graph.n
+        probs = np.asarray(channel_probs, dtype=np.float64)
+        self._probs = np.ascontiguousarray(np.full(n, float(probs)) if probs.ndim == 0 else probs)
+        if self._probs.shape != (n,):
+            raise ValueError(f"channel_probs must have {n} entries")
+        self.max_iter = int(max_iter)
+        h = ctypes.c_void_p()
+        _native.check(_native.lib().qldpc_firstmin_create(self.graph.handle, self._probs.ctypes.data_as(ctypes.c_void_p),
+                                                          self.max_iter, float(ms_scaling_factor), int(precision),
+                                                          ctypes.byref(h)), "qldpc_firstmin_create")
+        self.handle = h
+
+    def decode_device(self, synd_dev, corr_dev, steps_dev=None, stream=None):
+        torch = _torch()
+        s = stream if stream is not None else _stream_handle(torch, synd_dev.device)
+        _native.check(_native.lib().qldpc_firstmin_decode(
+            self.handle, ctypes.c_void_p(synd_dev.data_ptr()), ctypes.c_void_p(corr_dev.data_ptr()),
+            ctypes.c_void_p(steps_dev.data_ptr()) if steps_dev is not None else None, int(synd_dev.shape[0]), s),
+            "qldpc_firstmin_decode")
+
+    def decode_batch(self, synd):
+        """[B, m] syndromes -> (corrections [B, n] int64, accepted steps [B] int32)."""
+        torch = _torch()
+        S = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.int64) % 2, dtype=np.uint8)
+        B, n = S.shape[0], self.graph.n
+        if S.shape[1] != self.graph.m:
+            raise ValueError(f"syndromes must have {self.graph.m} columns")
+        dev = torch.device("cuda", self.graph.device)
+        sd = torch.from_numpy(S).to(dev)
+        corr = torch.empty((B, n), dtype=torch.uint8, device=dev)
+        steps = torch.empty(B, dtype=torch.int32, device=dev)
+        self.decode_device(sd, corr, steps)
+        torch.cuda.synchronize(dev)
+        return corr.cpu().numpy().astype(np.int64), steps.cpu().numpy()
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _native._lib is not None:
+            _native.lib().qldpc_firstmin_destroy(h)
+            self.handle = None
+
+
 @dataclass
 class MCResult:
     shots: int

@@ -196,7 +196,7 @@ def test_decoders_default_to_local_rank_device(monkeypatch):
 
     for cls in (decoders.BPDecoder, decoders.BPOSD_Decoder, decoders.ST_BP_Decoder_syndrome, decoders.BP_Decoder_Class,
                 decoders.BPOSD_Decoder_Class, decoders.ST_BP_Decoder_Class, decoders.FirstMinBPDecoder,
-                engine.DeviceBP, engine.DeviceGraph):
+                engine.DeviceBP, engine.DeviceGraph, engine.DeviceFirstMin):
         assert inspect.signature(cls.__init__).parameters["device"].default is None, cls
 
 

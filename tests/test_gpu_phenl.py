@@ -191,6 +191,43 @@ def test_firstmin_decoder_matches_reference_fixture(gpu):
     assert np.array_equal(fm.decode(g["firstmin_synd"][3]).astype(np.uint8), g["firstmin_corr"][3])
 
 
+@pytest.mark.parametrize("precision,alpha", [(64, 0.625), (32, 0.625), (64, 0.0), (64, 0.9)])
+def test_firstmin_device_loop_matches_reference_algorithm(gpu, oracle, precision, alpha):
+    """The device-resident first-min loop (qldpc_firstmin_*, one kernel) == the reference's
+    FirstMinBPDecoder.decode loop (src/Decoders.py:60-74) run over the oracle's one-iteration BP,
+    per syndrome (corrections and accepted steps), with non-uniform priors on [h | I], including
+    the zero syndrome (every step accepted with an empty correction) and ldpc's alpha = 0 schedule."""
+    code = codes.get_code("hgp_34_n225")
+    hz_ext = np.hstack([code.hz, np.identity(code.hz.shape[0])]).astype(np.uint8)
+    n = hz_ext.shape[1]
+    rng = np.random.default_rng(7 + precision + int(alpha * 10))
+    probs = rng.uniform(0.005, 0.06, n)
+    probs[::5] = probs[2]  # tied priors: equal minima
+    e = (rng.random((80, n)) < 0.035).astype(np.uint8)
+    synd = (e.astype(np.int64) @ hz_ext.T.astype(np.int64) % 2).astype(np.uint8)
+    synd[0] = 0
+    mi = 12
+    fm = decoders.FirstMinBPDecoder(hz_ext, probs, mi, "minimum_sum", alpha, precision=precision)
+    out = fm.decode_batch(synd)
+    H = hz_ext.astype(np.int64)
+
+    def bp1(s):
+        return oracle.bp_decode_batch(hz_ext, probs, 1, "minimum_sum", alpha, s[None].astype(np.uint8),
+                                      precision)[0][0].astype(np.int64)
+
+    for b in range(synd.shape[0]):
+        corr, cur, k = np.zeros(n, dtype=np.int64), synd[b].astype(np.int64), 0
+        nc = bp1(cur)
+        ns = (H @ nc + cur) % 2
+        while ns.sum() <= cur.sum() and k < mi:
+            cur, corr, k = ns, (corr + nc) % 2, k + 1
+            nc = bp1(cur)
+            ns = (H @ nc + cur) % 2
+        assert np.array_equal(out[b], corr), b
+        assert fm.steps_batch[b] == k, b
+    assert fm.steps_batch[0] == mi and not out[0].any()
+
+
 @pytest.mark.parametrize("p", [0.01, 0.06])
 def test_st_fp32_byte_f_family_decode_matches_oracle(gpu, oracle, p):
     """The fp32 space-time decoder of config 5 on the byte-F family (512 threads x 11 variables,

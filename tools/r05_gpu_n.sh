@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 5 GPU pass N: the device-resident FirstMinBPDecoder (qldpc_firstmin_*): parity tests and
+# the decode-rate probe against the host-stepped loop.
+set -u
+R=$(pwd)
+O=$R/gpurun_out/${1:-r05n}
+mkdir -p "$O"
+export TMPDIR=/tmp
+step() {  # name, timeout, command...
+  local n=$1 t=$2
+  shift 2
+  echo "== $n" >&2
+  timeout -k 10 "$t" "$@" > "$O/$n.out" 2> "$O/$n.err" || { echo "step $n failed ($?)"; tail -40 "$O/$n.out"; tail -5 "$O/$n.err"; exit 1; }
+}
+step pytest_fm 600 python -u -m pytest tests/test_gpu_phenl.py -x -v -k "firstmin" --timeout 300 --timeout-method thread
+tail -3 "$O/pytest_fm.out"
+step probe 300 python -u tools/dev/probe_firstmin.py 65536
+cat "$O/probe.out"
