@@ -169,6 +169,9 @@ int qldpc_osd_gpu_decode(qldpc_osd_gpu *osd, const uint8_t *d_synd, const double
  * Replaces the Python loop of FirstMinBPDecoder.decode (Decoders.py:60-74).
  */
 typedef struct qldpc_firstmin qldpc_firstmin;
+/* qldpc_phenl_set_round_firstmin (declared after qldpc_phenl below) makes the noisy rounds of the
+ * phenomenological pipeline decode with these (CodeSimulator_Phenon with FirstMinBPDecoder decoder1,
+ * the Single-Shot notebook's configuration). */
 int qldpc_firstmin_create(const qldpc_graph *g, const double *channel_probs, int32_t max_iter,
                           double ms_scaling_factor, int32_t precision, qldpc_firstmin **out);
 int qldpc_firstmin_destroy(qldpc_firstmin *fm);
@@ -256,6 +259,10 @@ int qldpc_phenl_launch(qldpc_phenl *ph, double px, double py, double pz, double 
  * qldpc_bp_create_soft) and then OSD where BP did not converge.  NULL = plain
  * BP for that sector.  Declared after qldpc_osd_gpu above. */
 int qldpc_phenl_set_final_osd(qldpc_phenl *ph, qldpc_osd_gpu *osd_x, qldpc_osd_gpu *osd_z);
+/* Noisy rounds decoded by FirstMinBPDecoder (qldpc_firstmin_*, built on exactly the ST graph of st_x /
+ * st_z) instead of BP; NULL keeps BP for that sector.  The trace counters then hold the accepted
+ * first-min steps as iterations and count no non-converged decodes for those rounds. */
+int qldpc_phenl_set_round_firstmin(qldpc_phenl *ph, qldpc_firstmin *fm_x, qldpc_firstmin *fm_z);
 
 /* Launch geometry chosen for a decoder (threads per shot, vars per thread,
  * LDS bytes, resident blocks per CU) — reported by bench.py / DESIGN.md. */

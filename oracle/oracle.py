@@ -330,11 +330,13 @@ def phenl_trace_len(code, num_rep, num_rounds):
 def phenl_run(code, px, py, pz, q, seed, shot_begin, shot_count, num_rounds, num_rep, logical_mode="Total",
               p_data=None, p_synd=None, max_iter_st=None, max_iter_2=None, bp_method="minimum_sum",
               ms_scaling_factor=0.625, precision=64, uniforms=None, per_shot=False, nthreads=0,
-              osd_method=None, osd_order=10):
+              osd_method=None, osd_order=10, firstmin_max_iter=None):
     """Phenomenological space-time shot loop on the CPU (CodeSimulator_Phenon_SpaceTime restated).
 
     ``osd_method`` (e.g. "osd_e"): decoder2 is BPOSD_Decoder (min-sum BP, then the C OSD
-    restatement on the final posteriors when BP did not converge), as the notebooks use."""
+    restatement on the final posteriors when BP did not converge), as the notebooks use.
+    ``firstmin_max_iter``: decoder1 is FirstMinBPDecoder (src/Decoders.py:49-74) with that many
+    accepted steps at most (min-sum; ``max_iter_st`` unused)."""
     n = code.N
     hz, lz, hx, lx = code.csr("hz"), code.csr("lz"), code.csr("hx"), code.csr("lx")
     mz, mx = hz.m, hx.m
@@ -378,7 +380,14 @@ def phenl_run(code, px, py, pz, q, seed, shot_begin, shot_count, num_rounds, num
     tail = [f64(px), f64(py), f64(pz), f64(q), ctypes.c_uint64(seed), ctypes.c_uint64(shot_begin), ctypes.c_int64(S),
             ctypes.c_int(num_rounds), ctypes.c_int(mode), p(uniforms, f64), ctypes.byref(cnt),
             p(fail, ctypes.c_uint8), p(trace, ctypes.c_uint8), ctypes.c_int(int(nthreads))]
-    if osd_method is None:
+    if firstmin_max_iter is not None:
+        assert bp_method == "minimum_sum", "FirstMinBPDecoder: min-sum"
+        head[-2] = ctypes.c_int(int(firstmin_max_iter))
+        meth = -1 if osd_method is None else (OSD_METHODS[osd_method] if isinstance(osd_method, str) else int(osd_method))
+        L.oracle_phenl_run_firstmin.restype = ctypes.c_int
+        rc = L.oracle_phenl_run_firstmin(*head, f64(ms_scaling_factor), ctypes.c_int(precision), *tail,
+                                         ctypes.c_int(meth), ctypes.c_int(int(osd_order)))
+    elif osd_method is None:
         L.oracle_phenl_run.restype = ctypes.c_int
         rc = L.oracle_phenl_run(*head, ctypes.c_int(METHODS[bp_method]), f64(ms_scaling_factor),
                                 ctypes.c_int(precision), *tail)

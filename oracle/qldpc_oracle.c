@@ -701,7 +701,7 @@ static int phenl_run_impl(int n,
                           double px, double py, double pz, double q, uint64_t seed, uint64_t shot_begin,
                           int64_t shot_count, int num_rounds, int logical_mode, const double *uniforms,
                           oracle_counters_t *out, uint8_t *fail_out, uint8_t *trace_out, int nthreads,
-                          int osd_method, int osd_order);
+                          int osd_method, int osd_order, int fm_max_iter);
 
 ORACLE_API int oracle_phenl_run(int n,
                                 int mz, const int32_t *hz_rp, const int32_t *hz_ci,
@@ -717,7 +717,7 @@ ORACLE_API int oracle_phenl_run(int n,
     return phenl_run_impl(n, mz, hz_rp, hz_ci, kx, lz_rp, lz_ci, mx, hx_rp, hx_ci, kz, lx_rp, lx_ci, probs_st_x,
                           probs_st_z, probs2_x, probs2_z, reps, max_iter_st, max_iter_2, method, alpha, precision, px,
                           py, pz, q, seed, shot_begin, shot_count, num_rounds, logical_mode, uniforms, out, fail_out,
-                          trace_out, nthreads, -1, 0);
+                          trace_out, nthreads, -1, 0, -1);
 }
 
 /* The same with decoder2 = BPOSD_Decoder (src/Decoders.py:26-41; the Threshold notebook's
@@ -739,7 +739,32 @@ ORACLE_API int oracle_phenl_run_osd(int n,
     return phenl_run_impl(n, mz, hz_rp, hz_ci, kx, lz_rp, lz_ci, mx, hx_rp, hx_ci, kz, lx_rp, lx_ci, probs_st_x,
                           probs_st_z, probs2_x, probs2_z, reps, max_iter_st, max_iter_2, 1, alpha, precision, px,
                           py, pz, q, seed, shot_begin, shot_count, num_rounds, logical_mode, uniforms, out, fail_out,
-                          trace_out, nthreads, osd_method, osd_order);
+                          trace_out, nthreads, osd_method, osd_order, -1);
+}
+
+/* The same with decoder1 = FirstMinBPDecoder (src/Decoders.py:49-74, the Single-Shot notebook's
+ * CodeSimulator_Phenon decoder1): per noisy round, one-iteration min-sum BP on the running
+ * detector vector while the residual weight does not grow, at most fm_max_iter accepted steps, the
+ * xor of the accepted decisions folded like a BP decoding; a sector's "iterations" count the
+ * accepted steps (no convergence notion: never counted non-converged).  decoder2: BP, or
+ * BPOSD_Decoder when osd_method >= 0. */
+ORACLE_API int oracle_phenl_run_firstmin(int n,
+                                         int mz, const int32_t *hz_rp, const int32_t *hz_ci,
+                                         int kx, const int32_t *lz_rp, const int32_t *lz_ci,
+                                         int mx, const int32_t *hx_rp, const int32_t *hx_ci,
+                                         int kz, const int32_t *lx_rp, const int32_t *lx_ci,
+                                         const double *probs_st_x, const double *probs_st_z,
+                                         const double *probs2_x, const double *probs2_z,
+                                         int reps, int fm_max_iter, int max_iter_2, double alpha, int precision,
+                                         double px, double py, double pz, double q, uint64_t seed,
+                                         uint64_t shot_begin, int64_t shot_count, int num_rounds, int logical_mode,
+                                         const double *uniforms, oracle_counters_t *out, uint8_t *fail_out,
+                                         uint8_t *trace_out, int nthreads, int osd_method, int osd_order) {
+    if (osd_method > 2 || fm_max_iter < 0) return -1;
+    return phenl_run_impl(n, mz, hz_rp, hz_ci, kx, lz_rp, lz_ci, mx, hx_rp, hx_ci, kz, lx_rp, lx_ci, probs_st_x,
+                          probs_st_z, probs2_x, probs2_z, reps, 1, max_iter_2, 1, alpha, precision, px, py, pz, q,
+                          seed, shot_begin, shot_count, num_rounds, logical_mode, uniforms, out, fail_out, trace_out,
+                          nthreads, osd_method < 0 ? -1 : osd_method, osd_order, fm_max_iter);
 }
 
 static int phenl_run_impl(int n,
@@ -753,7 +778,7 @@ static int phenl_run_impl(int n,
                           double px, double py, double pz, double q, uint64_t seed, uint64_t shot_begin,
                           int64_t shot_count, int num_rounds, int logical_mode, const double *uniforms,
                           oracle_counters_t *out, uint8_t *fail_out, uint8_t *trace_out, int nthreads,
-                          int osd_method, int osd_order) {
+                          int osd_method, int osd_order, int fm_max_iter) {
     const int m[2] = {mz, mx};
     const int32_t *hrp[2] = {hz_rp, hx_rp}, *hci[2] = {hz_ci, hx_ci};
     const int32_t *lrp[2] = {lz_rp, lx_rp}, *lci[2] = {lz_ci, lx_ci};
@@ -798,6 +823,10 @@ static int phenl_run_impl(int n,
         uint8_t *cur[2], *hist[2], *det = (uint8_t *)malloc((size_t)reps * mm + 1);
         uint8_t *ser[2], *syn = (uint8_t *)malloc((size_t)mm + 1), *chk = (uint8_t *)malloc((size_t)mm + 1);
         uint8_t *r = (uint8_t *)malloc((size_t)n);
+        /* first-min decoder1: running detector vector, its residual, the accepted correction */
+        const size_t nst = (size_t)reps * (n + mm);
+        uint8_t *fcur = (uint8_t *)malloc((size_t)reps * mm + 1), *fns = (uint8_t *)malloc((size_t)reps * mm + 1);
+        uint8_t *fcor = (uint8_t *)malloc(nst + 1);
         uint8_t *o0 = (uint8_t *)malloc((size_t)n), *ow = (uint8_t *)malloc((size_t)n);
         double *post = (double *)malloc(sizeof(double) * (size_t)n);
         for (int s = 0; s < 2; s++) {
@@ -840,7 +869,30 @@ static int phenl_run_impl(int n,
                     if (tr) tr += R;
                     if (!need[s]) continue;
                     int it, conv; const uint8_t *e;
-                    if (precision == 32) { conv = bp_run_f32(&GS[s], &PSs[s], &w32s[s], det, &it); e = w32s[s].dec; }
+                    if (fm_max_iter >= 0) {  /* FirstMinBPDecoder.decode, src/Decoders.py:60-74 */
+                        const int nS = GS[s].n;
+                        const uint8_t *d;
+                        int wc = 0, wn = 0, k = 0;
+                        memcpy(fcur, det, (size_t)R); memset(fcor, 0, (size_t)nS);
+                        for (int i = 0; i < R; i++) wc += fcur[i];
+#define FM_STEP()                                                                                   \
+    do {                                                                                            \
+        if (precision == 32) { bp_run_f32(&GS[s], &PSs[s], &w32s[s], fcur, &it); d = w32s[s].dec; } \
+        else { bp_run_f64(&GS[s], &PSs[s], &w64s[s], fcur, &it); d = w64s[s].dec; }                 \
+        csr_mulvec(srp[s], sci[s], R, d, fns);                                                      \
+        wn = 0;                                                                                     \
+        for (int i = 0; i < R; i++) { fns[i] ^= fcur[i]; wn += fns[i]; }                            \
+    } while (0)
+                        FM_STEP();
+                        while (wn <= wc && k < fm_max_iter) {
+                            memcpy(fcur, fns, (size_t)R);
+                            for (int p = 0; p < nS; p++) fcor[p] ^= d[p];
+                            k++; wc = wn;
+                            FM_STEP();
+                        }
+#undef FM_STEP
+                        it = k; conv = 1; e = fcor;
+                    } else if (precision == 32) { conv = bp_run_f32(&GS[s], &PSs[s], &w32s[s], det, &it); e = w32s[s].dec; }
                     else { conv = bp_run_f64(&GS[s], &PSs[s], &w64s[s], det, &it); e = w64s[s].dec; }
                     loc.sector_decodes[s]++; loc.sector_iters[s] += it; loc.sector_nonconv[s] += !conv;
                     const int w = n + m[s];
@@ -892,7 +944,7 @@ static int phenl_run_impl(int n,
             else { ws_free_f64(&w64s[s]); ws_free_f64(&w64f[s]); }
             free(cur[s]); free(hist[s]); free(ser[s]);
         }
-        free(det); free(syn); free(chk); free(r); free(o0); free(ow); free(post);
+        free(det); free(syn); free(chk); free(r); free(o0); free(ow); free(post); free(fcur); free(fns); free(fcor);
 #ifdef _OPENMP
 #pragma omp critical
 #endif

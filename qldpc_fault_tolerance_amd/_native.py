@@ -23,7 +23,7 @@ EXPORTED = [
     "qldpc_phenl_trace_len", "qldpc_phenl_launch", "qldpc_bp_degree3_slots", "qldpc_bp_create_soft",
     "qldpc_bp_decode_batch_soft", "qldpc_osd_create", "qldpc_osd_destroy", "qldpc_osd_rank",
     "qldpc_osd_decode_batch", "qldpc_osd_gpu_create", "qldpc_osd_gpu_destroy", "qldpc_osd_gpu_decode", "qldpc_osd_gpu_geometry",
-    "qldpc_firstmin_create", "qldpc_firstmin_destroy", "qldpc_firstmin_decode", "qldpc_phenl_set_final_osd",
+    "qldpc_firstmin_create", "qldpc_firstmin_destroy", "qldpc_firstmin_decode", "qldpc_phenl_set_round_firstmin", "qldpc_phenl_set_final_osd",
     "qldpc_bp_bank_stats", "qldpc_bp_create_hbm", "qldpc_mc_set_osd", "qldpc_comm_unique_id",
     "qldpc_comm_init_rank", "qldpc_comm_init_all", "qldpc_comm_rank", "qldpc_comm_allreduce_counters",
     "qldpc_comm_allreduce_counters_group", "qldpc_comm_destroy", "qldpc_mc_run_sharded", "qldpc_sample_errors",
@@ -116,6 +116,8 @@ def _declare(L):
     L.qldpc_firstmin_destroy.argtypes = [_vp]
     L.qldpc_firstmin_decode.restype = ctypes.c_int
     L.qldpc_firstmin_decode.argtypes = [_vp, _vp, _vp, _vp, _i64, _vp]
+    L.qldpc_phenl_set_round_firstmin.restype = ctypes.c_int
+    L.qldpc_phenl_set_round_firstmin.argtypes = [_vp, _vp, _vp]
     L.qldpc_osd_gpu_geometry.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 4
     L.qldpc_osd_gpu_decode.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]
     L.qldpc_phenl_set_final_osd.restype = ctypes.c_int

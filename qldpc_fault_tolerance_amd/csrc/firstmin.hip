@@ -35,7 +35,13 @@ struct qldpc_firstmin {
   qldpc_rt::DevBuf cp, crow;    // CSC in column order (rows ascending): col_ptr [n + 1], row [E]
   qldpc_rt::DevBuf csb, cmag;   // per CSC entry: prior-sign parity of the row's other edges (u8), |c2b| (T)
   qldpc_rt::DevBuf prior;       // [n] T
+  std::vector<int32_t> row_ptr, col_idx;  // the graph it was built on (qldpc_phenl_set_round_firstmin checks it)
 };
+
+bool qldpc_rt::firstmin_matches(const qldpc_firstmin* fm, const qldpc_graph* g) {
+  return fm && g && fm->device == g->device && fm->m == g->m && fm->n == g->n && fm->row_ptr == g->row_ptr &&
+         fm->col_idx == g->col_idx;
+}
 
 namespace {
 
@@ -202,6 +208,8 @@ int qldpc_firstmin_create(const qldpc_graph* g, const double* channel_probs, int
   F->max_iter = max_iter > 0 ? max_iter : 0;
   F->precision = precision;
   F->lds = lds;
+  F->row_ptr = g->row_ptr;
+  F->col_idx = g->col_idx;
   auto fail = [&](int code) {
     F->rp.release(); F->ci.release(); F->cp.release(); F->crow.release(); F->csb.release(); F->cmag.release();
     F->prior.release();

@@ -140,6 +140,8 @@ bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g);
 bool osd_host_matches(const qldpc_osd* o, const qldpc_graph* g);
 // GPU OSD handle from a host OSD stage on graph g: same method / order / rank / soft weights (osd.hip)
 int osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* host, qldpc_osd_gpu** out);
+// true when the first-min decoder was built on exactly this graph (shape and edges) and device
+bool firstmin_matches(const qldpc_firstmin* fm, const qldpc_graph* g);
 // BP+OSD stage of the fused shot loop, one sector (osd.hip)
 int osd_gpu_bposd_stage(qldpc_osd_gpu* osd, const uint8_t* synd, const double* post, const uint8_t* err,
                         const long long* shot, uint8_t* outw, long long ncand, const unsigned long long* lmask, int kw,

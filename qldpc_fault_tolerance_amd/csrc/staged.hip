@@ -273,6 +273,8 @@ struct qldpc_phenl {
   // BP+OSD final round (qldpc_phenl_set_final_osd): soft BP posteriors and BP decisions
   qldpc_osd_gpu* osd2[2] = {nullptr, nullptr};
   DevBuf post, bpcorr;
+  // FirstMinBPDecoder noisy rounds (qldpc_phenl_set_round_firstmin): replace the ST BP decodes
+  qldpc_firstmin* fm1[2] = {nullptr, nullptr};
 };
 
 extern "C" {
@@ -378,6 +380,18 @@ int qldpc_phenl_set_final_osd(qldpc_phenl* P, qldpc_osd_gpu* osd_x, qldpc_osd_gp
   return 0;
 }
 
+int qldpc_phenl_set_round_firstmin(qldpc_phenl* P, qldpc_firstmin* fm_x, qldpc_firstmin* fm_z) {
+  if (!P) return set_err(QLDPC_EINVAL, "NULL phenl");
+  qldpc_firstmin* f[2] = {fm_x, fm_z};
+  for (int q = 0; q < 2; ++q)
+    if (f[q] && !qldpc_rt::firstmin_matches(f[q], P->st[q]->g))
+      return set_err(QLDPC_EINVAL, q == 0 ? "X-sector first-min decoder was built on a different graph than st_x"
+                                          : "Z-sector first-min decoder was built on a different graph than st_z");
+  P->fm1[0] = fm_x;
+  P->fm1[1] = fm_z;
+  return 0;
+}
+
 int qldpc_phenl_destroy(qldpc_phenl* P) {
   if (!P) return 0;
   for (int q = 0; q < 2; ++q) {
@@ -469,10 +483,18 @@ int qldpc_phenl_launch(qldpc_phenl* P, double px, double py, double pz, double q
                              static_cast<const unsigned long long*>(P->D[s].p), static_cast<uint8_t*>(P->det[s].p),
                              d_trace, tlen, toff, c0, R, W, B);
           QLDPC_HIP(hipGetLastError());
-          int rc = qldpc_bp_decode_batch(P->st[s], static_cast<const uint8_t*>(P->det[s].p),
-                                         static_cast<uint8_t*>(P->corr[s].p), static_cast<int32_t*>(P->iters.p),
-                                         static_cast<uint8_t*>(P->conv.p), B, stream);
-          if (rc) return rc;
+          int rc;
+          if (P->fm1[s]) {  // FirstMinBPDecoder: accepted steps as "iterations", never non-converged
+            rc = qldpc_firstmin_decode(P->fm1[s], static_cast<const uint8_t*>(P->det[s].p),
+                                       static_cast<uint8_t*>(P->corr[s].p), static_cast<int32_t*>(P->iters.p), B, stream);
+            if (rc) return rc;
+            QLDPC_HIP(hipMemsetAsync(P->conv.p, 1, (size_t)B, st));
+          } else {
+            rc = qldpc_bp_decode_batch(P->st[s], static_cast<const uint8_t*>(P->det[s].p),
+                                       static_cast<uint8_t*>(P->corr[s].p), static_cast<int32_t*>(P->iters.p),
+                                       static_cast<uint8_t*>(P->conv.p), B, stream);
+            if (rc) return rc;
+          }
           hipLaunchKernelGGL(ph_iters, dim3((unsigned)((B + kTile - 1) / kTile)), dim3(kTile), 0, st,
                              static_cast<const int32_t*>(P->iters.p), static_cast<const uint8_t*>(P->conv.p), cnt, s, B);
           QLDPC_HIP(hipGetLastError());

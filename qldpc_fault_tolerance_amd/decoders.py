@@ -83,6 +83,20 @@ class FirstMinBPDecoder:
         else:
             self._bp = BPDecoder(h, channel_probs, 1, bp_method, ms_scaling_factor, precision=precision, device=device)
         self.steps_batch = None
+        self._st_bp = None
+        self._probs = np.asarray(channel_probs, dtype=np.float64)
+
+    def st_bp(self):
+        """A one-iteration engine BP on this decoder's own device graph: the slot the fused
+        phenomenological pipeline validates its space-time graph against (its decodes are replaced
+        by this decoder's first-min loop, qldpc_phenl_set_round_firstmin)."""
+        if self._st_bp is None:
+            from .engine import DeviceBP
+
+            n = self._H.n
+            p = np.full(n, float(self._probs)) if self._probs.ndim == 0 else self._probs
+            self._st_bp = DeviceBP(self._H, p, max_iter=1, graph=self._fm.graph)
+        return self._st_bp
 
     def decode(self, synd):
         return self.decode_batch(np.asarray(synd).reshape(1, -1))[0]

@@ -609,6 +609,14 @@ class DevicePhenl:
             self.handle, osd_x.handle if osd_x is not None else None, osd_z.handle if osd_z is not None else None),
             "qldpc_phenl_set_final_osd")
 
+    def set_round_firstmin(self, fm_x: "DeviceFirstMin | None", fm_z: "DeviceFirstMin | None"):
+        """Noisy rounds decoded by FirstMinBPDecoder (``qldpc_phenl_set_round_firstmin``): each
+        handle must be built on exactly its sector's space-time graph."""
+        self._fm1 = (fm_x, fm_z)  # keep the handles alive
+        _native.check(_native.lib().qldpc_phenl_set_round_firstmin(
+            self.handle, fm_x.handle if fm_x is not None else None, fm_z.handle if fm_z is not None else None),
+            "qldpc_phenl_set_round_firstmin")
+
     def trace_len(self, num_rounds: int) -> int:
         v = ctypes.c_int64()
         _native.check(_native.lib().qldpc_phenl_trace_len(self.handle, int(num_rounds), ctypes.byref(v)),

@@ -473,14 +473,30 @@ class CodeSimulator_Phenon:
         from .decoders import BPDecoder
 
         d1 = (self.decoder1_x, self.decoder1_z)
-        if not all(isinstance(d, BPDecoder) for d in d1):
+        fm = self._firstmin1()
+        if fm is None and not all(isinstance(d, BPDecoder) for d in d1):
             return None
         # decoder2 = engine BPDecoder, or BPOSD_Decoder with GPU OSD (the Threshold notebook's
         # BPDecoder + BPOSD_Decoder osd_e(10) pair): its soft BP feeds qldpc_phenl_set_final_osd
         b2 = tuple(_final_round_bp(d) for d in (self.decoder2_x, self.decoder2_z))
         if any(b is None for b in b2):
             return None
+        if fm is not None:  # the pipeline's ST slot: a BP handle on the first-min decoders' own graphs
+            return fm[0].st_bp(), fm[1].st_bp(), b2[0], b2[1]
         return d1[0].decoder, d1[1].decoder, b2[0], b2[1]
+
+    def _firstmin1(self):
+        """decoder1_x / decoder1_z as device first-min handles (FirstMinBPDecoder, minimum_sum, on
+        [h | I] of this code: the Single-Shot notebook's decoder1), or None."""
+        from .decoders import FirstMinBPDecoder
+
+        d1 = (self.decoder1_x, self.decoder1_z)
+        if not all(isinstance(d, FirstMinBPDecoder) and d._fm is not None for d in d1):
+            return None
+        ext = (self.hz_ext, self.hx_ext)
+        if any(d.h.shape != e.shape or not np.array_equal(d.h % 2, e % 2) for d, e in zip(d1, ext)):
+            return None
+        return d1
 
     def _final_osd(self):
         return tuple(getattr(d, "gpu_osd", None) for d in (self.decoder2_x, self.decoder2_z))
@@ -499,6 +515,9 @@ class CodeSimulator_Phenon:
             ox, oz = self._final_osd()
             if ox is not None or oz is not None:
                 self._ph.set_final_osd(ox, oz)
+            fm = self._firstmin1()
+            if fm is not None:
+                self._ph.set_round_firstmin(fm[0]._fm, fm[1]._fm)
         rank, ws = parallel.world()
         b, c = parallel.shard_range(num_samples, rank, ws, begin=self._shot_offset)
         self._shot_offset += int(num_samples)

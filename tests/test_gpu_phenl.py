@@ -178,6 +178,42 @@ def test_phen_single_shot_dropin_matches_oracle(gpu, oracle):
     assert sim.last_result.sector_iters == ref["sector_iters"]
 
 
+@pytest.mark.parametrize("dec2", ["bp", "bposd"])
+def test_phen_single_shot_firstmin_decoder1_fused_matches_oracle(gpu, oracle, dec2):
+    """CodeSimulator_Phenon with FirstMinBPDecoder decoder1 (the Single-Shot notebook's configuration:
+    p_data = p_synd = 2p/3 on [h | I], max_iter = N/10) runs fused (qldpc_phenl_set_round_firstmin) and
+    equals the oracle's pipeline with the reference's first-min loop per noisy round: failures, per-sector
+    failures, accepted steps and the final round's iterations; decoder2 BP or BPOSD osd_e(10)."""
+    code = codes.get_code("hgp_34_n225")
+    p = 0.03
+    pd = 2 * p / 3
+    ext = lambda h: np.hstack([h, np.identity(h.shape[0])])  # noqa: E731
+    mi = int(code.N / 10)
+    d1x = decoders.FirstMinBPDecoder(ext(code.hz), np.hstack([pd * np.ones(code.N), pd * np.ones(code.hz.shape[0])]),
+                                     mi, "minimum_sum", 0.625)
+    d1z = decoders.FirstMinBPDecoder(ext(code.hx), np.hstack([pd * np.ones(code.N), pd * np.ones(code.hx.shape[0])]),
+                                     mi, "minimum_sum", 0.625)
+    pp = 2 * p / 3  # decoder2 channel: (p/3 + p/3)
+    if dec2 == "bposd":
+        d2x = decoders.BPOSD_Decoder(code.hz, pp * np.ones(code.N), mi, "minimum_sum", 0.625, "osd_e", 10)
+        d2z = decoders.BPOSD_Decoder(code.hx, pp * np.ones(code.N), mi, "minimum_sum", 0.625, "osd_e", 10)
+    else:
+        d2x = decoders.BPDecoder(code.hz, pp * np.ones(code.N), mi, "minimum_sum", 0.625)
+        d2z = decoders.BPDecoder(code.hx, pp * np.ones(code.N), mi, "minimum_sum", 0.625)
+    sim = simulators.CodeSimulator_Phenon(code=code, decoder1_x=d1x, decoder1_z=d1z, decoder2_x=d2x, decoder2_z=d2z,
+                                          pauli_error_probs=[p / 3] * 3, q=pd, eval_logical_type="Total", seed=77)
+    assert sim._engine_parts() is not None and sim._firstmin1() is not None
+    wer, _ = sim.WordErrorRate(5, 600)
+    ref = oracle.phenl_run(code, p / 3, p / 3, p / 3, pd, 77, 0, 600, 5, 1, "Total", p_data=pd, p_synd=pd,
+                           max_iter_2=mi, firstmin_max_iter=mi, osd_method="osd_e" if dec2 == "bposd" else None)
+    res = sim.last_result
+    assert res.failures == ref["failures"]
+    assert list(res.sector_fail) == list(ref["sector_fail"])
+    assert list(res.sector_iters) == list(ref["sector_iters"])
+    assert list(res.sector_nonconv) == list(ref["sector_nonconv"])
+    assert wer == simulators.word_error_rate_phenl(ref["failures"], 600, code.K, 5)
+
+
 def test_firstmin_decoder_matches_reference_fixture(gpu):
     """FirstMinBPDecoder (src/Decoders.py:49-74) over the engine == the reference class on the oracle BP."""
     g = np.load(PHEN)

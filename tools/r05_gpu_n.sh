@@ -12,7 +12,9 @@ step() {  # name, timeout, command...
   echo "== $n" >&2
   timeout -k 10 "$t" "$@" > "$O/$n.out" 2> "$O/$n.err" || { echo "step $n failed ($?)"; tail -40 "$O/$n.out"; tail -5 "$O/$n.err"; exit 1; }
 }
-step pytest_fm 600 python -u -m pytest tests/test_gpu_phenl.py -x -v -k "firstmin" --timeout 300 --timeout-method thread
+step pytest_fm 600 python -u -m pytest tests/test_gpu_phenl.py -x -v -k "firstmin or phen_single" --timeout 300 --timeout-method thread
 tail -3 "$O/pytest_fm.out"
 step probe 300 python -u tools/dev/probe_firstmin.py 65536
 cat "$O/probe.out"
+step probe_phen 600 python -u tools/dev/probe_phen_firstmin.py hgp_34_n625 65536 5
+cat "$O/probe_phen.out"
