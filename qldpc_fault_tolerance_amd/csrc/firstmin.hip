@@ -36,6 +36,7 @@ struct qldpc_firstmin {
   qldpc_rt::DevBuf csb, cmag;   // per CSC entry: prior-sign parity of the row's other edges (u8), |c2b| (T)
   qldpc_rt::DevBuf prior;       // [n] T
   std::vector<int32_t> row_ptr, col_idx;  // the graph it was built on (qldpc_phenl_set_round_firstmin checks it)
+  qldpc_rt::DevBuf colm;  // m <= 64: [n] u64 row mask of each column (the one-iteration thread-per-syndrome kernel)
 };
 
 bool qldpc_rt::firstmin_matches(const qldpc_firstmin* fm, const qldpc_graph* g) {
@@ -57,12 +58,14 @@ struct FmArgs {
   const void* prior;
   const uint8_t* synd;  // [B][m]
   uint8_t* corr;        // [B][n]
-  int32_t* steps;       // [B] or null
+  int32_t* steps;       // [B] or null (BP1: iterations)
+  uint8_t* conv;        // BP1: [B] or null
   long long B;
   int m, n, max_iter;
 };
 
-template <typename T>
+// BP1: one step only -- the one-iteration BP's decision, iterations 1, converged iff H d == s
+template <typename T, bool BP1 = false>
 __global__ void __launch_bounds__(kFmThreads) firstmin_kernel(FmArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   const int tid = threadIdx.x, TB = blockDim.x, m = a.m, n = a.n;
@@ -122,6 +125,16 @@ __global__ void __launch_bounds__(kFmThreads) firstmin_kernel(FmArgs a) {
     __syncthreads();
     int k = 0;
     int wn = step();
+    if (BP1) {
+      uint8_t* out = a.corr + b * (long long)n;
+      for (int j = tid; j < n; j += TB) out[j] = dec[j];
+      if (tid == 0) {
+        if (a.steps) a.steps[b] = 1;
+        if (a.conv) a.conv[b] = wn == 0 ? 1 : 0;
+      }
+      __syncthreads();
+      continue;
+    }
     while (wn <= wc && k < a.max_iter) {  // uniform
       if (wc == 0 && !s_any) {  // cur = 0 and BP1(0) = 0: every remaining step accepts nothing
         k = a.max_iter;
@@ -138,6 +151,52 @@ __global__ void __launch_bounds__(kFmThreads) firstmin_kernel(FmArgs a) {
     for (int j = tid; j < n; j += TB) out[j] = cor[j];
     if (tid == 0 && a.steps) a.steps[b] = k;
     __syncthreads();  // LDS reused by the next syndrome
+  }
+}
+
+// One-iteration BP for graphs of <= 64 checks (the circuit loop's h1: 27 x 153): one THREAD per
+// syndrome, the syndrome and its residual as 64-bit masks in registers, the tables walked in the
+// same (uniform) order by every lane (scalar / broadcast loads).  The workgroup-per-syndrome kernel
+// above spends its time in barriers on such graphs (0.20 ms per 65,536 syndromes against the
+// engine's 0.18).  Same adds in the same order: identical decisions.
+// STG: the workgroup's 256 syndromes and decisions staged through LDS (coalesced global reads and
+// writes of its contiguous [256][m] / [256][n] blocks) when 256 (m + n) bytes fit
+template <typename T, bool STG>
+__global__ void __launch_bounds__(256) bp1_small_kernel(FmArgs a, const unsigned long long* __restrict__ colm) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  const int m = a.m, n = a.n, tid = threadIdx.x;
+  const long long b0 = (long long)blockIdx.x * 256, b = b0 + tid;
+  const int nb = (int)(a.B - b0 < 256 ? a.B - b0 : 256);
+  uint8_t* ssy = sm;                        // [256][m]
+  uint8_t* sdc = sm + (size_t)256 * m;      // [256][n]
+  if (STG) {
+    for (int t = tid; t < nb * m; t += 256) ssy[t] = a.synd[b0 * m + t];
+    __syncthreads();
+  }
+  const T* mag = static_cast<const T*>(a.cmag);
+  const T* prior = static_cast<const T*>(a.prior);
+  if (b < a.B) {
+    const uint8_t* sy = STG ? ssy + (size_t)tid * m : a.synd + b * (long long)m;
+    unsigned long long cur = 0;
+    for (int i = 0; i < m; ++i) cur |= (unsigned long long)(sy[i] & 1u) << i;
+    unsigned long long ns = cur;
+    uint8_t* out = STG ? sdc + (size_t)tid * n : a.corr + b * (long long)n;
+    for (int j = 0; j < n; ++j) {
+      T post = prior[j];
+      for (int k = a.cp[j]; k < a.cp[j + 1]; ++k) {
+        const T c = mag[k];
+        post += (((cur >> a.crow[k]) ^ a.csb[k]) & 1ull) ? -c : c;
+      }
+      const bool d = post <= (T)0;
+      out[j] = d ? 1 : 0;
+      ns ^= d ? colm[j] : 0ull;
+    }
+    if (a.steps) a.steps[b] = 1;
+    if (a.conv) a.conv[b] = ns == 0 ? 1 : 0;
+  }
+  if (STG) {
+    __syncthreads();
+    for (int t = tid; t < nb * n; t += 256) a.corr[b0 * n + t] = sdc[t];
   }
 }
 
@@ -210,9 +269,15 @@ int qldpc_firstmin_create(const qldpc_graph* g, const double* channel_probs, int
   F->lds = lds;
   F->row_ptr = g->row_ptr;
   F->col_idx = g->col_idx;
+  std::vector<unsigned long long> colm;
+  if (m <= 64) {
+    colm.assign(std::max(n, 1), 0ull);
+    for (int i = 0; i < m; ++i)
+      for (int e = g->row_ptr[i]; e < g->row_ptr[i + 1]; ++e) colm[g->col_idx[e]] ^= 1ull << i;
+  }
   auto fail = [&](int code) {
     F->rp.release(); F->ci.release(); F->cp.release(); F->crow.release(); F->csb.release(); F->cmag.release();
-    F->prior.release();
+    F->prior.release(); F->colm.release();
     delete F;
     return code;
   };
@@ -236,8 +301,10 @@ int qldpc_firstmin_create(const qldpc_graph* g, const double* channel_probs, int
   if ((rc = F->rp.alloc((size_t)(m + 1) * 4)) || (rc = F->ci.alloc(std::max(E, 1) * (size_t)4)) ||
       (rc = F->cp.alloc((size_t)(n + 1) * 4)) || (rc = F->crow.alloc(std::max(E, 1) * (size_t)4)) ||
       (rc = F->csb.alloc(std::max(E, 1))) || (rc = F->cmag.alloc(std::max(E, 1) * ts)) ||
-      (rc = F->prior.alloc(std::max(n, 1) * ts)))
+      (rc = F->prior.alloc(std::max(n, 1) * ts)) || (m <= 64 && (rc = F->colm.alloc(colm.size() * 8))))
     return fail(rc);
+  if (m <= 64 && hipMemcpy(F->colm.p, colm.data(), colm.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(set_err(QLDPC_EHIP, "upload first-min column masks"));
   if (hipMemcpy(F->rp.p, g->row_ptr.data(), (size_t)(m + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
       (E && hipMemcpy(F->ci.p, g->col_idx.data(), (size_t)E * 4, hipMemcpyHostToDevice) != hipSuccess) ||
       hipMemcpy(F->cp.p, cp.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
@@ -257,10 +324,58 @@ int qldpc_firstmin_create(const qldpc_graph* g, const double* channel_probs, int
   return 0;
 }
 
+}  // extern "C"
+
+int qldpc_rt::bp1_decode(qldpc_firstmin* fm, const uint8_t* d_synd, uint8_t* d_corr, int32_t* d_iters, uint8_t* d_conv,
+                         int64_t B, hipStream_t stream) {
+  if (!fm || (B > 0 && (!d_synd || !d_corr))) return set_err(QLDPC_EINVAL, "NULL argument");
+  if (B <= 0) return 0;
+  FmArgs a;
+  a.rp = static_cast<const int32_t*>(fm->rp.p);
+  a.ci = static_cast<const int32_t*>(fm->ci.p);
+  a.cp = static_cast<const int32_t*>(fm->cp.p);
+  a.crow = static_cast<const int32_t*>(fm->crow.p);
+  a.csb = static_cast<const uint8_t*>(fm->csb.p);
+  a.cmag = fm->cmag.p;
+  a.prior = fm->prior.p;
+  a.synd = d_synd;
+  a.corr = d_corr;
+  a.steps = d_iters;
+  a.conv = d_conv;
+  a.B = B;
+  a.m = fm->m;
+  a.n = fm->n;
+  a.max_iter = 0;
+  if (fm->colm.p) {  // <= 64 checks: one thread per syndrome
+    const unsigned g1 = (unsigned)((B + 255) / 256);
+    const auto* cm = static_cast<const unsigned long long*>(fm->colm.p);
+    const size_t sl = (size_t)256 * (fm->m + fm->n);
+    const bool stg = sl <= 64 * 1024;
+    if (fm->precision == 64) {
+      if (stg) hipLaunchKernelGGL((bp1_small_kernel<double, true>), dim3(g1), dim3(256), sl, stream, a, cm);
+      else hipLaunchKernelGGL((bp1_small_kernel<double, false>), dim3(g1), dim3(256), 0, stream, a, cm);
+    } else {
+      if (stg) hipLaunchKernelGGL((bp1_small_kernel<float, true>), dim3(g1), dim3(256), sl, stream, a, cm);
+      else hipLaunchKernelGGL((bp1_small_kernel<float, false>), dim3(g1), dim3(256), 0, stream, a, cm);
+    }
+    QLDPC_HIP(hipGetLastError());
+    return 0;
+  }
+  const int grid = (int)std::min<long long>(B, fm->grid);
+  if (fm->precision == 64)
+    hipLaunchKernelGGL((firstmin_kernel<double, true>), dim3(grid), dim3(kFmThreads), fm->lds, stream, a);
+  else
+    hipLaunchKernelGGL((firstmin_kernel<float, true>), dim3(grid), dim3(kFmThreads), fm->lds, stream, a);
+  QLDPC_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" {
+
 int qldpc_firstmin_destroy(qldpc_firstmin* fm) {
   if (!fm) return 0;
   fm->rp.release(); fm->ci.release(); fm->cp.release(); fm->crow.release(); fm->csb.release(); fm->cmag.release();
-  fm->prior.release();
+  fm->prior.release(); fm->colm.release();
   delete fm;
   return 0;
 }
@@ -281,6 +396,7 @@ int qldpc_firstmin_decode(qldpc_firstmin* fm, const uint8_t* d_synd, uint8_t* d_
   a.synd = d_synd;
   a.corr = d_corr;
   a.steps = d_steps;
+  a.conv = nullptr;
   a.B = B;
   a.m = fm->m;
   a.n = fm->n;

@@ -1431,6 +1431,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
 
 int qldpc_bp_destroy(qldpc_bp* bp) {
   if (!bp) return 0;
+  if (bp->bp1) qldpc_firstmin_destroy(bp->bp1);
   for (DevBuf* d : {&bp->vchk, &bp->llr, &bp->rdeg, &bp->rowtab, &bp->perm, &bp->rperm, &bp->work, &bp->ps_rp, &bp->ps_ci, &bp->ps_cp,
                     &bp->ps_ce, &bp->ps_ws, &bp->h_rp, &bp->h_rcol, &bp->h_rcpos, &bp->h_cp, &bp->h_crpos, &bp->h_ws})
     d->release();
@@ -1446,6 +1447,11 @@ int qldpc_bp_set_channel_probs(qldpc_bp* bp, const double* channel_probs) {
         return set_err(QLDPC_ENOTSUP, "this decoder's kernels hold one uniform prior: create a new decoder for "
                                       "non-uniform channel_probs");
   bp->probs.assign(channel_probs, channel_probs + bp->g->n);
+  if (bp->bp1) {  // rebuilt from the new priors on the next one-iteration decode
+    qldpc_firstmin_destroy(bp->bp1);
+    bp->bp1 = nullptr;
+  }
+  bp->bp1_off = false;
   return upload_llr(bp);
 }
 
@@ -1609,6 +1615,18 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
   if (!bp || (B > 0 && (!d_synd || !d_corr))) return set_err(QLDPC_EINVAL, "NULL argument");
   if (B == 0) return 0;
   QLDPC_HIP(hipSetDevice(bp->g->device));
+  // max_iter = 1 min-sum (the circuit loop's h1 rounds: max_iter = int(18 / 10)): a one-iteration BP
+  // from fresh state is the first-min step kernel (per-edge magnitudes fixed by the priors, bit-exact
+  // with every engine); QLDPC_BP1=0 keeps the engine
+  if (!d_post && bp->max_iter == 1 && bp->method == 1 && !bp->bp1_off) {
+    if (!bp->bp1) {
+      if (env_int("QLDPC_BP1", 1) == 0 || qldpc_firstmin_create(bp->g, bp->probs.data(), 0, bp->alpha, bp->precision, &bp->bp1) != 0) {
+        bp->bp1 = nullptr;
+        bp->bp1_off = true;  // (graph past the kernel's LDS envelope: the engine decodes)
+      }
+    }
+    if (bp->bp1) return qldpc_rt::bp1_decode(bp->bp1, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
+  }
   if (bp->engine == 5) return ps_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
   if (bp->engine == 6) return hbm_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
   const long long cap = (long long)bp->blocks_per_cu * bp->cus;

@@ -67,6 +67,10 @@ struct qldpc_bp {
   int nch = 0;  // engine 2: 16-byte chunks per check row
   int lds_bytes = 0, blocks_per_cu = 0, cus = 0;
   std::vector<double> probs;
+  // max_iter = 1 min-sum decodes (qldpc_bp_decode_batch): the first-min step kernel's one-iteration
+  // BP (firstmin.hip), built on first use from these priors; dropped when they change
+  qldpc_firstmin* bp1 = nullptr;
+  bool bp1_off = false;
   qldpc_rt::DevBuf vchk, llr;  // engine 1: packed u16 check ids; engines 2-4: edge words (check | slot<<16)
   qldpc_rt::DevBuf rdeg;       // engines 3/4: u8 row degrees (by check label)
   qldpc_rt::DevBuf rowtab;     // m2v: the check phase's row table [kM2vRows][TB] x 4 u32
@@ -142,6 +146,10 @@ bool osd_host_matches(const qldpc_osd* o, const qldpc_graph* g);
 int osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* host, qldpc_osd_gpu** out);
 // true when the first-min decoder was built on exactly this graph (shape and edges) and device
 bool firstmin_matches(const qldpc_firstmin* fm, const qldpc_graph* g);
+// one-iteration min-sum BP through a first-min handle (built with max_iter 0): corrections, iterations
+// (1) and convergence (H d == s), the qldpc_bp_decode_batch contract at max_iter = 1
+int bp1_decode(qldpc_firstmin* fm, const uint8_t* d_synd, uint8_t* d_corr, int32_t* d_iters, uint8_t* d_conv,
+               int64_t B, hipStream_t stream);
 // BP+OSD stage of the fused shot loop, one sector (osd.hip)
 int osd_gpu_bposd_stage(qldpc_osd_gpu* osd, const uint8_t* synd, const double* post, const uint8_t* err,
                         const long long* shot, uint8_t* outw, long long ncand, const unsigned long long* lmask, int kw,

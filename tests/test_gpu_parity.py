@@ -20,6 +20,38 @@ def _sample_synd(H, p, B, seed):
 
 
 @pytest.mark.parametrize("precision", [64, 32])
+@pytest.mark.parametrize("name", ["hgp_34_n225", "hgp_34_n1600", "LP_Matg8_L30_Dmin20", "rand40x120"])
+def test_one_iteration_decode_matches_oracle(gpu, oracle, monkeypatch, precision, name):
+    """max_iter = 1 min-sum decodes (the circuit loop's h1 rounds) run the first-min step kernel
+    (qldpc_bp_decode_batch's one-iteration path): corrections, iterations and convergence equal the
+    oracle and the engine's own kernels (QLDPC_BP1=0), with non-uniform and tied priors, alpha 0.625
+    and ldpc's alpha = 0 schedule."""
+    from qldpc_fault_tolerance_amd.engine import DeviceBP
+
+    if name == "rand40x120":  # <= 64 checks: the thread-per-syndrome kernel
+        g = np.random.default_rng(3)
+        H = np.zeros((40, 120), np.uint8)
+        for j in range(120):
+            H[g.choice(40, 3, replace=False), j] = 1
+        n = 120
+    else:
+        H = codes.get_code(name).hz
+        n = H.shape[1]
+    rng = np.random.default_rng(n + precision)
+    pr = rng.uniform(0.01, 0.1, n)
+    pr[::4] = pr[1]
+    synd = _sample_synd(H, 0.05, 300, seed=precision)
+    for alpha in (0.625, 0.0):
+        c, i, v = DeviceBP(H, pr, max_iter=1, ms_scaling_factor=alpha, precision=precision).decode_batch(synd)
+        oc, oi, ov = oracle.bp_decode_batch(H, pr, 1, "minimum_sum", alpha, synd, precision)
+        assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64)), alpha
+        monkeypatch.setenv("QLDPC_BP1", "0")
+        c2, i2, v2 = DeviceBP(H, pr, max_iter=1, ms_scaling_factor=alpha, precision=precision).decode_batch(synd)
+        monkeypatch.delenv("QLDPC_BP1")
+        assert np.array_equal(c2, c) and np.array_equal(i2, i) and np.array_equal(v2, v), alpha
+
+
+@pytest.mark.parametrize("precision", [64, 32])
 @pytest.mark.parametrize("name,ratio", [("hgp_34_n225", 10), ("GenBicycleA2", 10), ("LP_Matg8_L16_Dmin12", 10)])
 def test_decode_batch_matches_oracle(gpu, oracle, precision, name, ratio):
     from qldpc_fault_tolerance_amd.engine import DeviceBP
