@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "runtime.h"
@@ -159,6 +160,85 @@ __global__ void __launch_bounds__(kFmThreads) firstmin_kernel(FmArgs a) {
 // same (uniform) order by every lane (scalar / broadcast loads).  The workgroup-per-syndrome kernel
 // above spends its time in barriers on such graphs (0.20 ms per 65,536 syndromes against the
 // engine's 0.18).  Same adds in the same order: identical decisions.
+// One WAVE per syndrome (4 per 256-thread workgroup), no workgroup barrier: a wave's LDS accesses
+// are processed in order, so the running syndrome / decision arrays only need the compiler fence
+// between a wave's writes and its other lanes' reads; the weights are wave sums.  Same steps, same
+// arithmetic as firstmin_kernel.
+__device__ inline int wave_sum_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+#define FM_WAVE_FENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront")
+
+template <typename T>
+__global__ void __launch_bounds__(256) firstmin_wave_kernel(FmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, m = a.m, n = a.n;
+  const size_t per = ((size_t)2 * m + (size_t)2 * n + 15) & ~(size_t)15;
+  uint8_t* cur = sm + (size_t)wv * per;
+  uint8_t* nsy = cur + m;
+  uint8_t* dec = nsy + m;
+  uint8_t* cor = dec + n;
+  const T* mag = static_cast<const T*>(a.cmag);
+  const T* prior = static_cast<const T*>(a.prior);
+  auto step = [&]() -> int {
+    for (int j = lane; j < n; j += 64) {
+      T post = prior[j];
+      for (int k = a.cp[j]; k < a.cp[j + 1]; ++k) {
+        const T c = mag[k];
+        post += ((cur[a.crow[k]] ^ a.csb[k]) & 1u) ? -c : c;
+      }
+      dec[j] = post <= (T)0 ? 1 : 0;
+    }
+    FM_WAVE_FENCE();
+    int w = 0;
+    for (int i = lane; i < m; i += 64) {
+      uint8_t x = cur[i];
+      for (int e = a.rp[i]; e < a.rp[i + 1]; ++e) x ^= dec[a.ci[e]];
+      nsy[i] = x;
+      w += x;
+    }
+    FM_WAVE_FENCE();
+    return wave_sum_i32(w);
+  };
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long b = (long long)blockIdx.x * 4 + wv; b < a.B; b += nw) {  // uniform per wave
+    const uint8_t* sy = a.synd + b * (long long)m;
+    int w = 0;
+    for (int i = lane; i < m; i += 64) {
+      const uint8_t x = sy[i] & 1u;
+      cur[i] = x;
+      w += x;
+    }
+    for (int j = lane; j < n; j += 64) cor[j] = 0;
+    FM_WAVE_FENCE();
+    int wc = wave_sum_i32(w);
+    int k = 0;
+    int wn = step();
+    while (wn <= wc && k < a.max_iter) {  // uniform per wave
+      if (wc == 0) {  // cur = 0: does BP1(0) decide anything?
+        int any = 0;
+        for (int j = lane; j < n; j += 64) any |= dec[j];
+        if (!__any(any)) {
+          k = a.max_iter;
+          break;
+        }
+      }
+      for (int i = lane; i < m; i += 64) cur[i] = nsy[i];
+      for (int j = lane; j < n; j += 64) cor[j] ^= dec[j];
+      ++k;
+      wc = wn;
+      FM_WAVE_FENCE();
+      wn = step();
+    }
+    uint8_t* out = a.corr + b * (long long)n;
+    for (int j = lane; j < n; j += 64) out[j] = cor[j];
+    if (lane == 0 && a.steps) a.steps[b] = k;
+    FM_WAVE_FENCE();
+  }
+}
+
 // STG: the workgroup's 256 syndromes and decisions staged through LDS (coalesced global reads and
 // writes of its contiguous [256][m] / [256][n] blocks) when 256 (m + n) bytes fit
 template <typename T, bool STG>
@@ -401,6 +481,18 @@ int qldpc_firstmin_decode(qldpc_firstmin* fm, const uint8_t* d_synd, uint8_t* d_
   a.m = fm->m;
   a.n = fm->n;
   a.max_iter = fm->max_iter;
+  // one wave per syndrome when four syndromes' arrays fit 64 KiB (QLDPC_FM_WAVE=0: one workgroup each)
+  const size_t per = ((size_t)2 * fm->m + (size_t)2 * fm->n + 15) & ~(size_t)15;
+  const char* we = std::getenv("QLDPC_FM_WAVE");
+  if (4 * per <= 64 * 1024 && !(we && std::atoi(we) == 0)) {
+    const int gw = (int)std::min<long long>((B + 3) / 4, (long long)fm->grid * 4);
+    if (fm->precision == 64)
+      hipLaunchKernelGGL(firstmin_wave_kernel<double>, dim3(gw), dim3(256), 4 * per, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(firstmin_wave_kernel<float>, dim3(gw), dim3(256), 4 * per, (hipStream_t)stream, a);
+    QLDPC_HIP(hipGetLastError());
+    return 0;
+  }
   const int grid = (int)std::min<long long>(B, fm->grid);
   if (fm->precision == 64)
     hipLaunchKernelGGL(firstmin_kernel<double>, dim3(grid), dim3(kFmThreads), fm->lds, (hipStream_t)stream, a);

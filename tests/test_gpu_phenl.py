@@ -227,8 +227,9 @@ def test_firstmin_decoder_matches_reference_fixture(gpu):
     assert np.array_equal(fm.decode(g["firstmin_synd"][3]).astype(np.uint8), g["firstmin_corr"][3])
 
 
+@pytest.mark.parametrize("kernel", ["wave", "wg"])
 @pytest.mark.parametrize("precision,alpha", [(64, 0.625), (32, 0.625), (64, 0.0), (64, 0.9)])
-def test_firstmin_device_loop_matches_reference_algorithm(gpu, oracle, precision, alpha):
+def test_firstmin_device_loop_matches_reference_algorithm(gpu, oracle, monkeypatch, precision, alpha, kernel):
     """The device-resident first-min loop (qldpc_firstmin_*, one kernel) == the reference's
     FirstMinBPDecoder.decode loop (src/Decoders.py:60-74) run over the oracle's one-iteration BP,
     per syndrome (corrections and accepted steps), with non-uniform priors on [h | I], including
@@ -243,6 +244,8 @@ def test_firstmin_device_loop_matches_reference_algorithm(gpu, oracle, precision
     synd = (e.astype(np.int64) @ hz_ext.T.astype(np.int64) % 2).astype(np.uint8)
     synd[0] = 0
     mi = 12
+    if kernel == "wg":  # one workgroup per syndrome instead of one wave
+        monkeypatch.setenv("QLDPC_FM_WAVE", "0")
     fm = decoders.FirstMinBPDecoder(hz_ext, probs, mi, "minimum_sum", alpha, precision=precision)
     out = fm.decode_batch(synd)
     H = hz_ext.astype(np.int64)
