@@ -412,6 +412,10 @@ constexpr int kOsdXB = QLDPC_OSD_XB;
 #define QLDPC_OSD_G 4
 #endif
 constexpr bool kOsdM4R = QLDPC_OSD_M4R && !QLDPC_OSD_1B;
+// A/B build: OSD steps 4-5 from the register rows (see the RR branch's end); 0 = the HBM path
+#ifndef QLDPC_OSD_XREG
+#define QLDPC_OSD_XREG 0
+#endif
 // diagnostic A/B build: the lean loop's row xors done three times (same rows): the step's
 // sensitivity to its row-update VALU work
 #ifndef QLDPC_OSD_XOR3
@@ -633,6 +637,7 @@ osd_gpu_kernel(OsdGpuArgs A) {
       s_pivx = 0u;
     }
     __syncthreads();
+    bool xdone = false;  // uniform: S0 / x(h_j) built from the register rows (steps 4-5 done)
     if constexpr (kRR) {
       // 2-3 (register rows): rows tid + j*TB (j < RPT) of the permuted H, words by compile-time index
       u64 row[RPT][WR];
@@ -1742,10 +1747,77 @@ osd_gpu_kernel(OsdGpuArgs A) {
         __syncthreads();
         continue;
       }
+      // Steps 4-5 from the registers (osd_e / osd_0, round 5): the reduced rows never leave them.
+      // The swap trace runs on one wave with the staged pivot positions read 64 at a time (one LDS
+      // round trip per 64 transpositions instead of one per transposition), the needed non-pivot
+      // positions Ht[j] go to LDS, and every pivot row writes its bits of S0 / x(h_j) as bytes at
+      // its pivot index (no atomics: one writer per index), packed by one ballot per word; the
+      // reduced-row write-out to the HBM slice and step 5's two dependent global reads per bit are
+      // gone.  MEASURED AND NOT KEPT (A/B build QLDPC_OSD_XREG=1): bit-exact (96 BP+OSD / circuit
+      // GPU tests), but the n1600 OSD total is unchanged (1.672 M vs 1.675 M cycles per syndrome,
+      // BP+OSD 605 k vs 614 k shots/s, profiles/r05/osd_notkept/xreg_*): the steps' time is not the
+      // HBM round trips this removes.
+      const int rW = (npiv + 63) / 64;
+      if (QLDPC_OSD_XREG && PNL != 5 && nh <= 31 && (size_t)4 * (m + 32) + (size_t)(1 + nh) * npiv <= (size_t)NP * 8) {  // uniform
+        if (tid == 0) s_npiv = npiv;
+        int32_t* rowpiv = reinterpret_cast<int32_t*>(smem);  // [m] pivot index of each row, -1 (over the dead keys)
+        int32_t* swl = rowpiv + m;                          // [32] Ht positions
+        uint8_t* xb = reinterpret_cast<uint8_t*>(swl + 32);  // [1 + nh][npiv] bits of S0 / x(h_j) by pivot index
+        int32_t* lpp = reinterpret_cast<int32_t*>(smem + A.pbuf_off + (size_t)(osd_prows(LB) + (PNL == 4 ? 1 : 0)) * (WR + 1) * 8);
+        __syncthreads();  // pivrow / pivpos written, the (dead) pivot list read
+        for (int i = tid; i < npiv; i += TB) lpp[i] = pivpos[i];
+        for (int i = tid; i < m; i += TB) rowpiv[i] = -1;
+        __syncthreads();
+        for (int i = tid; i < npiv; i += TB) rowpiv[pivrow[i]] = i;
+        if (tid < 64) {  // wave 0: lane j traces position npiv + j back through the transpositions
+          int cur = npiv + tid;
+          for (int c0 = ((npiv - 1) >> 6) << 6; c0 >= 0; c0 -= 64) {  // uniform
+            const int il = c0 + tid;
+            const int v = il < npiv ? lpp[il] : 0;
+            const int top = npiv - 1 - c0 < 63 ? npiv - 1 - c0 : 63;
+            for (int t = top; t >= 0; --t) {  // uniform
+              const int pi = __builtin_amdgcn_readlane(v, t);
+              const int i = c0 + t;
+              cur = cur == i ? pi : (cur == pi ? i : cur);
+            }
+          }
+          if (tid < nh && npiv + tid < n) {
+            swp[npiv + tid] = cur;
+            swl[tid] = cur;
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+          const int i = tid + j * TB;
+          const int k = i < m ? rowpiv[i] : -1;
+          if (k >= 0) {
+            xb[k] = (uint8_t)(sbit[j] & 1u);
+            for (int jj = 0; jj < nh; ++jj) {  // uniform
+              const int hp = swl[jj];
+              const int hq = hp >> 6;
+              u64 wsel = 0;
+              osd_for_words(std::make_integer_sequence<int, WR>{}, [&](auto Qc) __attribute__((always_inline)) {
+                constexpr int Q = decltype(Qc)::value;
+                if (Q == hq) wsel = row[j][Q];
+                return true;
+              });
+              xb[(size_t)(1 + jj) * npiv + k] = (uint8_t)((wsel >> (hp & 63)) & 1ull);
+            }
+          }
+        }
+        __syncthreads();
+        for (int t = tid >> 6; t < (1 + nh) * rW; t += TB >> 6) {  // uniform per wave: one ballot per word
+          const int jj = t / rW, q = t % rW, i = q * 64 + (tid & 63);
+          const unsigned long long v = __ballot(i < npiv && xb[(size_t)jj * npiv + i] != 0);
+          if ((tid & 63) == 0) X[(size_t)jj * RW + q] = v;
+        }
+        xdone = true;
+      }
       // reduced rows -> the HBM slice (word-major), syndrome bits -> sb (forward elimination: the
       // pivot rows are there already, in pivot order)
 #pragma unroll
-      for (int j = 0; j < RPT && PNL != 5; ++j) {
+      for (int j = 0; j < RPT && PNL != 5 && !xdone; ++j) {
         const int i = tid + j * TB;
         if (i < m) {
           // opaque row pointer: the compiler otherwise hoists the WR word addresses out of the
@@ -1871,6 +1943,8 @@ osd_gpu_kernel(OsdGpuArgs A) {
     }
     const int r = s_npiv;
     OSD_ST(2)
+    const int RWr = (r + 63) / 64;
+    if (!xdone) {  // (register rows, osd_e / osd_0: done from the registers above)
     // 4. Neal's column swaps -> non-pivot order Ht.  Only the non-pivot positions swp[r + j],
     // j < nh, are used: each is the identity traced backwards through the transpositions
     // (i, pivpos[i]), i = r-1 .. 0 -- one thread per needed position, no serial replay.
@@ -1893,7 +1967,6 @@ osd_gpu_kernel(OsdGpuArgs A) {
     __syncthreads();
     // 5. S0 and x(h_j) as bit-vectors over the pivot index: one wave per 64-bit word, lane c
     // forms bit c (pivot q*64 + c) and a ballot packs the word
-    const int RWr = (r + 63) / 64;
     if constexpr (kRR && PNL == 5) {
       // 5'. (forward elimination) the Jordan half on the right-hand sides: thread k holds pivot row
       // k (final since it was chosen, HBM slice row k) and b_k = (syndrome bit, bits Ht[j] of the
@@ -1977,6 +2050,7 @@ osd_gpu_kernel(OsdGpuArgs A) {
       const unsigned long long v = __ballot(bitv);
       if (c == 0) X[(size_t)j * RW + q] = v;
     }
+    }  // !xdone
     if (tid == 0) s_best = ~0ull;
     __syncthreads();
     OSD_ST(3)
