@@ -9,3 +9,5 @@ timeout -k 10 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-m
 tail -3 "$O/pytest_gpu.out"
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.out" 2>&1 || { echo "smoke failed"; tail -5 "$O/smoke.out"; exit 1; }
 tail -1 "$O/smoke.out"
+timeout -k 10 300 python -u bench.py --workload bposd --p 0.04 --steps 2 --warmup 1 --no-cpu-baseline > "$O/bposd.out" 2> "$O/bposd.err" || { echo "bposd failed"; tail -5 "$O/bposd.err"; exit 1; }
+tail -1 "$O/bposd.out" | cut -c1-200
