@@ -44,14 +44,23 @@ SEED = 0x51D5EED0 + 2  # seed = 0x51D5EED0 + config_id (config 2
 LDS_PEAK_GBS = 75_000.0
 HBM_PEAK_GBS = 8_000.0
 LDS_CALIB = os.path.join(ROOT, "profiles", "r05", "calib", "lds_peak.jsonl")
-_LDS_CYC = {"ds_read_b64": 2, "ds_read_b128": 4, "ds_write_b64": 6, "ds_write_b128": 13}
-# per family: (edges per row, {instruction: count per wave-row}, calib mode or None, description)
+_LDS_CYC = {"ds_read_b64": 2, "ds_read_b128": 4, "ds_write_b32": 4, "ds_write_b64": 6, "ds_write_b128": 13}
+# per family: (edges per row, {instruction: count per wave-row}, calib mode or None, description
+# [, algorithmic bytes per edge-iteration: 32 in fp64 (default), 16 in fp32])
 LDS_MIX = {
+    "f32w": (7, {"ds_read_b64": 7, "ds_read_b128": 2, "ds_write_b32": 7, "ds_write_b64": 1}, None,
+             "fp32 two-word row of 7 in 2 chunks (engine id 3, compile-time 2-chunk rows, own v2c in VGPRs: the "
+             "headline code's fp32 fast mode): 7 x (CS gather b64 + v2c store b32) + the row (2 x b128) + the CS "
+             "store (b64) = 56 cycles per 7 x 16 B x 64 lanes", 16),
     "m2s": (7, {"ds_read_b64": 15, "ds_read_b128": 3, "ds_write_b64": 9}, "m2s_row_mix",
             "m2s row of 7 (engine id 11103): 7 x (CS gather b64 + V-slot read b64 + v2c store b64) + the row "
             "(3 x b128 + tail b64) + CS / argmin-slot stores (2 x b64) = 96 cycles"),
     "m2s8": (8, {"ds_read_b64": 16, "ds_read_b128": 4, "ds_write_b64": 10}, "m2s8_row_mix",
              "m2s8 row of 8 (engine ids 10103 / 10203): 8 x (b64 + b64 + store b64) + 4 x b128 + 2 x store b64 = 108 cycles"),
+    "st64m2s": (9, {"ds_read_b64": 19, "ds_read_b128": 4, "ds_write_b64": 11}, None,
+                "fp64 one-word tail row of 9 (engine ids 11313 / 111313, round 6: 1024-thread workgroups, own v2c "
+                "in VGPRs): 9 x (CS gather b64 + V-slot read b64 + v2c store b64) + the row (4 x b128 + tail b64) + "
+                "CS / argmin-slot stores (2 x b64) = 120 cycles"),
     "st64": (9, {"ds_read_b64": 10, "ds_read_b128": 13, "ds_write_b64": 9, "ds_write_b128": 1}, None,
              "fp64 two-word tail row of 9 (engine ids 1013 / 101013; 1024-thread workgroups, 128-VGPR budget: the "
              "own previous v2c is re-read from LDS, bp_reg.h RState::kKeepV false): 9 x (CS gather b128 + own V-slot "
@@ -61,10 +70,11 @@ LDS_MIX = {
 
 def lds_ceiling(kind):
     """(GB/s algorithmic, provenance dict) of an LDS-bound kernel family's row mix."""
-    edges, mix, mode, what = LDS_MIX[kind]
+    edges, mix, mode, what = LDS_MIX[kind][:4]
+    bpe = LDS_MIX[kind][4] if len(LDS_MIX[kind]) > 4 else 32
     cyc = sum(_LDS_CYC[k] * v for k, v in mix.items())
-    gbs = 64 * edges * 32 / cyc * 256 * 2.4  # B per cycle per CU x CUs x GHz
-    prov = {"family": kind, "mix": mix, "cycles_per_wave_row": cyc, "algorithmic_bytes_per_wave_row": 64 * edges * 32,
+    gbs = 64 * edges * bpe / cyc * 256 * 2.4  # B per cycle per CU x CUs x GHz
+    prov = {"family": kind, "mix": mix, "cycles_per_wave_row": cyc, "algorithmic_bytes_per_wave_row": 64 * edges * bpe,
             "what": what, "source": "MI355X_MICROARCH.md §LDS cycle table, 256 CUs x 2.4 GHz"}
     if mode:
         try:
@@ -81,8 +91,10 @@ def lds_ceiling(kind):
     return gbs, prov
 
 
-def mix_of_kernel(kernel_id, precision):
+def mix_of_kernel(kernel_id, precision, row_width=None):
     """The LDS_MIX family of an engine-3 kernel id (None: no row-mix ceiling derived; the guide aggregate)."""
+    if precision == 32 and kernel_id == 3 and row_width == 7:
+        return "f32w"
     if precision != 64 or kernel_id is None:
         return None
     if kernel_id == 11103:
@@ -91,6 +103,8 @@ def mix_of_kernel(kernel_id, precision):
         return "m2s8"
     if kernel_id % 100000 in (1013, 101013) or kernel_id in (1013, 101013):
         return "st64"
+    if kernel_id % 100000 == 11313:
+        return "st64m2s"
     return None
 
 
@@ -706,6 +720,44 @@ def native_comm_main(a, torch):
           "logical_error_rate": res.failures / max(res.shots, 1), "comm": "native"})
 
 
+def circuit_kernel_roofline(torch, sim, g, dev, B):
+    """The circuit loop's dominant kernel (the h1 round decode, 27 % of the r05 trace, profiles/r05/final/
+    circuit_kernel_stats.csv) alone: decoder1's decode_batch over B round-0 syndromes of DEM samples,
+    timed with HIP events on its stream (3 launches after 1 warm-up).  max_iter = int(N / 10) = 1 here,
+    so the decode is the one-iteration first-min step kernel: it reads the precomputed
+    per-edge magnitudes and never moves messages through LDS, so the bound is its HBM I/O (u8 syndrome
+    in, u8 correction / int32 iterations / u8 flag out per syndrome) against 8 TB/s; the §8d message
+    bytes of the same decodes (32 B per edge-iteration) are reported beside it."""
+    dec1 = sim.decoder1_z.decoder
+    R1, n1 = int(np.shape(g["h1"])[0]), int(np.shape(g["h1"])[1])
+    E1 = int(np.asarray(g["h1"]).astype(bool).sum())
+    det = sim._device().sample(sim.seed, 1 << 40, B)[:, :R1]  # round 0's detectors (no space correction yet)
+    synd = torch.from_numpy(np.ascontiguousarray(det.astype(np.uint8))).to(dev)
+    corr = torch.empty((B, n1), dtype=torch.uint8, device=dev)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)
+    conv = torch.empty(B, dtype=torch.uint8, device=dev)
+    dec1.decode_batch_device(synd, corr, iters, conv)
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 3
+    ev0.record()
+    for _ in range(reps):
+        dec1.decode_batch_device(synd, corr, iters, conv)
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    ms = ev0.elapsed_time(ev1) / reps
+    io = B * (R1 + n1 + 4 + 1)
+    it = int(iters.sum().item())
+    ach = io / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": None, "kernel": f"decoder1 h1 decode_batch ({R1}x{n1}, max_iter {dec1.max_iter}: "
+                                        f"{'one-iteration first-min step kernel' if dec1.max_iter == 1 else 'BP engine'})",
+            "kernel_ms": ms, "bytes_per_launch": io, "decodes_per_launch": B,
+            "algorithmic_message_bytes_GBs": 32 * E1 * it / (ms * 1e-3) / 1e9,
+            "note": "HBM I/O per syndrome (R1 + n1 + 5 B) over the HIP-event time; the loop is launch- and "
+                    "latency-bound at this graph size (DESIGN.md §4 circuit)"}
+
+
 def circuit_main(a, torch, dist, world, rank, dev):
     """Circuit-level space-time (not the headline): the demo configuration of
     SpaceTimeDecodingDemo.ipynb cell 2 (hgp(ring_code(3), ring_code(3)), p = 1e-3, CX noise only,
@@ -764,7 +816,8 @@ def circuit_main(a, torch, dist, world, rank, dev):
            "logical_error_rate": fails / max(shots, 1),
            "wer_per_cycle": word_error_rate_per_cycle(fails, shots, code.K, a.num_cycles),
            "printed_reference_wer": 0.00019299501269032238 if p == 1e-3 and a.num_cycles == 13 and a.num_rep == 3
-           else None}
+           else None,
+           "roofline": circuit_kernel_roofline(torch, sim, g, dev, min(S, 65536))}
     if rank == 0:
         emit(out)
     if world > 1:
@@ -903,11 +956,18 @@ def main():
     if world == 1 and a.precision == 64 and a.fp32_line:
         # fp32 fast mode on the same workload: reported beside the headline, never as `value`
         r32 = time_data(a, 32, torch, dist, world, rank, dev)
+        # on the headline's basis: the same algorithmic bytes (16 B per edge-iteration in fp32) over the
+        # kernel's HIP-event time, against its own family's LDS row-mix ceiling
+        ach32 = (16 * E * r32["iters"] / a.steps + r32["decodes"] / a.steps * ((mh + 7) // 8 + (nh + 7) // 8 + 16)) \
+            / (r32["kern_ms"] * 1e-3) / 1e9
+        fam32 = mix_of_kernel(r32.get("kernel_id"), 32, E // mh if E % mh == 0 else None)
+        peak32, src32 = lds_ceiling(fam32) if fam32 else (LDS_PEAK_GBS, "MI355X_MICROARCH.md aggregate")
         out["fp32_fast_mode"] = {
             "value": r32["value"], "unit": "shots/s", "ms_per_step": r32["elapsed"] / a.steps * 1e3,
             "kernel": r32["kernel"], "kernel_ms": r32["kern_ms"],
-            "roofline_frac": (16 * E * r32["iters"] / a.steps + r32["decodes"] / a.steps * ((mh + 7) // 8 + (nh + 7) // 8 + 16))
-            / (r32["kern_ms"] * 1e-3) / 1e9 / LDS_PEAK_GBS,
+            "roofline": {"bound": "lds", "achieved": ach32, "peak": peak32, "unit": "GB/s", "frac": ach32 / peak32,
+                         "peak_source": src32, "frac_guide_aggregate": ach32 / LDS_PEAK_GBS},
+            "roofline_frac": ach32 / peak32,
             "logical_error_rate": r32["failures"] / max(r32["shots"], 1),
             "note": "float32 messages: NOT ldpc's float64 arithmetic (decoded-vector agreement with fp64 is "
                     "measured in tests/test_gpu_agreement.py)"}

@@ -391,7 +391,7 @@ int qldpc_mc_run_sharded(qldpc_mc **mcs, qldpc_comm **comms, int32_t ndev, doubl
  * 53-bit uniform is < probs[j] (shot = shot_begin + s).  Counters: shots, failures, sector 0 =
  * decoder1 decodes (num_rounds per sample), sector 1 = decoder2 decodes.  d_fail [S] (or NULL),
  * d_detobs [S][D + K] sampled detector and observable bits (or NULL).  Asynchronous on `stream`
- * (no host round trip, BP+OSD included).  dec1 = dec2 = NULL (and NULL h1_space_cor / L1 /
+ * (no host round trip, BP+OSD included, unless the OSD is a host stage past the GPU envelope).  dec1 = dec2 = NULL (and NULL h1_space_cor / L1 /
  * L2) makes a sampler-only handle for qldpc_circ_sample (decoders outside the engine).
  */
 typedef struct qldpc_circ qldpc_circ;
@@ -400,7 +400,9 @@ int qldpc_circ_create(const qldpc_graph *dem, const qldpc_graph *dem_obs, const 
                       int32_t num_rounds, int32_t num_rep, int64_t max_batch, qldpc_circ **out);
 /* decoder2 as bposd_decoder (ST_BPOSD_Decoder_Circuit, src/Decoders_SpaceTime.py:277-292): dec2 from
  * qldpc_bp_create_soft and ONE of a GPU OSD or a host OSD stage on h2; a host stage is turned into a
- * GPU OSD with its method, order, rank and soft weights, so the launch never leaves the device. */
+ * GPU OSD with its method, order, rank and soft weights, so the launch never leaves the device —
+ * except past the GPU kernel's envelope (n > 8192, osd_e order > 24), where the host stage decodes
+ * the final layer (one synchronous D2H / H2D round trip per batch inside qldpc_circ_launch). */
 int qldpc_circ_set_final_osd(qldpc_circ *circ, qldpc_osd_gpu *osd_gpu, const qldpc_osd *osd_host);
 int qldpc_circ_info(const qldpc_circ *circ, int32_t *detectors, int32_t *observables, int32_t *mechanisms);
 int qldpc_circ_launch(qldpc_circ *circ, uint64_t seed, uint64_t shot_begin, int64_t shot_count, void *d_counters,

@@ -39,8 +39,15 @@ class NativeUnavailable(RuntimeError):
     pass
 
 
+ENOTSUP = -4  # QLDPC_ENOTSUP (include/qldpc_hip.h)
+
+
 class QldpcError(RuntimeError):
-    pass
+    """A negative return code of the C ABI (``rc``: QLDPC_EINVAL, QLDPC_ENOTSUP, ...)."""
+
+    def __init__(self, msg: str = "", rc: int = 0):
+        super().__init__(msg)
+        self.rc = rc
 
 
 class Counters(ctypes.Structure):
@@ -219,7 +226,7 @@ def lib():
 def check(rc: int, what: str = "") -> None:
     if rc != 0:
         msg = lib().qldpc_last_error().decode(errors="replace")
-        raise QldpcError(f"{what} failed (rc={rc}): {msg}")
+        raise QldpcError(f"{what} failed (rc={rc}): {msg}", rc)
 
 
 def experimental_families() -> bool:

@@ -104,6 +104,9 @@ constexpr bool eng_m2s(int E) { return (E / 10000) % 10 == 1 || (E / 10000) % 10
 // phase reads and writes its slots lane-linearly (conflict-free, one base VGPR and immediate
 // offsets), and the check phase gathers its row's 7 slots from a per-thread register table
 constexpr bool eng_m2v(int E) { return (E / 10000) % 10 == 4; }
+// m2s + tail + dword-scaled packed addresses + 300 (own v2c in VGPRs, neither split nor byte-packed)
+// = engine id 11313 (+ 100000 * D2K): the fp64 space-time family (rows of 4 chunks + a tail slot,
+// 1024-thread workgroups, 128-VGPR budget, kern_r_f64_m2st.hip), round 6
 // edge slots of variable slots 0..k-1 (degree-3 slots k < D3K keep 3)
 template <int D3K>
 __host__ __device__ constexpr int m2v_ecnt(int k) { return 3 * (k < D3K ? k : D3K) + 4 * (k > D3K ? k - D3K : 0); }
@@ -405,7 +408,8 @@ __device__ inline void r_load(const SSector& S, RState<T, DMAX, VPL, ENG>& R, co
       } else if constexpr (RState<T, DMAX, VPL, ENG>::kPk) {  // absolute byte addresses, packed
         R.ea[k][t] = (sbase + echk(e) * (uint32_t)sizeof(T)) | ((sbase + va) << 16);
       } else if constexpr (RState<T, DMAX, VPL, ENG>::kAbs) {  // absolute dword indices
-        R.ea[k][t] = ((sbase + echk(e) * (uint32_t)(2 * sizeof(T))) >> 2) | (((sbase + va) >> 2) << 16);
+        // (m2s: one-word CS entries)
+        R.ea[k][t] = ((sbase + echk(e) * (uint32_t)((eng_m2s(ENG) ? 1 : 2) * sizeof(T))) >> 2) | (((sbase + va) >> 2) << 16);
       } else {
         R.ea[k][t] = ((echk(e) * (uint32_t)(2 * sizeof(T))) >> eng_sh(ENG)) | ((va >> eng_sh(ENG)) << 16);
       }
@@ -483,7 +487,8 @@ __device__ inline uint32_t r_fa(const RState<T, DMAX, VPL, ENG>& R, int k, int t
     // absolute dword index w = csa / 4 in the low half: csa >> 3 = w >> 1, csa >> 1 = 2 w, csa >> 2 = w
     const uint32_t w = R.ea[k][t];
     if constexpr (eng_fb(ENG)) return __builtin_amdgcn_ubfe(w, 1, 15) + fbase;
-    if constexpr (sizeof(T) == 4) return sdwa_shl<0, 1>(w) + fbase;
+    // fp32 two-word and fp64 one-word (m2s) CS entries are 8 bytes: F word = 2 x the dword index
+    if constexpr (sizeof(T) == 4 || eng_m2s(ENG)) return sdwa_shl<0, 1>(w) + fbase;
     return (w & 0xFFFFu) + fbase;
   }
   if constexpr (eng_fb(ENG)) return (r_csa(R, k, t) >> 3) + fbase;
@@ -980,9 +985,8 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
                                  double* post, const int32_t* perm) {
   using U = typename FT<T>::U;
   constexpr bool KV1 = RState<T, DMAX, VPL, ENG>::kKeepV;
-  static_assert(sizeof(T) == 8 && (RState<T, DMAX, VPL, ENG>::kSplit || RState<T, DMAX, VPL, ENG>::kPk) &&
-                    (RState<T, DMAX, VPL, ENG>::kKeepV || eng_c2s(ENG)),
-                "m2s / c2s: fp64 split-address family only");
+  static_assert(sizeof(T) == 8 && RState<T, DMAX, VPL, ENG>::kAbs && (RState<T, DMAX, VPL, ENG>::kKeepV || eng_c2s(ENG)),
+                "m2s / c2s: fp64 absolute-address families only");
   T c[ND];
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
@@ -1057,7 +1061,9 @@ __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   uint32_t xbits = 0;
   U ab[PF][DMAX], vb[PF][DMAX];
   auto gk = [&](int k, U (&an)[DMAX], U (&vn)[DMAX]) {
-    if (k < D3K)
+    if (k < eng_d2k(ENG))  // (the space-time family's measurement variables: two edge slots)
+      m_gather<T, DMAX, VPL, 2, ENG, D3K, LB>(R, k, an, vn);
+    else if (k < D3K)
       m_gather<T, DMAX, VPL, N3, ENG, D3K, LB>(R, k, an, vn);
     else
       m_gather<T, DMAX, VPL, DMAX, ENG, D3K, LB>(R, k, an, vn);
@@ -1076,8 +1082,9 @@ __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     if (k == VPL - 1 && !last_live) break;
     const bool xp = ((xprev >> k) & 1u) != 0;
     const int32_t* pk = perm ? perm + k * TB : nullptr;
-    const bool x = k < D3K ? m_var_one<T, DMAX, VPL, N3, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk)
-                           : m_var_one<T, DMAX, VPL, DMAX, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk);
+    const bool x = k < eng_d2k(ENG) ? m_var_one<T, DMAX, VPL, 2, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk)
+                   : k < D3K        ? m_var_one<T, DMAX, VPL, N3, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk)
+                                    : m_var_one<T, DMAX, VPL, DMAX, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk);
     xbits |= (x ? 1u : 0u) << k;
   }
   return xbits;

@@ -12,7 +12,8 @@
 //       effect (h1_space_cor · c) and logical effect (L1 · c) accumulate (:983-993);
 //   (4) the final m detector rows XOR the accumulated space correction, decoded by decoder2 on h2
 //       (BP, or BP + OSD on the GPU: the DEM's non-uniform priors weigh the OSD candidates by
-//       sum log(1 / p_j), osd.hip step 6'; no host round trip);
+//       sum log(1 / p_j), osd.hip step 6'; no host round trip — a host OSD stage past the GPU
+//       kernel's envelope decodes on the host, circ_host_osd);
 //   (5) failure = (final syndrome + h2 · c2 != 0) or (observables + Σ L · c != 0) (:996-1004).
 // State is BIT-SLICED between the stages (word w of row r = row r of samples 64w..64w+63), so the
 // mechanism scatter of (1)-(2) is one wave ballot + one 64-bit atomic xor per (mechanism row, 64
@@ -21,6 +22,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -188,6 +190,11 @@ struct qldpc_circ {
   qldpc_bp* dec2 = nullptr;
   qldpc_osd_gpu* osd_gpu = nullptr;
   qldpc_osd_gpu* osd_owned = nullptr;  // the GPU OSD built from a host stage (qldpc_circ_set_final_osd)
+  // a host stage past the GPU kernel's envelope (n > 8192, osd_e order > 24, priors of 0 or 1): the
+  // final layer's soft BP output goes to the host, through qldpc_osd_decode_batch, and back
+  const qldpc_osd* osd_host = nullptr;
+  std::vector<uint8_t> h_synd, h_conv, h_bpc, h_out;
+  std::vector<double> h_post;
   int D = 0, K = 0, M = 0, m = 0, n1 = 0, n2 = 0, rounds = 0, reps = 0;
   long long max_batch = 0;
   DevBuf mp, mr, k53, a_rp, a_ci, f_rp, f_ci;  // mechanism rows, thresholds, [Hs; L1], [h2; L2]
@@ -215,6 +222,29 @@ void stack_csr(const qldpc_graph* A, const qldpc_graph* B, std::vector<int32_t>&
       rp.push_back((int32_t)ci.size());
     }
   }
+}
+
+// the final layer's OSD through a host stage: D2H of the layer's syndromes, posteriors, BP
+// corrections and convergence flags, qldpc_osd_decode_batch, H2D of the osdw corrections
+int circ_host_osd(qldpc_circ* c, long long B, hipStream_t st) {
+  const size_t m = (size_t)c->m, n2 = (size_t)c->n2;
+  c->h_synd.resize((size_t)B * m);
+  c->h_post.resize((size_t)B * n2);
+  c->h_bpc.resize((size_t)B * n2);
+  c->h_conv.resize((size_t)B);
+  c->h_out.resize((size_t)B * n2);
+  QLDPC_HIP(hipMemcpyAsync(c->h_synd.data(), c->synd2.p, (size_t)B * m, hipMemcpyDeviceToHost, st));
+  QLDPC_HIP(hipMemcpyAsync(c->h_post.data(), c->post2.p, (size_t)B * n2 * 8, hipMemcpyDeviceToHost, st));
+  QLDPC_HIP(hipMemcpyAsync(c->h_bpc.data(), c->bpcorr2.p, (size_t)B * n2, hipMemcpyDeviceToHost, st));
+  QLDPC_HIP(hipMemcpyAsync(c->h_conv.data(), c->conv.p, (size_t)B, hipMemcpyDeviceToHost, st));
+  QLDPC_HIP(hipStreamSynchronize(st));
+  const int rc = qldpc_osd_decode_batch(c->osd_host, c->h_synd.data(), c->h_post.data(), c->h_conv.data(),
+                                        c->h_bpc.data(), nullptr, c->h_out.data(), B, 0);
+  if (rc) return rc;
+  QLDPC_HIP(hipMemcpyAsync(c->corr2.p, c->h_out.data(), (size_t)B * n2, hipMemcpyHostToDevice, st));
+  // the host buffer is reused by the next batch: wait for the copy to land
+  QLDPC_HIP(hipStreamSynchronize(st));
+  return 0;
 }
 
 void circ_release(qldpc_circ* c) {
@@ -325,15 +355,26 @@ int qldpc_circ_set_final_osd(qldpc_circ* c, qldpc_osd_gpu* osd_gpu, const qldpc_
       return rc;
   }
   // a host stage runs on the GPU too (its method, order, rank and soft weights): the launch never
-  // leaves the device
+  // leaves the device.  Past the GPU kernel's envelope it stays a host stage (one D2H / H2D round
+  // trip per batch of the final layer).
   qldpc_osd_gpu* own = nullptr;
+  const qldpc_osd* keep_host = nullptr;
   if (osd_host) {
-    const int rc = osd_gpu_from_host(c->dec2->g, osd_host, &own);
-    if (rc) return rc;
+    // (QLDPC_CIRC_HOST_OSD=1 keeps any host stage on the host: the test hook of that branch, whose
+    // natural trigger, n > 8192 mechanisms in h2, is too large a circuit for a unit test)
+    const char* ho = std::getenv("QLDPC_CIRC_HOST_OSD");
+    const int rc = (ho && std::atoi(ho) == 1) ? QLDPC_ENOTSUP : osd_gpu_from_host(c->dec2->g, osd_host, &own);
+    if (rc == QLDPC_ENOTSUP) {
+      own = nullptr;
+      keep_host = osd_host;
+    } else if (rc) {
+      return rc;
+    }
   }
   if (c->osd_owned) qldpc_osd_gpu_destroy(c->osd_owned);
   c->osd_owned = own;
   c->osd_gpu = osd_gpu ? osd_gpu : own;
+  c->osd_host = keep_host;
   return 0;
 }
 
@@ -443,6 +484,11 @@ int qldpc_circ_launch(qldpc_circ* c, uint64_t seed, uint64_t shot_begin, int64_t
         rc = qldpc_osd_gpu_decode(c->osd_gpu, synd2, static_cast<const double*>(c->post2.p),
                                   static_cast<const uint8_t*>(c->conv.p), static_cast<const uint8_t*>(c->bpcorr2.p),
                                   nullptr, corr2, B, stream);
+    } else if (c->osd_host) {  // host OSD stage: soft BP on the device, OSD on the host, corr2 back
+      rc = qldpc_bp_decode_batch_soft(c->dec2, synd2, static_cast<uint8_t*>(c->bpcorr2.p),
+                                      static_cast<int32_t*>(c->iters.p), static_cast<uint8_t*>(c->conv.p),
+                                      static_cast<double*>(c->post2.p), B, stream);
+      if (!rc) rc = circ_host_osd(c, B, st);
     } else {
       rc = qldpc_bp_decode_batch(c->dec2, synd2, corr2, static_cast<int32_t*>(c->iters.p),
                                  static_cast<uint8_t*>(c->conv.p), B, stream);

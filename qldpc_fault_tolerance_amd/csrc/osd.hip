@@ -34,6 +34,12 @@
 
 #include "runtime.h"
 
+// measured-and-not-kept elimination variants (panel modes PNL 1-5, two rows per thread, the column
+// window, two syndromes per workgroup): out of the product build unless -DQLDPC_EXPERIMENTAL=1
+#ifndef QLDPC_EXPERIMENTAL
+#define QLDPC_EXPERIMENTAL 0
+#endif
+
 
 using qldpc_rt::set_err;
 
@@ -2676,15 +2682,22 @@ constexpr int kOsdWR[] = {2, 4, 8, 12, 16, 20, 25};
 // the pivot loop only): two half-size syndromes per CU cost more than one full-size
 // (profiles/r05/osd_notkept/rpt2_*, lean_rpt2_*)
 inline int osd_rpt(int wr, int pnl) {
+#if QLDPC_EXPERIMENTAL
   const char* e = std::getenv("QLDPC_OSD_RPT");
   return ((pnl == 3 || pnl == 0) && wr >= 20 && e && std::atoi(e) == 2) ? 2 : 1;
+#else
+  (void)wr;
+  (void)pnl;
+  return 1;  // (two rows per thread: experimental builds only)
+#endif
 }
 inline int osd_rr_threads(int wr, int pnl = 0) { return wr <= 16 ? 1024 : 768 / osd_rpt(wr, pnl); }
 using OsdKern = void (*)(OsdGpuArgs);
 template <int WR, int PNL>
 OsdKern osd_rr_wide(int rpt) {
-  if constexpr (PNL == 3 || PNL == 0)  // two rows per thread, 384 threads, two syndromes per CU
+  if constexpr ((PNL == 3 || PNL == 0) && QLDPC_EXPERIMENTAL)  // two rows per thread, 384 threads, two syndromes per CU
     if (rpt == 2) return &osd_gpu_kernel<384, WR, 2, PNL>;
+  (void)rpt;
   return &osd_gpu_kernel<768, WR, 1, PNL>;
 }
 template <int PNL>
@@ -2700,9 +2713,15 @@ OsdKern osd_rr_kernel_t(int wr) {
     default: return nullptr;
   }
 }
+// (the panel / blocked / lagged / forward-elimination modes PNL 1-5 were measured and not kept
+// (DESIGN.md §4): compiled into experimental builds only, -DQLDPC_EXPERIMENTAL=1)
 OsdKern osd_rr_kernel(int wr, int pnl) {
+#if QLDPC_EXPERIMENTAL
   return pnl == 5 ? osd_rr_kernel_t<5>(wr) : pnl == 4 ? osd_rr_kernel_t<4>(wr) : pnl == 3 ? osd_rr_kernel_t<3>(wr) : pnl == 2 ? osd_rr_kernel_t<2>(wr) : pnl ? osd_rr_kernel_t<1>(wr)
                                                                                    : osd_rr_kernel_t<0>(wr);
+#else
+  return pnl ? nullptr : osd_rr_kernel_t<0>(wr);
+#endif
 }
 // column-window kernels (register rows, m <= 768, no panel modes): the first WR row words only and
 // a VGPR budget of 6 waves per SIMD, i.e. two 768-thread workgroups per CU
@@ -2719,8 +2738,13 @@ OsdKern osd_win_kernel_t(int wr) {
   }
 }
 OsdKern osd_win_kernel(int wr) {
+#if QLDPC_EXPERIMENTAL  // (the column window: measured and not kept, experimental builds only)
   const char* e = std::getenv("QLDPC_OSD_WPE");
   return (e && std::atoi(e) == 3) ? osd_win_kernel_t<3>(wr) : osd_win_kernel_t<6>(wr);
+#else
+  (void)wr;
+  return nullptr;
+#endif
 }
 OsdKern osd_rr2_kernel_of(int wr) {
 #if QLDPC_EXPERIMENTAL
@@ -2818,7 +2842,7 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
   // m <= 1024 and n <= 2048; QLDPC_OSD_RR=0 keeps the LDS / HBM image
   const char* rr_env = std::getenv("QLDPC_OSD_RR");
   const char* pnl_env = std::getenv("QLDPC_OSD_PNL");
-  const int want_pnl = pnl_env ? std::atoi(pnl_env) : 0;
+  const int want_pnl = (QLDPC_EXPERIMENTAL && pnl_env) ? std::atoi(pnl_env) : 0;  // (PNL 1-5: experimental builds)
   if (!rr_env || std::atoi(rr_env) != 0)
     for (int wr : kOsdWR)
       if (wr >= G->W) {
@@ -2860,7 +2884,7 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
   }
   // two syndromes per workgroup (osd_rr2_kernel, the 768-thread register-row kernels): a second LDS
   // area and HBM slice per workgroup; QLDPC_OSD_NSY=1 keeps one
-  const char* nsy_env = std::getenv("QLDPC_OSD_NSY");
+  const char* nsy_env = QLDPC_EXPERIMENTAL ? std::getenv("QLDPC_OSD_NSY") : nullptr;  // (osd_rr2_kernel: experimental builds)
   if (G->wr >= 20 && !G->pnl && !QLDPC_OSD_1B && G->host.uniform && (nsy_env ? std::atoi(nsy_env) : 1) == 2 && osd_rr2_kernel_of(G->wr)) {
     G->nsy = 2;
     G->syn_lds = (int)((G->lds + 15) & ~(size_t)15);
@@ -2876,7 +2900,7 @@ int qldpc_rt::osd_gpu_from_host(const qldpc_graph* g, const qldpc_osd* O, qldpc_
   // the END of the reliability order (hgp_34_n1600 at p = 0.04: last pivot at position 1419-1538
   // of 1600, tools/dev/osd_last_pivot.py), so nearly every syndrome overruns a 14-word window and
   // pays twice: 491 k BP+OSD shots/s vs 615 k at full width (profiles/r05/osd_notkept/window_*).
-  const char* win_env = std::getenv("QLDPC_OSD_WIN");
+  const char* win_env = QLDPC_EXPERIMENTAL ? std::getenv("QLDPC_OSD_WIN") : nullptr;  // (experimental builds)
   const int win_force = win_env ? std::atoi(win_env) : 0;
   if (G->wr && !G->pnl && G->nsy == 1 && m <= 768 && win_force > 0 && QLDPC_OSD_LEAN && !kOsdM4R && !QLDPC_OSD_1B) {
     const long long need = (long long)rank + G->nh;

@@ -109,6 +109,10 @@ SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int 
   }
   // fp64 m2-in-slot family (rows of 3 chunks + a tail slot, <= 256 threads, 3 workgroups per CU)
   if (m2s) {
+    // the fp64 space-time graphs: rows of 4 chunks + a tail slot, dword-scaled addresses, 1024
+    // threads (engine id 111313, round 6)
+    if (m2s == 1 && engine == 3 && precision == 64 && dmax == 4 && ea_shift == 2 && nch == 4 && tail && tb > 512)
+      return get_rvariant_f64_m2st(vpl, d3k, d2k);
     // rows of 8 (4 chunks, no tail array), column degree 5, 256 threads: engine id 10103
     if (m2s == 1 && engine == 3 && precision == 64 && dmax == 5 && ea_shift == 0 && nch == 4 && !tail && tb == 256)
       return pk ? get_rvariant_f64_m2s8pk(vpl, d3k) : get_rvariant_f64_m2s8(vpl, d3k);
@@ -398,11 +402,14 @@ static int upload_llr(qldpc_bp* bp) {
 static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
                              const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1,
                              const std::vector<int>& lab = {}, int tail = 0, int m2s = 0, int d3k = 0,
-                             int dummy0 = -1, int* ndummy = nullptr, int anneal = 0, int anneal_iters = -1) {
+                             int dummy0 = -1, int* ndummy = nullptr, int anneal = 0, int anneal_iters = -1,
+                             int tail_base = -1, int d2k = 0) {
   const int nv = 16 / tsize;  // messages per 16-byte chunk
   const int rw = nch * nv;
   const int rwt = rw + (tail ? 1 : 0);  // tail layouts: logical slot rw = the row's tail slot
-  const int tail0 = (1 + g->m * nch) * nv;  // first tail slot (right after V, bp_reg.h r_layout)
+  // first tail slot: right after V (bp_reg.h r_layout), i.e. after the private dummy slots when the
+  // layout has them (tail_base, the space-time m2s family)
+  const int tail0 = tail_base >= 0 ? tail_base : (1 + g->m * nch) * nv;
   const int swz_mask = (nch == 2) ? 1 : (nch == 4) ? 3 : 0;
   const int swz_shift = (nch == 2) ? 3 : 2;
   auto L = [&](int i) { return lab.empty() ? i : lab[i]; };
@@ -615,16 +622,16 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
         out[((size_t)k * DM + d) * TB + t] = (uint32_t)(L(i) + 1) | ((uint32_t)slot << 16);
       }
     }
-  // m2s rows of 8: the missing edges of real variables (slots k >= d3k hold DM edge slots, k < d3k
-  // three) get private V slots from dummy0 on, lane-consecutive per (k, d) (conflict-free reads and
-  // stores), and the dummy CS entry 0
+  // m2s rows of 8 / space-time rows: the missing edges of real variables (slots k >= d3k hold DM
+  // edge slots, d2k <= k < d3k three, k < d2k two) get private V slots from dummy0 on,
+  // lane-consecutive per (k, d) (conflict-free reads and stores), and the dummy CS entry 0
   int nd = 0;
   if (dummy0 >= 0)
     for (int k = 0; k < VPL; ++k)
       for (int d = 0; d < DM; ++d)
         for (int t = 0; t < TB; ++t) {
           const int j = slot_var[(size_t)k * TB + t];
-          if (j >= 0 && d >= (int)g->col_rows[j].size() && d < (k < d3k ? 3 : DM))
+          if (j >= 0 && d >= (int)g->col_rows[j].size() && d < (k < d2k ? 2 : k < d3k ? 3 : DM))
             out[((size_t)k * DM + d) * TB + t] = (uint32_t)(dummy0 + nd++) << 16;
         }
   if (ndummy) *ndummy = nd;
@@ -920,6 +927,25 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
                           double ms_scaling_factor, int32_t precision, int32_t vars_per_thread,
                           int32_t min_col_slots, int forced_engine, qldpc_bp** out);
 
+// The one-iteration first-min step kernel of a max_iter = 1 min-sum decoder (decode_batch routes
+// its decodes there), built when the decoder is created and whenever its priors change, so that
+// decode_batch only launches kernels (no synchronous uploads or occupancy queries between
+// stream-ordered launches).  Graphs past the kernel's LDS envelope keep the engine.
+static void bp1_prepare(qldpc_bp* bp) {
+  if (bp->bp1) {
+    qldpc_firstmin_destroy(bp->bp1);
+    bp->bp1 = nullptr;
+  }
+  bp->bp1_off = !(bp->max_iter == 1 && bp->method == 1) || env_int("QLDPC_BP1", 1) == 0;
+  if (bp->bp1_off) return;
+  const std::string keep = qldpc_rt::g_err;  // an ENOTSUP here is not the caller's error
+  if (qldpc_firstmin_create(bp->g, bp->probs.data(), 0, bp->alpha, bp->precision, &bp->bp1) != 0) {
+    bp->bp1 = nullptr;
+    bp->bp1_off = true;
+    qldpc_rt::g_err = keep;
+  }
+}
+
 int qldpc_bp_create(qldpc_graph* g, const double* channel_probs, int32_t max_iter, int32_t bp_method,
                     double ms_scaling_factor, int32_t precision, int32_t vars_per_thread, int32_t min_col_slots,
                     qldpc_bp** out) {
@@ -996,6 +1022,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb6, hbm_kernel(precision), bp->TB, 0) != hipSuccess) nb6 = 1;
     bp->blocks_per_cu = std::max(1, nb6);
     if ((rc6 = device_cus(g->device, bp->cus))) return fail(rc6);
+    bp1_prepare(bp);
     *out = bp;
     return 0;
   };
@@ -1027,7 +1054,11 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     if (bp->engine == 4 && g->max_row > 8) bp->engine = 3;  // engine 4 rows are 8 slots wide
     bp->nch = bp->engine == 4 ? 8 * tsize / 16 : (std::max(1, g->max_row) * tsize + 15) / 16;
     const int vslots = (1 + g->m * bp->nch) * (16 / tsize);
-    if (vslots >= 0xFFFF) return fail(set_err(QLDPC_ENOTSUP, "V image exceeds 65535 message slots"));
+    if (vslots >= 0xFFFF) {  // no LDS image addresses this many slots: HBM-resident messages (engine 6)
+      if (env_int("QLDPC_HBM_FALLBACK", 1) == 0)
+        return fail(set_err(QLDPC_ENOTSUP, "V image exceeds 65535 message slots (QLDPC_HBM_FALLBACK=0)"));
+      return setup_hbm();
+    }
     // degree-5/6 variables hold 2.5x the registers of degree-4 ones: fewer per thread
     const int pref = DM == 4 ? kPrefVplR : 4, vmax = DM == 4 ? kMaxVplR : 5;
     // images of 64-256 KiB (space-time graphs): engine 3 with dword-scaled addresses (fp32, 4 slots)
@@ -1106,6 +1137,55 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
           bp->vslots_m2v = vm;
           bp->m2v_vlast = ecl * 256;
           bp->m2v_nl = NL;
+        }
+      }
+    }
+    // fp64 space-time graphs on the tail layout (rows of 8 / 9 as 4 chunks + a tail slot, 1024 threads,
+    // one decode per CU): the one-word check state too (round 6, kern_r_f64_m2st.hip, engine id
+    // 111313).  The two-word tail family re-reads each edge's own previous v2c from LDS (its 128-VGPR
+    // budget had no room for it) and gathers 16-byte check states: 24 B of variable-phase reads per
+    // edge.  Here the own v2c lives in VGPRs (118 with the uniform prior in SGPRs, no scratch) and an
+    // edge reads the 8-byte CS and its own slot: 16 B.  Real variables never touch a shared dummy:
+    // the measurement variables in 3-edge slots and the degree-3 ones in 4-edge slots get private
+    // dummy V slots (config 5: 1,348, 10.8 KB), placed before the tail array.  Uniform priors only.
+    if (bp->engine == 3 && precision == 64 && DM == 4 && bp->tail && !bp->fb && !bp->m2s && bp->nch == 4 &&
+        env_int("QLDPC_M2ST", 1) != 0 && env_int("QLDPC_DEGSORT", 1) != 0 && env_int("QLDPC_D2K", 1) != 0) {
+      int tb = 0, vpl = 0;
+      bool uni = true;
+      for (int j = 1; j < g->n && QLDPC_M2S_UNIL; ++j) uni = uni && channel_probs[j] == channel_probs[0];
+      if (uni && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb > 512) {
+        // the slot map the build below makes (sort2: degree <= 2, 3, 4 in column order), its D2K / D3K
+        // and the private dummies of build_slot_edges
+        std::vector<int> deg;
+        deg.reserve((size_t)vpl * tb);
+        for (int c = 0; c < 3; ++c)
+          for (int j = 0; j < g->n; ++j) {
+            const int d = (int)g->col_rows[j].size();
+            if ((d <= 2 ? 0 : d <= 3 ? 1 : 2) == c) deg.push_back(d);
+          }
+        deg.resize((size_t)vpl * tb, -1);
+        auto whole = [&](int lim) {  // leading variable slots whose variables all have degree <= lim
+          int kk = 0;
+          for (; kk < vpl; ++kk) {
+            bool ok = true;
+            for (int t = 0; t < tb && ok; ++t) ok = deg[(size_t)kk * tb + t] <= lim;
+            if (!ok) break;
+          }
+          return kk;
+        };
+        const int d2 = whole(2), d3 = whole(3);
+        int nd = 0, dmax = 0;
+        for (int k = 0; k < vpl; ++k)
+          for (int t = 0; t < tb; ++t) {
+            const int d = deg[(size_t)k * tb + t];
+            dmax = std::max(dmax, d);
+            if (d >= 0) nd += (k < d2 ? 2 : k < d3 ? 3 : DM) - d;
+          }
+        const int vs = (1 + g->m * 4) * 2 + nd;
+        if (dmax <= DM && d2 >= 1 && vs < 0x3FFFF && get_rvariant_f64_m2st(vpl, d3, d2).dec_k &&
+            r_fits(3, vs, g->m, 8, 2, 1, 1)) {
+          bp->m2s = 1;
+          bp->vslots_dummy = nd;
         }
       }
     }
@@ -1199,7 +1279,8 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     const bool sort3 = bp->engine == 3 && DM >= 4 && env_int("QLDPC_DEGSORT", 1) != 0;
     // byte-F kernels also keep degree <= 2 variables (the space-time measurement columns) in
     // compile-time 2-edge slots: those go first
-    const bool sort2 = sort3 && (bp->fb || (bp->tail && !bp->m2s && precision == 64)) && env_int("QLDPC_D2K", 1) != 0;
+    const bool sort2 = sort3 && (bp->fb || (bp->tail && precision == 64 && (!bp->m2s || bp->nch == 4))) &&
+                       env_int("QLDPC_D2K", 1) != 0;
     auto cls = [&](int j) {
       const int d = (int)g->col_rows[j].size();
       return sort2 ? (d <= 2 ? 0 : d <= 3 ? 1 : 2) : (d <= 3 ? 0 : 1);
@@ -1312,7 +1393,10 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
                      bp->vslots_dummy ? (1 + g->m * bp->nch) * (16 / tsize) : -1, &ndummy,
                      (bp->engine == 3 && precision == 64 && bp->m2s != 3)
                          ? ((bp->m2s || bp->tail) ? 1 : env_int("QLDPC_ANNEAL_2W", 1) != 0 ? 2 : 0)
-                         : 0);
+                         : 0,
+                     -1,
+                     (bp->tail && bp->vslots_dummy) ? (int)(r_layout(3, vslots2, g->m, tsize, 1, bp->m2s).t - r_layout(3, vslots2, g->m, tsize, 1, bp->m2s).v) / tsize : -1,
+                     bp->d2k);
     if (ndummy != bp->vslots_dummy) return fail(set_err(QLDPC_EINVAL, "m2s private dummy slot count mismatch"));
     if (bp->engine == 3 && precision == 64 && bp->m2s != 3 && bp->ea_shift == 0)
       lds_model_var_phase(vchk, bp->TB, bp->VPL, DM, bp->d3k,
@@ -1425,6 +1509,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, bp->TB, bp->lds_bytes) != hipSuccess) nb = 1;
   bp->blocks_per_cu = std::max(1, nb);
   if ((rc = device_cus(g->device, bp->cus))) return fail(rc);
+  bp1_prepare(bp);
   *out = bp;
   return 0;
 }
@@ -1447,12 +1532,10 @@ int qldpc_bp_set_channel_probs(qldpc_bp* bp, const double* channel_probs) {
         return set_err(QLDPC_ENOTSUP, "this decoder's kernels hold one uniform prior: create a new decoder for "
                                       "non-uniform channel_probs");
   bp->probs.assign(channel_probs, channel_probs + bp->g->n);
-  if (bp->bp1) {  // rebuilt from the new priors on the next one-iteration decode
-    qldpc_firstmin_destroy(bp->bp1);
-    bp->bp1 = nullptr;
-  }
-  bp->bp1_off = false;
-  return upload_llr(bp);
+  const int rc = upload_llr(bp);
+  if (rc) return rc;
+  bp1_prepare(bp);  // rebuilt from the new priors
+  return 0;
 }
 
 int qldpc_bp_degree3_slots(const qldpc_bp* bp, int32_t* d3k) {
@@ -1517,7 +1600,8 @@ int qldpc_bp_kernel_id(const qldpc_bp* bp, int32_t* kernel_id, int32_t* row_chun
   int id = bp->engine;
   if (bp->engine == 3) {
     if (bp->m2s)
-      id = bp->m2s == 2 ? 31103 : bp->m2s == 3 ? 40103 : bp->tail ? 11103 : bp->m2s_pk ? 10203 : 10103;
+      id = bp->m2s == 2 ? 31103 : bp->m2s == 3 ? 40103 : (bp->tail && bp->nch == 4) ? 11313 + 100000 * std::min(bp->d2k, 1)
+           : bp->tail ? 11103 : bp->m2s_pk ? 10203 : 10103;
     else if (bp->fb)
       id = 21013 + ((bp->d3k >= 8 && bp->d2k > 0) ? 100000 * std::min(bp->d2k, 4) : 0);  // + D2K digit
     else if (bp->tail)
@@ -1618,15 +1702,8 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
   // max_iter = 1 min-sum (the circuit loop's h1 rounds: max_iter = int(18 / 10)): a one-iteration BP
   // from fresh state is the first-min step kernel (per-edge magnitudes fixed by the priors, bit-exact
   // with every engine); QLDPC_BP1=0 keeps the engine
-  if (!d_post && bp->max_iter == 1 && bp->method == 1 && !bp->bp1_off) {
-    if (!bp->bp1) {
-      if (env_int("QLDPC_BP1", 1) == 0 || qldpc_firstmin_create(bp->g, bp->probs.data(), 0, bp->alpha, bp->precision, &bp->bp1) != 0) {
-        bp->bp1 = nullptr;
-        bp->bp1_off = true;  // (graph past the kernel's LDS envelope: the engine decodes)
-      }
-    }
-    if (bp->bp1) return qldpc_rt::bp1_decode(bp->bp1, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
-  }
+  // (built with the decoder and on every qldpc_bp_set_channel_probs, bp1_prepare: no uploads here)
+  if (!d_post && bp->bp1) return qldpc_rt::bp1_decode(bp->bp1, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
   if (bp->engine == 5) return ps_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
   if (bp->engine == 6) return hbm_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
   const long long cap = (long long)bp->blocks_per_cu * bp->cus;
@@ -1701,7 +1778,9 @@ int qldpc_mc_create(qldpc_bp* dec_x, const qldpc_graph* logical_x, qldpc_bp* dec
   if (!out || (!dec_x && !dec_z)) return set_err(QLDPC_EINVAL, "need at least one sector decoder");
   qldpc_bp* d0 = dec_x ? dec_x : dec_z;
   const bool staged = (dec_x && dec_x->engine >= 5) || (dec_z && dec_z->engine >= 5) ||
-                      (dec_x && dec_x->tail && !dec_x->m2s) || (dec_z && dec_z->tail && !dec_z->m2s) ||
+                      // (the space-time tail families, two-word or one-word: decode_batch kernels only)
+                      (dec_x && dec_x->tail && (!dec_x->m2s || dec_x->nch == 4)) ||
+                      (dec_z && dec_z->tail && (!dec_z->m2s || dec_z->nch == 4)) ||
                       // the fused kernel runs one layout family for both sectors
                       (dec_x && dec_z &&
                        (dec_x->m2s != dec_z->m2s || dec_x->tail != dec_z->tail || dec_x->fb != dec_z->fb ||

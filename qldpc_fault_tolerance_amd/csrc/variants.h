@@ -57,6 +57,7 @@ SVariant get_rvariant_f64_w4(int vpl, int d3k);
 SVariant get_rvariant_f64_st(int vpl, int d3k, int d2k = 0);  // kern_r_f64_st*.hip: tail layout, 1024 threads (engine id 1013)
 SVariant get_rvariant_f64_st_hi(int vpl, int d3k);
 SVariant get_rvariant_f32_st(int vpl, int d3k);  // kern_r_f32_st.hip: tail layout in float (engine id 1013)
+SVariant get_rvariant_f64_m2st(int vpl, int d3k, int d2k);  // kern_r_f64_m2st.hip: m2s on the fp64 space-time tail layout, 1024 threads (engine id 111313)
 SVariant get_rvariant_f64_m2s(int vpl, int d3k);  // kern_r_f64_m2s.hip: m2 in the argmin slot, rows of 3 chunks + tail (engine id 11103)
 SVariant get_rvariant_f64_m2s8(int vpl, int d3k);  // kern_r_f64_m2s8.hip: m2s, rows of 4 chunks (8 edges), column degree 5 (engine id 10103)
 SVariant get_rvariant_f64_m2s8pk(int vpl, int d3k);  // the same with packed absolute edge addresses, 4 per CU (engine id 10203)

@@ -15,6 +15,7 @@ the native OSD stage (csrc/osd.hip) on the syndromes BP did not converge on.
 """
 from __future__ import annotations
 
+import math
 from abc import ABC, abstractmethod
 
 import numpy as np
@@ -63,11 +64,15 @@ class FirstMinBPDecoder:
     """Repeated one-iteration BP while the syndrome weight does not grow (``src/Decoders.py:49-74``).
 
     ``minimum_sum`` (every reference call site) runs the whole loop on the GPU in one kernel
-    (:class:`~.engine.DeviceFirstMin`, ``qldpc_firstmin_*``); ``product_sum`` steps the engine's
-    one-iteration BP from the host (one launch per first-min step for all active syndromes)."""
+    (:class:`~.engine.DeviceFirstMin`, ``qldpc_firstmin_*``); ``product_sum``, and graphs past that
+    kernel's envelope (2 (m + n) > 64 KiB: ``QLDPC_ENOTSUP``), step the engine's one-iteration BP
+    from the host (one launch per first-min step for all active syndromes).  ``max_iter`` is
+    compared raw, as ``iter_counter < self.max_iter`` (``:66``): a float N/10 = 22.5 allows 23
+    accepted steps, so the device loop takes ``ceil(max_iter)``."""
 
     def __init__(self, h, channel_probs, max_iter, bp_method, ms_scaling_factor, precision: int = 64,
                  device: int | None = None):
+        from . import _native
         from .engine import DeviceFirstMin, bp_method_code
 
         self.h = np.asarray(h)
@@ -78,9 +83,14 @@ class FirstMinBPDecoder:
         if bp_method_code(bp_method) == 1:
             n = self._H.n
             probs = np.asarray(channel_probs, dtype=np.float64)
-            self._fm = DeviceFirstMin(self._H, np.full(n, float(probs)) if probs.ndim == 0 else probs,
-                                      int(max_iter), ms_scaling_factor, precision=precision, device=device)
-        else:
+            try:
+                self._fm = DeviceFirstMin(self._H, np.full(n, float(probs)) if probs.ndim == 0 else probs,
+                                          max(0, math.ceil(max_iter)), ms_scaling_factor, precision=precision,
+                                          device=device)
+            except _native.QldpcError as e:
+                if e.rc != _native.ENOTSUP:
+                    raise
+        if self._fm is None:
             self._bp = BPDecoder(h, channel_probs, 1, bp_method, ms_scaling_factor, precision=precision, device=device)
         self.steps_batch = None
         self._st_bp = None
@@ -95,7 +105,7 @@ class FirstMinBPDecoder:
 
             n = self._H.n
             p = np.full(n, float(self._probs)) if self._probs.ndim == 0 else self._probs
-            self._st_bp = DeviceBP(self._H, p, max_iter=1, graph=self._fm.graph)
+            self._st_bp = DeviceBP(self._H, p, max_iter=1, graph=self._fm.graph if self._fm is not None else None)
         return self._st_bp
 
     def decode(self, synd):

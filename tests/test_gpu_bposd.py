@@ -151,6 +151,18 @@ _OSD_MODES = {"default": {}, "lds": {"QLDPC_OSD_RR": "0"}, "hbm": {"QLDPC_OSD_RR
               "win": {"QLDPC_OSD_WIN": "1"}, "win8": {"QLDPC_OSD_WIN": "8"},
               "winredo": {"QLDPC_OSD_WIN": "1", "QLDPC_OSD_WIN_REDO": "1"},
               "wpe3": {"QLDPC_OSD_WIN": "1", "QLDPC_OSD_WPE": "3"}}
+# the product modes: register rows, and the LDS image / HBM slice that serve graphs past them (the
+# switches only force them); the rest are measured-and-not-kept variants compiled into experimental
+# builds only (-DQLDPC_EXPERIMENTAL=1, tools/build_variant.py): skipped in the product build
+
+
+def _set_osd_mode(monkeypatch, mode):
+    from qldpc_fault_tolerance_amd import _native
+
+    if mode not in ("default", "lds", "hbm") and not _native.experimental_families():
+        pytest.skip(f"OSD mode {mode!r}: experimental builds only")
+    for k, v in _OSD_MODES[mode].items():
+        monkeypatch.setenv(k, v)
 
 
 @pytest.mark.parametrize("name,t0,method,order,mode", [
@@ -182,8 +194,7 @@ def test_gpu_osd_matches_host_osd(gpu, monkeypatch, name, t0, method, order, mod
     register rows by default; the LDS image and the HBM slice serve wider graphs)."""
     from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceOSD, HostOSD
 
-    for k, v in _OSD_MODES[mode].items():
-        monkeypatch.setenv(k, v)
+    _set_osd_mode(monkeypatch, mode)
 
     code = codes.get_code(name)
     H = code.hz if t0 == 0 else codes.space_time_csr(code.hz, t0).to_dense().astype(np.uint8)
@@ -227,8 +238,7 @@ def test_gpu_osd_nonuniform_priors_matches_oracle(gpu, oracle, monkeypatch, name
     circuit hypergraphs with their DEM priors (tests/golden/reference_circuit.npz)."""
     from qldpc_fault_tolerance_amd.engine import DeviceBP, DeviceOSD, HostOSD
 
-    for k, v in _OSD_MODES[mode].items():
-        monkeypatch.setenv(k, v)
+    _set_osd_mode(monkeypatch, mode)
     if name.startswith("circuit_"):
         import os
 

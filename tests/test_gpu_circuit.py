@@ -185,3 +185,38 @@ def test_demo_wer_against_printed(gpu):
     assert abs(ler - 0.00794) < 5 * sd, ler
     wer, _ = sim.WordErrorRate(10000)
     assert 0 < wer < 1e-3 and math.isfinite(wer)
+
+
+def test_host_osd_stage_past_gpu_envelope(gpu, monkeypatch):
+    """A host OSD stage that stays a host stage (``qldpc_circ_set_final_osd`` used to fail
+    with ENOTSUP past the GPU OSD kernel's envelope, n > 8192 mechanisms in h2; too large a circuit for
+    a unit test, so QLDPC_CIRC_HOST_OSD=1 forces the branch): decoder2 with ``use_gpu_osd=False``, the
+    fused launch decodes the final layer through the host stage (one D2H / H2D round trip per batch).
+    Same failures, sample for sample, as the reference's per-sample plugin path on the same draws."""
+    from qldpc_fault_tolerance_amd.decoders import ST_BPOSD_Decoder_Circuit
+
+    monkeypatch.setenv("QLDPC_CIRC_HOST_OSD", "1")
+    sim, mi = _sim(3e-3, ALL_NOISE, osd=True, max_iter_ratio=10)
+    g = sim.circuit_graph
+    sim.decoder2_z = ST_BPOSD_Decoder_Circuit(g["h2"], g["channel_ps2"], mi, "minimum_sum", 0.625, "osd_e", 10,
+                                              use_gpu_osd=False)
+    d2 = sim.decoder2_z
+    assert d2.gpu_osd is None
+    assert sim._engine_parts() is not None
+    S = 240
+    res = sim._device().run(sim.seed, 0, S, per_shot=True)
+
+    class Foreign:  # the reference's plugin contract: only .decode
+        def __init__(self, d):
+            self.d = d
+
+        def decode(self, synd):
+            return self.d.decode(synd)
+
+    sim._shot_offset = 0
+    sim.decoder1_z, sim.decoder2_z = Foreign(sim.decoder1_z), Foreign(d2)
+    assert sim._engine_parts() is None
+    samples = sim.detector_sampler.sample(shots=S, append_observables=True)
+    per = np.asarray(sim._decoding_samples(samples), dtype=np.uint8)
+    assert np.array_equal(samples, res.detobs)
+    assert np.array_equal(per, res.fail) and 0 < int(per.sum()) < S

@@ -81,26 +81,30 @@ def test_config_harness_replayed_on_gpu(gpu, name):
         assert np.array_equal(fx | fz, g[f"{name}_run_p{pc}_Total_fail"]), pc
 
 
-def test_config5_space_time_replayed_on_gpu_fp64(gpu):
+@pytest.mark.parametrize("family", ["one_word", "two_word", "hbm"])
+def test_config5_space_time_replayed_on_gpu_fp64(gpu, monkeypatch, family):
     """Config 5 in ldpc's float64 arithmetic: the 1764 x 5439 space-time decoder at the drop-in's default
-    precision — engine 3's tail layout (rows of 9 = 4 fp64 chunks + a tail slot, a 162.7 KB image),
-    and the same histories forced onto the HBM-resident message engine (engine 6)."""
+    precision — engine 3's tail layout (rows of 9 = 4 fp64 chunks + a tail slot, 1024 threads x 6
+    variables, the first slot's 1024 degree-2 measurement variables on 2 edge slots) in the one-word
+    "m2 in slot" family (round 6, engine id 111313, the default) and the two-word family (engine id
+    101013, QLDPC_M2ST=0), and the same histories forced onto the HBM-resident message engine (engine 6)."""
     from qldpc_fault_tolerance_amd.engine import DeviceBP, DevicePhenl
 
+    if family == "two_word":
+        monkeypatch.setenv("QLDPC_M2ST", "0")
     g = np.load(CONFIGS, allow_pickle=False)
     code = codes.get_code("hgp_34_n1225_q3")
     m, n, p = code.hz.shape[0], code.N, 0.01
     mi = int(n / 10)
     S = g["st1225_fail"].shape[0]
-    for hbm in (False, True):
+    for hbm in ((True,) if family == "hbm" else (False,)):
         st = [DeviceBP(codes.space_time_csr(h, 3), np.hstack([p * np.ones(n), p * np.ones(m)] * 3), max_iter=mi,
                        precision=64, hbm=hbm) for h in (code.hz, code.hx)]
         geo = st[0].geometry()
         assert geo["engine"] == (6 if hbm else 3), geo
         if not hbm:
             assert geo["lds_bytes"] > 64 * 1024 and geo["threads"] == 1024, geo  # the tail-layout family
-            # 6 variables per thread, the first slot's 1024 degree-2 measurement variables on 2 edge slots
-            assert geo["kernel_id"] == 101013, geo
+            assert geo["kernel_id"] == (111313 if family == "one_word" else 101013), geo
         d2 = [DeviceBP(code.csr(k), p * np.ones(n), max_iter=mi, precision=64) for k in ("hz", "hx")]
         ph = DevicePhenl(code, st[0], st[1], d2[0], d2[1], num_rep=3)
         u = uniforms(int(g["st1225_seed0"][0]), S, ph.uniforms_per_sample(3))

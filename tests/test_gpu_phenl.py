@@ -299,3 +299,85 @@ def test_st_fp32_byte_f_family_decode_matches_oracle(gpu, oracle, p):
         assert d1.geometry()["kernel_id"] == kid
         c1, i1, v1 = d1.decode_batch(synd)
         assert np.array_equal(c, c1) and np.array_equal(i, i1) and np.array_equal(v, v1), env
+
+
+@pytest.mark.parametrize("p,alpha", [(0.005, 0.625), (0.06, 0.625), (0.03, 0.0)])
+def test_st_fp64_one_word_family_decode_matches_oracle(gpu, oracle, p, alpha):
+    """The fp64 space-time decoder of config 5 on the one-word "m2 in slot" tail family (round 6,
+    engine id 111313: 1024 threads x 6 variables, own v2c in VGPRs, private dummy slots for the
+    measurement / degree-3 variables in wider slots) against the oracle's float64 restatement (the
+    reference arithmetic) and the two-word tail family (QLDPC_M2ST=0, engine id 101013), on
+    syndromes of i.i.d. errors (p = 0.06: every decode runs to max_iter; alpha 0: ldpc's schedule)."""
+    import os
+
+    from qldpc_fault_tolerance_amd.engine import DeviceBP
+
+    code = codes.get_code("hgp_34_n1225_q3")
+    H = codes.space_time_csr(code.hz, 3)
+    n = H.n
+    pr = np.full(n, p)
+    mi = int(code.N / 10)
+    rng = np.random.default_rng(int(p * 1000) + 17)
+    e = (rng.random((192, n)) < p).astype(np.uint8)
+    synd = H.matvec(e).astype(np.uint8)
+    synd[0] = 0
+    dec = DeviceBP(H, pr, max_iter=mi, ms_scaling_factor=alpha, precision=64)
+    assert dec.geometry()["kernel_id"] == 111313
+    c, i, v = dec.decode_batch(synd)
+    oc, oi, ov = oracle.bp_decode_batch(H, pr, mi, "minimum_sum", alpha, synd, 64)
+    assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64))
+    os.environ["QLDPC_M2ST"] = "0"
+    try:
+        d1 = DeviceBP(H, pr, max_iter=mi, ms_scaling_factor=alpha, precision=64)
+    finally:
+        del os.environ["QLDPC_M2ST"]
+    assert d1.geometry()["kernel_id"] == 101013
+    c1, i1, v1 = d1.decode_batch(synd)
+    assert np.array_equal(c1, c) and np.array_equal(i1, i) and np.array_equal(v1, v)
+
+
+def test_st_fp64_nonuniform_priors_keep_two_word_family(gpu, oracle):
+    """Non-uniform priors (p_synd != p_data) are outside the one-word family (one prior in SGPRs):
+    the two-word tail family decodes them, bit-exact against the oracle."""
+    from qldpc_fault_tolerance_amd.engine import DeviceBP
+
+    code = codes.get_code("hgp_34_n1225_q3")
+    H = codes.space_time_csr(code.hz, 3)
+    pr = np.hstack([0.02 * np.ones(code.N), 0.01 * np.ones(code.hz.shape[0])] * 3)
+    rng = np.random.default_rng(5)
+    synd = H.matvec((rng.random((64, H.n)) < pr).astype(np.uint8)).astype(np.uint8)
+    dec = DeviceBP(H, pr, max_iter=40, precision=64)
+    assert dec.geometry()["kernel_id"] == 101013
+    c, i, v = dec.decode_batch(synd)
+    oc, oi, ov = oracle.bp_decode_batch(H, pr, 40, "minimum_sum", 0.625, synd, 64)
+    assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64))
+
+
+def test_firstmin_past_device_envelope_steps_the_engine(gpu, oracle):
+    """A minimum_sum FirstMinBPDecoder on a graph past the first-min kernel's LDS envelope (2 (m + n)
+    > 64 KiB: QLDPC_ENOTSUP) steps the engine's one-iteration BP from the host instead of raising;
+    corrections equal the reference loop (src/Decoders.py:60-74) over the oracle's one-iteration BP.
+    max_iter = 2.5 (a float, as N / 10 can be) allows 3 accepted steps, as the reference's raw
+    comparison does."""
+    rng = np.random.default_rng(11)
+    m, n = 12000, 24000
+    rows = np.concatenate([rng.choice(m, 3, replace=False) for _ in range(n)])
+    cols = np.repeat(np.arange(n), 3)
+    H = np.zeros((m, n), np.uint8)
+    H[rows, cols] = 1
+    probs = np.full(n, 0.01)
+    fm = decoders.FirstMinBPDecoder(H, probs, 2.5, "minimum_sum", 0.625)
+    assert fm._fm is None and fm._bp is not None
+    e = (rng.random((3, n)) < 0.004).astype(np.uint8)
+    synd = (e.astype(np.int64) @ H.T.astype(np.int64) % 2).astype(np.uint8)
+    out = fm.decode_batch(synd)
+    Hl = H.astype(np.int64)
+    for b in range(synd.shape[0]):
+        corr, cur, k = np.zeros(n, dtype=np.int64), synd[b].astype(np.int64), 0
+        nc = oracle.bp_decode_batch(H, probs, 1, "minimum_sum", 0.625, cur[None].astype(np.uint8), 64)[0][0].astype(np.int64)
+        ns = (Hl @ nc + cur) % 2
+        while ns.sum() <= cur.sum() and k < 2.5:
+            cur, corr, k = ns, (corr + nc) % 2, k + 1
+            nc = oracle.bp_decode_batch(H, probs, 1, "minimum_sum", 0.625, cur[None].astype(np.uint8), 64)[0][0].astype(np.int64)
+            ns = (Hl @ nc + cur) % 2
+        assert np.array_equal(out[b], corr), b
