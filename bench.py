@@ -132,6 +132,12 @@ def parse():
     ap.add_argument("--workload", default="data", choices=("data", "phenl", "bposd", "circuit"),
                     help="data = headline (config 2); phenl = space-time phenomenological (config 5)")
     ap.add_argument("--num-rep", type=int, default=3)
+    ap.add_argument("--dem-d", type=int, default=3,
+                    help="circuit workload: toric distance (3 = the demo's hgp(ring_code(3), ring_code(3)))")
+    ap.add_argument("--circuit-noise", default="cx", choices=("cx", "all"),
+                    help="circuit workload: CX noise only (the demo) or every noise source at p")
+    ap.add_argument("--sampler", default="skip", choices=("skip", "keyed"),
+                    help="circuit workload: DEM sampler (geometric skip, the default, or keyed per sample)")
     ap.add_argument("--dec2", default="bp", choices=("bp", "bposd"),
                     help="phenl final-round decoder: BP, or BP+OSD-E(10) as the notebooks use")
     ap.add_argument("--num-cycles", type=int, default=13)
@@ -768,14 +774,18 @@ def circuit_main(a, torch, dist, world, rank, dev):
     from qldpc_fault_tolerance_amd.decoders import ST_BP_Decoder_Circuit, ST_BPOSD_Decoder_Circuit
     from qldpc_fault_tolerance_amd.simulators import CodeSimulator_Circuit_SpaceTime
 
-    ring = np.zeros((3, 3), np.uint8)
-    for i in range(3):
-        ring[i, i] = ring[i, (i + 1) % 3] = 1
-    code = codes.hgp(ring, ring, name="toric_d3")
+    d = int(a.dem_d)
+    ring = np.zeros((d, d), np.uint8)
+    for i in range(d):
+        ring[i, i] = ring[i, (i + 1) % d] = 1
+    code = codes.hgp(ring, ring, name=f"toric_d{d}")
     p = a.p if a.p != DEFAULT_P else 1e-3
-    ep = {"p_i": 0.0, "p_state_p": 0.0, "p_m": 0.0, "p_CX": p, "p_idling_gate": 0.0}
+    if a.circuit_noise == "all":
+        ep = {"p_i": p, "p_state_p": p, "p_m": p, "p_CX": p, "p_idling_gate": p}
+    else:
+        ep = {"p_i": 0.0, "p_state_p": 0.0, "p_m": 0.0, "p_CX": p, "p_idling_gate": 0.0}
     sim = CodeSimulator_Circuit_SpaceTime(code=code, p=p, num_cycles=a.num_cycles, num_rep=a.num_rep, error_params=ep,
-                                          eval_logical_type="Z", seed=SEED + 7)
+                                          eval_logical_type="Z", seed=SEED + 7, sampler=a.sampler)
     sim._generate_circuit()
     sim._generate_circuit_graph()
     g = sim.circuit_graph
@@ -808,15 +818,17 @@ def circuit_main(a, torch, dist, world, rank, dev):
            "value": shots / elapsed, "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
            "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
            "dtype": "f64", "data": "synthetic: Philox-sampled DEM mechanisms of the restated stim circuit",
-           "config": {"workload": f"toric d3 (hgp(ring_code(3), ring_code(3))), p_CX={p}, num_rep={a.num_rep}, "
-                                  f"num_cycles={a.num_cycles}, BP (max_iter {mi}) rounds + BP+OSD-E(10) final",
-                      "samples_per_gpu_step": S, "dem_mechanisms": sim.dem.num_errors,
+           "config": {"workload": f"toric d{d} (hgp(ring_code({d}), ring_code({d}))), "
+                                  + (f"p_CX={p}" if a.circuit_noise == "cx" else f"every noise source at p={p}")
+                                  + f", num_rep={a.num_rep}, num_cycles={a.num_cycles}, BP (max_iter {mi}) rounds + "
+                                    f"BP+OSD-E(10) final, {a.sampler} DEM sampler",
+                      "samples_per_gpu_step": S, "dem_mechanisms": sim.dem.num_errors, "sampler": a.sampler,
                       "h1": list(np.shape(g["h1"])), "h2": list(np.shape(g["h2"])),
                       "parallelism": f"sample-sharded x{world}"},
            "logical_error_rate": fails / max(shots, 1),
            "wer_per_cycle": word_error_rate_per_cycle(fails, shots, code.K, a.num_cycles),
-           "printed_reference_wer": 0.00019299501269032238 if p == 1e-3 and a.num_cycles == 13 and a.num_rep == 3
-           else None,
+           "printed_reference_wer": 0.00019299501269032238 if (p == 1e-3 and a.num_cycles == 13 and a.num_rep == 3
+                                                               and d == 3 and a.circuit_noise == "cx") else None,
            "roofline": circuit_kernel_roofline(torch, sim, g, dev, min(S, 65536))}
     if rank == 0:
         emit(out)

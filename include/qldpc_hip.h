@@ -116,6 +116,10 @@ int qldpc_bp_decode_batch(qldpc_bp *bp, const uint8_t *d_synd, uint8_t *d_corr, 
  * can write posteriors); qldpc_bp_decode_batch_soft is qldpc_bp_decode_batch
  * plus d_post: double [B][n] = the last iteration's posterior log-probability
  * ratios (ldpc's log_prob_ratios; exact fp32 values widened in fp32 mode).
+ * A product-sum decoder (qldpc_bp_create with bp_method 0, engine 5) takes
+ * qldpc_bp_decode_batch_soft too: d_post = ldpc bp_decode_prob_ratios'
+ * log_prob_ratios = log(1 / posterior ratio) in double (the device's log: equal
+ * to libm's except for rare 1-ulp differences).
  */
 int qldpc_bp_create_soft(qldpc_graph *g, const double *channel_probs, int32_t max_iter, double ms_scaling_factor,
                          int32_t precision, qldpc_bp **out);
@@ -404,6 +408,13 @@ int qldpc_circ_create(const qldpc_graph *dem, const qldpc_graph *dem_obs, const 
  * except past the GPU kernel's envelope (n > 8192, osd_e order > 24), where the host stage decodes
  * the final layer (one synchronous D2H / H2D round trip per batch inside qldpc_circ_launch). */
 int qldpc_circ_set_final_osd(qldpc_circ *circ, qldpc_osd_gpu *osd_gpu, const qldpc_osd *osd_host);
+/* DEM sampler of qldpc_circ_launch / qldpc_circ_sample (stim's compile_detector_sampler().sample,
+ * src/Simulators_SpaceTime.py:940, :1029): 1 = geometric skip (the default since round 6: per
+ * mechanism and global 64-sample word, Philox-drawn gaps u < ceil(2^53 (1 - p)^k); ~1 + 64 p draws
+ * per word), 0 = keyed (one Philox uniform per (sample, mechanism), u < p).  Both are exact
+ * Bernoulli(p_j) samplers keyed by global sample indices (shard-invariant); they draw different
+ * samples. */
+int qldpc_circ_set_sampler(qldpc_circ *circ, int32_t sampler);
 int qldpc_circ_info(const qldpc_circ *circ, int32_t *detectors, int32_t *observables, int32_t *mechanisms);
 int qldpc_circ_launch(qldpc_circ *circ, uint64_t seed, uint64_t shot_begin, int64_t shot_count, void *d_counters,
                       uint8_t *d_fail, uint8_t *d_detobs, void *stream);

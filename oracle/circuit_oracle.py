@@ -124,13 +124,72 @@ def dem_as_map(dem):
     return {(tuple(d), tuple(k)): p for p, d, k in zip(dem.probs, dem.dets, dem.obs)}
 
 
-def sample_mechanisms(probs, seed, shot_begin, shot_count):
-    """[S][M] uint8: mechanism j of shot s fires when Philox uniform(seed, shot, j) < p_j."""
+def sample_mechanisms_keyed(probs, seed, shot_begin, shot_count):
+    """[S][M] uint8, the keyed sampler (``qldpc_circ_set_sampler(c, 0)``): mechanism j of shot s fires
+    when Philox uniform(seed, shot, j) < p_j."""
     M = len(probs)
     out = np.zeros((shot_count, M), np.uint8)
     for s in range(shot_count):
         for j, p in enumerate(probs):
             out[s, j] = oracle.uniform(seed, shot_begin + s, j, STREAM_CIRC) < p
+    return out
+
+
+STREAM_SKIP = 0x51D50004  # Philox counter word 3 of the geometric-skip sampler (csrc/circuit.hip kStreamSkip)
+
+
+def _ceil53(t):
+    return math.ceil(math.ldexp(t, 53)) if t > 0.0 else 0
+
+
+def skip_thresholds(p):
+    """T_k = ceil(2^53 (1 - p)^k), k = 1..64, (1 - p)^k by repeated IEEE multiplication (as the
+    library's host table in qldpc_circ_create)."""
+    q, t, out = 1.0 - float(p), 1.0, []
+    for _ in range(64):
+        t *= q
+        out.append(_ceil53(t))
+    return out
+
+
+def skip_word(seed, j, gw, T):
+    """The 64 samples 64 gw .. 64 gw + 63 of mechanism j as a bit word (bit b = sample 64 gw + b):
+    from position pos, G = #{k in 1..64-pos : u < T_k} non-firing samples, then a firing; u the 53-bit
+    Philox integer of (seed, j, gw, draw index c) (csrc/circuit.hip skip_word)."""
+    bits, pos, c = 0, 0, 0
+    while c <= 64:
+        shot = (gw & 0xFFFFFFFF) | ((((gw >> 32) << 8) | c) << 32)
+        u = int(oracle.uniform(seed, shot, j, STREAM_SKIP) * 9007199254740992.0)
+        g = 0
+        while g < 64 - pos and T[g] > u:  # T non-increasing: the count of k with T_k > u
+            g += 1
+        pos += g
+        if pos >= 64:
+            break
+        bits |= 1 << pos
+        pos += 1
+        c += 1
+    return bits
+
+
+def sample_mechanisms(probs, seed, shot_begin, shot_count):
+    """[S][M] uint8, the geometric-skip sampler (the default, ``qldpc_circ_set_sampler(c, 1)``):
+    per mechanism the global 64-sample words covering the shots, each from :func:`skip_word`."""
+    M = len(probs)
+    out = np.zeros((shot_count, M), np.uint8)
+    if shot_count <= 0:
+        return out
+    g0, g1 = shot_begin >> 6, (shot_begin + shot_count - 1) >> 6
+    for j, p in enumerate(probs):
+        T = skip_thresholds(p)
+        for gw in range(g0, g1 + 1):
+            w = skip_word(seed, j, gw, T)
+            while w:
+                b = (w & -w).bit_length() - 1
+                w &= w - 1
+                s = gw * 64 + b - shot_begin
+                if 0 <= s < shot_count:
+                    out[s, j] = 1
     return out
 
 

@@ -52,6 +52,10 @@ def lib():
         L.oracle_bp_decode_batch_soft.argtypes = [
             ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, ctypes.c_double,
             ctypes.c_int, _u8p, _u8p, _i32p, _u8p, _f64p, ctypes.c_int64, ctypes.c_int]
+        L.oracle_bp_decode_batch_soft_method.restype = ctypes.c_int
+        L.oracle_bp_decode_batch_soft_method.argtypes = [
+            ctypes.c_int, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+            ctypes.c_int, _u8p, _u8p, _i32p, _u8p, _f64p, ctypes.c_int64, ctypes.c_int]
         L.oracle_philox4x32_10.restype = None
         L.oracle_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.oracle_uniform.restype = ctypes.c_double
@@ -91,8 +95,9 @@ def bp_decode_batch(H, channel_probs, max_iter, bp_method="minimum_sum", ms_scal
 
 
 def bp_decode_batch_soft(H, channel_probs, max_iter, ms_scaling_factor=0.625, synd=None, precision=64,
-                         nthreads=0):
-    """Min-sum BP that also returns the final ``log_prob_ratios`` [B, n] (OSD's sort key)."""
+                         nthreads=0, bp_method="minimum_sum"):
+    """BP that also returns the final ``log_prob_ratios`` [B, n] (OSD's sort key): min-sum's posterior
+    sums, or (``bp_method="product_sum"``) ldpc's ``log(1 / ratio)`` of ``bp_decode_prob_ratios``."""
     m, n, rp, ci = _csr(H)
     synd = np.ascontiguousarray(np.atleast_2d(np.asarray(synd)).astype(np.uint8) & 1)
     B = synd.shape[0]
@@ -102,8 +107,9 @@ def bp_decode_batch_soft(H, channel_probs, max_iter, ms_scaling_factor=0.625, sy
     conv = np.zeros(B, np.uint8)
     post = np.zeros((B, n), np.float64)
     probs = np.ascontiguousarray(np.broadcast_to(np.asarray(channel_probs, np.float64), (n,)))
-    rc = lib().oracle_bp_decode_batch_soft(m, n, rp, ci, probs, int(max_iter), float(ms_scaling_factor),
-                                           int(precision), synd, corr, iters, conv, post, B, int(nthreads))
+    rc = lib().oracle_bp_decode_batch_soft_method(m, n, rp, ci, probs, int(max_iter), METHODS[bp_method],
+                                                  float(ms_scaling_factor), int(precision), synd, corr, iters, conv,
+                                                  post, B, int(nthreads))
     if rc:
         raise RuntimeError("oracle_bp_decode_batch_soft failed")
     return corr, iters, conv.astype(bool), post

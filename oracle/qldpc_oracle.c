@@ -197,6 +197,8 @@ static int bp_ps_##SUFFIX(const graph_t *g, const bp_params_t *P, ws_##SUFFIX *w
                 if (isnan(temp)) temp = (T)1;                                                   \
             }                                                                                   \
             w->dec[j] = (temp >= (T)1) ? 1 : 0;                                                 \
+            /* ldpc bp_decode_prob_ratios: log_prob_ratios[j] = log(1 / temp) (OSD's sort key) */\
+            w->lpr[j] = (T)log(1.0 / (double)temp);                                             \
             temp = (T)1;                                                                        \
             for (int k = k1 - 1; k >= k0; k--) {                                                \
                 int e = g->col_edge[k];                                                         \
@@ -237,13 +239,22 @@ ORACLE_API int oracle_bp_decode_batch(int m, int n, const int32_t *row_ptr, cons
                                 synd, corr, iters, conv, NULL, B, nthreads);
 }
 
-/* The same plus post [B][n]: the final log_prob_ratios (min-sum only), the
- * input of ldpc's OSD (bposd_decoder.osd). */
+/* The same plus post [B][n]: the final log_prob_ratios, the input of ldpc's OSD
+ * (bposd_decoder.osd): min-sum's posterior sums, or product-sum's log(1 / ratio)
+ * (method 0; ldpc's bp_decode_prob_ratios). */
 ORACLE_API int oracle_bp_decode_batch_soft(int m, int n, const int32_t *row_ptr, const int32_t *col_idx,
                                            const double *channel_probs, int max_iter, double alpha,
                                            int precision, const uint8_t *synd, uint8_t *corr, int32_t *iters,
                                            uint8_t *conv, double *post, int64_t B, int nthreads) {
     return bp_decode_batch_impl(m, n, row_ptr, col_idx, channel_probs, max_iter, 1, alpha, precision,
+                                synd, corr, iters, conv, post, B, nthreads);
+}
+ORACLE_API int oracle_bp_decode_batch_soft_method(int m, int n, const int32_t *row_ptr, const int32_t *col_idx,
+                                                  const double *channel_probs, int max_iter, int method,
+                                                  double alpha, int precision, const uint8_t *synd, uint8_t *corr,
+                                                  int32_t *iters, uint8_t *conv, double *post, int64_t B,
+                                                  int nthreads) {
+    return bp_decode_batch_impl(m, n, row_ptr, col_idx, channel_probs, max_iter, method, alpha, precision,
                                 synd, corr, iters, conv, post, B, nthreads);
 }
 

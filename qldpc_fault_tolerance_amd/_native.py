@@ -27,7 +27,7 @@ EXPORTED = [
     "qldpc_bp_bank_stats", "qldpc_bp_create_hbm", "qldpc_mc_set_osd", "qldpc_comm_unique_id",
     "qldpc_comm_init_rank", "qldpc_comm_init_all", "qldpc_comm_rank", "qldpc_comm_allreduce_counters",
     "qldpc_comm_allreduce_counters_group", "qldpc_comm_destroy", "qldpc_mc_run_sharded", "qldpc_sample_errors",
-    "qldpc_stream_sync", "qldpc_bp_kernel_id", "qldpc_build_flags", "qldpc_circ_create", "qldpc_circ_set_final_osd",
+    "qldpc_stream_sync", "qldpc_bp_kernel_id", "qldpc_build_flags", "qldpc_circ_create", "qldpc_circ_set_final_osd", "qldpc_circ_set_sampler",
     "qldpc_circ_info", "qldpc_circ_launch", "qldpc_circ_sample", "qldpc_circ_destroy",
     "qldpc_shard_range", "qldpc_bp_lds_model", "qldpc_m2s_place_model",
 ]
@@ -186,6 +186,8 @@ def _declare(L):
     L.qldpc_circ_create.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i64, _pp]
     L.qldpc_circ_set_final_osd.restype = ctypes.c_int
     L.qldpc_circ_set_final_osd.argtypes = [_vp, _vp, _vp]
+    L.qldpc_circ_set_sampler.restype = ctypes.c_int
+    L.qldpc_circ_set_sampler.argtypes = [_vp, ctypes.c_int32]
     L.qldpc_circ_info.restype = ctypes.c_int
     L.qldpc_circ_info.argtypes = [_vp] + [ctypes.POINTER(_i32)] * 3
     L.qldpc_circ_launch.restype = ctypes.c_int

@@ -37,6 +37,7 @@ struct PsArgs {
   uint8_t* corr;        // [B][n]
   int32_t* iters;       // [B] or NULL
   uint8_t* conv;        // [B] or NULL
+  double* post;         // [B][n] or NULL: ldpc's log_prob_ratios = log(1 / ratio) of the last iteration
   long long B;
   int m, n, E, max_iter;
 };
@@ -99,6 +100,10 @@ __global__ void __launch_bounds__(kPsThreads) ps_decode_kernel(PsArgs A) {
           if (__builtin_isnan(temp)) temp = one;
         }
         dec[j] = temp >= one ? 1 : 0;
+        // soft output (BP+OSD with bp_method="product_sum"): ldpc sets log_prob_ratios[j] = log(1 / temp)
+        // every iteration, so the last one's stays; evaluated in double with the device's log (libm's
+        // log on the host: the two agree to the last bit except for rare 1-ulp differences)
+        if (A.post) A.post[b * n + j] = (double)(T)log(1.0 / (double)temp);
         temp = one;
         for (int k = k1 - 1; k >= k0; --k) {
           const int e = A.ce[k];
@@ -146,7 +151,7 @@ const void* ps_kernel(int precision) {
 }
 
 int ps_decode_launch(const qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int32_t* iters, uint8_t* conv, int64_t B,
-                     hipStream_t stream) {
+                     hipStream_t stream, double* post) {
   const qldpc_graph* g = bp->g;
   PsArgs a;
   a.rp = static_cast<const int32_t*>(bp->ps_rp.p);
@@ -159,6 +164,7 @@ int ps_decode_launch(const qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int
   a.corr = corr;
   a.iters = iters;
   a.conv = conv;
+  a.post = post;
   a.B = B;
   a.m = g->m;
   a.n = g->n;

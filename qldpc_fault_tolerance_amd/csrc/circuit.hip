@@ -59,6 +59,61 @@ __global__ void __launch_bounds__(kTileC) cs_sample(const int32_t* __restrict__ 
   }
 }
 
+// Geometric-skip DEM sampling (round 6; the default sampler).  The keyed sampler
+// above draws one Philox number per (sample, mechanism): B x M draws per batch, almost all of them
+// misses at circuit-level rates (p_j ~ 1e-3).  Here the samples of mechanism j are generated per
+// GLOBAL 64-sample word gw (samples 64 gw .. 64 gw + 63) as a run of geometric gaps: from position
+// pos, the number of non-firing samples before the next firing is G = #{k in 1..64-pos : u < T_k},
+// u the 53-bit Philox integer of (seed, j, gw, draw index c), T_k = ceil(2^53 (1 - p_j)^k) (host
+// table, (1 - p)^k by repeated IEEE multiplication), so P(G >= k) = (1 - p_j)^k exactly as the
+// keyed comparison u < ceil(2^53 p) prices one sample; the word costs 1 + (#firings) draws, ~1.06 at
+// p = 1e-3 instead of 64.  The words are keyed by the global word index, so any batching or sharding
+// (shot0 not a multiple of 64: a batch word spans two global words) draws the same samples.
+// oracle/circuit_oracle.py sample_mechanisms restates it.
+constexpr uint32_t kStreamSkip = 0x51D50004u;
+__device__ inline u64 skip_word(u64 seed, uint32_t j, u64 gw, const u64* __restrict__ t) {
+  u64 bits = 0;
+  int pos = 0;
+  for (uint32_t c = 0; c <= 64u; ++c) {  // at most 64 firings: the loop always ends
+    uint32_t w0, w1;
+    philox4x32_10(j, (uint32_t)gw, ((uint32_t)(gw >> 32) << 8) | c, kStreamSkip, (uint32_t)seed, (uint32_t)(seed >> 32),
+                  w0, w1);
+    const u64 u = ((u64)(w0 >> 5) << 26) | (u64)(w1 >> 6);
+    // G = the largest k in [0, 64 - pos] with k == 0 or T_k > u (T non-increasing): binary search
+    int lo = 0, hi = 64 - pos;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (t[mid - 1] > u) lo = mid; else hi = mid - 1;
+    }
+    pos += lo;
+    if (pos >= 64) break;
+    bits |= 1ull << pos;
+    ++pos;
+  }
+  return bits;
+}
+// grid x = batch words (tiles of 256), y = mechanisms (strided); one thread per (mechanism, word):
+// its batch word from the one or two global words it spans, then one 64-bit atomic xor per touched
+// row when the word is nonzero
+__global__ void __launch_bounds__(kTileC) cs_sample_skip(const int32_t* __restrict__ mp, const int32_t* __restrict__ mr,
+                                                        const u64* __restrict__ T, int M, u64 seed, u64 shot0,
+                                                        long long count, int W, u64* __restrict__ DO) {
+  const int w = blockIdx.x * kTileC + threadIdx.x;
+  if (w >= W) return;
+  const int a = (int)(shot0 & 63u);
+  const u64 gw = (shot0 >> 6) + (u64)w;
+  const long long nb = count - (long long)w * 64;
+  const u64 valid = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
+  for (int j = blockIdx.y; j < M; j += gridDim.y) {
+    const u64* t = T + (size_t)j * 64;
+    u64 word = skip_word(seed, (uint32_t)j, gw, t) >> a;
+    if (a) word |= skip_word(seed, (uint32_t)j, gw + 1, t) << (64 - a);
+    word &= valid;
+    if (word)
+      for (int e = mp[j]; e < mp[j + 1]; ++e) atomicXor(&DO[(long long)mr[e] * W + w], word);
+  }
+}
+
 // bit-sliced rows [row0, row0 + R) (the first nx XORed with X) -> bytes out[s][R].
 // grid x = row tiles, y = word w
 __global__ void __launch_bounds__(kTileC) cs_unpack(const u64* __restrict__ DO, const u64* __restrict__ X, int row0,
@@ -198,6 +253,8 @@ struct qldpc_circ {
   int D = 0, K = 0, M = 0, m = 0, n1 = 0, n2 = 0, rounds = 0, reps = 0;
   long long max_batch = 0;
   DevBuf mp, mr, k53, a_rp, a_ci, f_rp, f_ci;  // mechanism rows, thresholds, [Hs; L1], [h2; L2]
+  DevBuf skipT;                                // [M][64] geometric-skip thresholds ceil(2^53 (1 - p_j)^k)
+  int sampler = 1;                             // 1 = geometric skip (default), 0 = keyed per (sample, mechanism)
   DevBuf DO, acc, failw, synd1, corr1, synd2, corr2, bpcorr2, post2, iters, conv;
 };
 
@@ -247,10 +304,25 @@ int circ_host_osd(qldpc_circ* c, long long B, hipStream_t st) {
   return 0;
 }
 
+// (1)-(2) of one batch: the geometric-skip sampler (default) or the keyed one (qldpc_circ_set_sampler)
+int circ_sample_launch(qldpc_circ* c, uint64_t seed, u64 shot0, long long B, int W, u64* DO, hipStream_t st) {
+  const unsigned gy = (unsigned)std::min(c->M, 65535);
+  if (c->sampler == 1)
+    hipLaunchKernelGGL(cs_sample_skip, dim3((unsigned)((W + kTileC - 1) / kTileC), gy), dim3(kTileC), 0, st,
+                       static_cast<const int32_t*>(c->mp.p), static_cast<const int32_t*>(c->mr.p),
+                       static_cast<const u64*>(c->skipT.p), c->M, (u64)seed, shot0, B, W, DO);
+  else
+    hipLaunchKernelGGL(cs_sample, dim3((unsigned)((B + kTileC - 1) / kTileC), gy), dim3(kTileC), 0, st,
+                       static_cast<const int32_t*>(c->mp.p), static_cast<const int32_t*>(c->mr.p),
+                       static_cast<const u64*>(c->k53.p), c->M, (u64)seed, shot0, B, W, DO);
+  QLDPC_HIP(hipGetLastError());
+  return 0;
+}
+
 void circ_release(qldpc_circ* c) {
   if (c->osd_owned) qldpc_osd_gpu_destroy(c->osd_owned);
   c->osd_owned = nullptr;
-  for (DevBuf* b : {&c->mp, &c->mr, &c->k53, &c->a_rp, &c->a_ci, &c->f_rp, &c->f_ci, &c->DO, &c->acc, &c->failw,
+  for (DevBuf* b : {&c->mp, &c->mr, &c->k53, &c->skipT, &c->a_rp, &c->a_ci, &c->f_rp, &c->f_ci, &c->DO, &c->acc, &c->failw,
                     &c->synd1, &c->corr1, &c->synd2, &c->corr2, &c->bpcorr2, &c->post2, &c->iters, &c->conv})
     b->release();
 }
@@ -314,6 +386,15 @@ int qldpc_circ_create(const qldpc_graph* dem, const qldpc_graph* dem_obs, const 
   }
   std::vector<u64> k53(std::max(1, M));
   for (int j = 0; j < M; ++j) k53[j] = ceil53c(probs[j]);
+  std::vector<u64> skipT((size_t)std::max(1, M) * 64);
+  for (int j = 0; j < M; ++j) {
+    const double q = 1.0 - probs[j];
+    double t = 1.0;
+    for (int k = 0; k < 64; ++k) {
+      t *= q;  // (1 - p)^(k + 1), the same IEEE products as the oracle's
+      skipT[(size_t)j * 64 + k] = ceil53c(t);
+    }
+  }
   std::vector<int32_t> arp, aci, frp, fci;
   if (!sampler_only) {
     stack_csr(h1_space_cor, L1, arp, aci);
@@ -322,9 +403,10 @@ int qldpc_circ_create(const qldpc_graph* dem, const qldpc_graph* dem_obs, const 
   int rc;
   if ((rc = upload_i32(c->mp, mp)) || (rc = upload_i32(c->mr, mr)) || (rc = upload_i32(c->a_rp, arp)) ||
       (rc = upload_i32(c->a_ci, aci)) || (rc = upload_i32(c->f_rp, frp)) || (rc = upload_i32(c->f_ci, fci)) ||
-      (rc = c->k53.alloc(k53.size() * 8)))
+      (rc = c->k53.alloc(k53.size() * 8)) || (rc = c->skipT.alloc(skipT.size() * 8)))
     return fail(rc);
-  if (hipMemcpy(c->k53.p, k53.data(), k53.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMemcpy(c->k53.p, k53.data(), k53.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->skipT.p, skipT.data(), skipT.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
     return fail(set_err(QLDPC_EHIP, "hipMemcpy of the mechanism thresholds failed"));
   const size_t B = (size_t)c->max_batch, W = B / 64;
   if ((rc = c->DO.alloc((size_t)(D + K) * W * 8)) || (rc = c->acc.alloc((size_t)(m + K) * W * 8)) ||
@@ -378,6 +460,13 @@ int qldpc_circ_set_final_osd(qldpc_circ* c, qldpc_osd_gpu* osd_gpu, const qldpc_
   return 0;
 }
 
+int qldpc_circ_set_sampler(qldpc_circ* c, int32_t sampler) {
+  if (!c) return set_err(QLDPC_EINVAL, "NULL circuit handle");
+  if (sampler != 0 && sampler != 1) return set_err(QLDPC_EINVAL, "sampler must be 0 (keyed) or 1 (geometric skip)");
+  c->sampler = sampler;
+  return 0;
+}
+
 int qldpc_circ_destroy(qldpc_circ* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
@@ -410,10 +499,8 @@ int qldpc_circ_sample(qldpc_circ* c, uint64_t seed, uint64_t shot_begin, int64_t
     const int W = (int)((B + 63) / 64);
     QLDPC_HIP(hipMemsetAsync(DO, 0, (size_t)DK * W * 8, st));
     if (c->M > 0) {
-      hipLaunchKernelGGL(cs_sample, dim3((unsigned)((B + kTileC - 1) / kTileC), (unsigned)std::min(c->M, 65535)),
-                         dim3(kTileC), 0, st, static_cast<const int32_t*>(c->mp.p), static_cast<const int32_t*>(c->mr.p),
-                         static_cast<const u64*>(c->k53.p), c->M, (u64)seed, (u64)(shot_begin + c0), B, W, DO);
-      QLDPC_HIP(hipGetLastError());
+      const int rc = circ_sample_launch(c, seed, (u64)(shot_begin + c0), B, W, DO, st);
+      if (rc) return rc;
     }
     hipLaunchKernelGGL(cs_unpack, dim3((unsigned)((DK + kTileC - 1) / kTileC), (unsigned)W), dim3(kTileC), 0, st, DO,
                        static_cast<const u64*>(c->acc.p), 0, DK, 0, d_out + c0 * (long long)DK, W, B);
@@ -440,12 +527,9 @@ int qldpc_circ_launch(qldpc_circ* c, uint64_t seed, uint64_t shot_begin, int64_t
     QLDPC_HIP(hipMemsetAsync(acc, 0, (size_t)(m + K) * W * 8, st));
     QLDPC_HIP(hipMemsetAsync(c->failw.p, 0, (size_t)W * 8, st));
     // (1)-(2) sample the mechanisms, scatter into the detector / observable words
-    const unsigned gy = (unsigned)std::min(c->M, 65535);
     if (c->M > 0) {
-      hipLaunchKernelGGL(cs_sample, dim3((unsigned)((B + kTileC - 1) / kTileC), gy), dim3(kTileC), 0, st,
-                         static_cast<const int32_t*>(c->mp.p), static_cast<const int32_t*>(c->mr.p),
-                         static_cast<const u64*>(c->k53.p), c->M, (u64)seed, (u64)(shot_begin + c0), B, W, DO);
-      QLDPC_HIP(hipGetLastError());
+      const int rc = circ_sample_launch(c, seed, (u64)(shot_begin + c0), B, W, DO, st);
+      if (rc) return rc;
     }
     if (d_detobs) {
       hipLaunchKernelGGL(cs_unpack, dim3((unsigned)((D + K + kTileC - 1) / kTileC), (unsigned)W), dim3(kTileC), 0, st,

@@ -1690,7 +1690,10 @@ int qldpc_bp_decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, 
 int qldpc_bp_decode_batch_soft(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, int32_t* d_iters,
                                uint8_t* d_conv, double* d_post, int64_t B, void* stream) {
   if (!bp || (B > 0 && !d_post)) return set_err(QLDPC_EINVAL, "NULL argument");
-  if (bp->engine != 1) return set_err(QLDPC_ENOTSUP, "soft output needs a decoder from qldpc_bp_create_soft");
+  // engine 1 (min-sum, qldpc_bp_create_soft) or engine 5 (product-sum: any qldpc_bp_create decoder with
+  // bp_method 0 writes ldpc's log_prob_ratios on request)
+  if (bp->engine != 1 && bp->engine != 5)
+    return set_err(QLDPC_ENOTSUP, "soft output needs a decoder from qldpc_bp_create_soft (min-sum) or a product-sum decoder");
   return decode_batch(bp, d_synd, d_corr, d_iters, d_conv, d_post, B, stream);
 }
 
@@ -1704,7 +1707,7 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
   // with every engine); QLDPC_BP1=0 keeps the engine
   // (built with the decoder and on every qldpc_bp_set_channel_probs, bp1_prepare: no uploads here)
   if (!d_post && bp->bp1) return qldpc_rt::bp1_decode(bp->bp1, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
-  if (bp->engine == 5) return ps_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
+  if (bp->engine == 5) return ps_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream, d_post);
   if (bp->engine == 6) return hbm_decode_launch(bp, d_synd, d_corr, d_iters, d_conv, B, (hipStream_t)stream);
   const long long cap = (long long)bp->blocks_per_cu * bp->cus;
   if (bp->engine == 1) {

@@ -136,7 +136,8 @@ namespace qldpc_rt {
 size_t ps_lds_bytes(int precision, int m, int n, int E, bool lds_messages);
 const void* ps_kernel(int precision);
 int ps_decode_launch(const qldpc_bp* bp, const uint8_t* synd, uint8_t* corr, int32_t* iters, uint8_t* conv, int64_t B,
-                     hipStream_t stream);
+                     hipStream_t stream,
+                     double* post = nullptr);
 
 // GPU OSD handle built on this graph? (osd.hip; qldpc_phenl_set_final_osd checks it)
 bool osd_gpu_matches(const qldpc_osd_gpu* o, const qldpc_graph* g);

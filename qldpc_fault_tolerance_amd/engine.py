@@ -117,10 +117,9 @@ class DeviceBP:
             _native.check(_native.lib().qldpc_bp_create_hbm(
                 self.graph.handle, self.channel_probs.ctypes.data_as(ctypes.c_void_p), self.max_iter,
                 self.ms_scaling_factor, self.precision, ctypes.byref(h)), "qldpc_bp_create_hbm")
-        elif self.soft:
-            # BP+OSD: engine 1 hands back the final posteriors (qldpc_bp_create_soft)
-            if self.bp_method != 1:
-                raise NotImplementedError("soft-output BP (BP+OSD) is implemented for minimum_sum")
+        elif self.soft and self.bp_method == 1:
+            # BP+OSD: engine 1 hands back the final posteriors (qldpc_bp_create_soft); a product-sum
+            # decoder (engine 5) writes ldpc's log(1 / ratio) posteriors from the default create
             _native.check(_native.lib().qldpc_bp_create_soft(
                 self.graph.handle, self.channel_probs.ctypes.data_as(ctypes.c_void_p), self.max_iter,
                 self.ms_scaling_factor, self.precision, ctypes.byref(h)), "qldpc_bp_create_soft")
@@ -685,11 +684,17 @@ class DeviceCircuit:
     ``dec1`` decodes each round on h1 (num_rep·m rows), ``dec2`` the final layer on h2; ``hs``
     (h1_space_cor), ``L1`` and ``L2`` are dense 0/1 matrices as ``GenCorrecHyperGraph`` /
     ``GenFaultHyperGraph`` return them.  ``osd``: a :class:`DeviceOSD` (uniform priors) or a
-    :class:`HostOSD` on h2 makes decoder2 BP+OSD (``dec2`` built with ``soft=True``).
+    :class:`HostOSD` on h2 makes decoder2 BP+OSD (``dec2`` built with ``soft=True``).  ``sampler``:
+    "skip" (default: geometric gaps per mechanism and global 64-sample word) or "keyed" (one Philox
+    uniform per (sample, mechanism)); both exact and shard-invariant, different draws
+    (``qldpc_circ_set_sampler``).
     """
 
+    SAMPLERS = {"keyed": 0, "skip": 1}
+
     def __init__(self, dem, dec1: "DeviceBP | None" = None, hs=None, L1=None, dec2: "DeviceBP | None" = None, L2=None,
-                 num_rounds: int = 0, num_rep: int = 1, osd=None, max_batch: int = 0, device: int | None = None):
+                 num_rounds: int = 0, num_rep: int = 1, osd=None, max_batch: int = 0, device: int | None = None,
+                 sampler: str = "skip"):
         sampler_only = dec1 is None and dec2 is None
         if device is None:
             if dec1 is not None:
@@ -713,6 +718,8 @@ class DeviceCircuit:
             None if sampler_only else dec1.handle, hd(2), hd(3), None if sampler_only else dec2.handle, hd(4),
             self.num_rounds, self.num_rep, int(max_batch), ctypes.byref(h)), "qldpc_circ_create")
         self.handle = h
+        self.sampler = sampler
+        _native.check(_native.lib().qldpc_circ_set_sampler(h, self.SAMPLERS[sampler]), "qldpc_circ_set_sampler")
         self._osd = osd
         if osd is not None:
             gpu = osd.handle if isinstance(osd, DeviceOSD) else None

@@ -247,6 +247,10 @@ class CodeSimulator_DataError:
                                 vars_per_thread=vpl)
 
             self._bposd_dev = False
+            # the fused kernel is min-sum: product-sum BP+OSD decoders keep the host-assisted loop
+            if any(d.decoder.bp_method != 1 for d, need in ((self.decoder_x, need_x), (self.decoder_z, need_z))
+                   if need):
+                return None
             bx = fast(self.decoder_x) if need_x else None
             # one fused kernel serves both sectors: the Z sector takes the X sector's geometry
             bz = fast(self.decoder_z, bx.geometry()["vars_per_thread"] if bx is not None else 0) if need_z else None
@@ -711,7 +715,7 @@ class CodeSimulator_Circuit_SpaceTime:
 
     def __init__(self, code=None, decoder1_z=None, decoder1_x=None, decoder2_z=None, decoder2_x=None, p=0,
                  num_cycles=1, num_rep=1, error_params=None, eval_logical_type="Z", circuit_type="coloration",
-                 rand_scheduling_seed=0, seed=None, max_batch=0, compat_dem_text=False):
+                 rand_scheduling_seed=0, seed=None, max_batch=0, compat_dem_text=False, sampler="skip"):
         import copy as _copy
 
         from . import circuit as _circ
@@ -754,6 +758,7 @@ class CodeSimulator_Circuit_SpaceTime:
         self.dem = None
         self.fault_dem = None
         self.seed = int(seed) if seed is not None else None
+        self.sampler = sampler  # DEM sampler of the device loop: "skip" (geometric gaps) or "keyed"
         self.max_batch = int(max_batch)
         self._shot_offset = 0
         self._dev = None
@@ -848,11 +853,11 @@ class CodeSimulator_Circuit_SpaceTime:
                 raise RuntimeError("call _generate_circuit() and _generate_circuit_graph() first")
             cg = self.circuit_graph
             if parts is None:
-                self._dev = DeviceCircuit(self.dem, max_batch=self.max_batch)
+                self._dev = DeviceCircuit(self.dem, max_batch=self.max_batch, sampler=self.sampler)
             else:
                 b1, b2, osd = parts
                 self._dev = DeviceCircuit(self.dem, b1, self.h1_space_cor, cg["L1"], b2, cg["L2"], self.num_rounds,
-                                          self.num_rep, osd=osd, max_batch=self.max_batch)
+                                          self.num_rep, osd=osd, max_batch=self.max_batch, sampler=self.sampler)
             self._dev_key = key
         return self._dev
 
@@ -915,7 +920,7 @@ class _DetectorSampler:
             sim.seed = random.getrandbits(64)
         from .engine import DeviceCircuit
 
-        dev = sim._dev if sim._dev is not None else DeviceCircuit(sim.dem, max_batch=sim.max_batch)
+        dev = sim._dev if sim._dev is not None else DeviceCircuit(sim.dem, max_batch=sim.max_batch, sampler=sim.sampler)
         if sim._dev is None:
             sim._dev, sim._dev_key = dev, None
         out = dev.sample(sim.seed, sim._shot_offset, int(shots))

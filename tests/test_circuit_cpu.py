@@ -251,3 +251,26 @@ def test_compat_parse_reads_mantissas_of_exponent_notation():
         s._generate_circuit()
         s._generate_circuit_graph()
         assert not C.misparsed_mechanisms(s.fault_dem), tag
+
+
+def test_skip_sampler_oracle_is_batch_invariant_and_exact():
+    """oracle/circuit_oracle.py's restatement of the geometric-skip DEM sampler (the device default):
+    keyed by global 64-sample words, so any split of the shot range draws the same samples; p = 0 never
+    fires, p = 1 always does; the thresholds are (1 - p)^k by repeated multiplication, ceil(2^53 x)."""
+    import math
+
+    import circuit_oracle as co
+
+    probs = [0.0, 1.0, 1e-3, 0.05, 0.3, 0.5]
+    whole = co.sample_mechanisms(probs, 99, 70, 300)
+    split = np.vstack([co.sample_mechanisms(probs, 99, 70, 111), co.sample_mechanisms(probs, 99, 181, 189)])
+    assert np.array_equal(whole, split)
+    assert not whole[:, 0].any() and whole[:, 1].all()
+    T = co.skip_thresholds(0.25)
+    t = 1.0
+    for k in range(64):
+        t *= 0.75
+        assert T[k] == math.ceil(math.ldexp(t, 53))
+    assert all(T[k] >= T[k + 1] for k in range(63))
+    big = co.sample_mechanisms([0.05], 5, 0, 64 * 300)
+    assert abs(big.mean() - 0.05) < 5 * np.sqrt(0.05 * 0.95 / big.size)

@@ -80,16 +80,55 @@ ALL_NOISE = {"p_i": 1.0, "p_state_p": 1.0, "p_m": 1.0, "p_CX": 1.0, "p_idling_ga
 DEMO = {"p_i": 0.0, "p_state_p": 0.0, "p_m": 0.0, "p_CX": 1.0, "p_idling_gate": 0.0}
 
 
-def test_dem_sampler_matches_oracle_draws(gpu):
+@pytest.mark.parametrize("sampler", ["skip", "keyed"])
+def test_dem_sampler_matches_oracle_draws(gpu, sampler):
+    """qldpc_circ_sample == the oracle's restatement of the same sampler, bit for bit: the geometric-skip
+    sampler (the default since round 6: per mechanism and global 64-sample word, gaps u < ceil(2^53
+    (1 - p)^k)) and the keyed one (one uniform per (sample, mechanism)); shot_begin 1000 is not a
+    multiple of 64, so every batch word spans two global words."""
     import circuit_oracle
+    from qldpc_fault_tolerance_amd.engine import DeviceCircuit
 
     sim, _ = _sim(4e-3, ALL_NOISE)
     dem = sim.dem
     S = 192
-    got = sim._device().sample(sim.seed, 1000, S)
-    e = circuit_oracle.sample_mechanisms(dem.probs, sim.seed, 1000, S).astype(np.int64)
+    got = DeviceCircuit(dem, sampler=sampler).sample(sim.seed, 1000, S)
+    fn = circuit_oracle.sample_mechanisms if sampler == "skip" else circuit_oracle.sample_mechanisms_keyed
+    e = fn(dem.probs, sim.seed, 1000, S).astype(np.int64)
     want = np.hstack([(e @ dem.check_matrix().T.astype(np.int64)) % 2, (e @ dem.observable_matrix().T.astype(np.int64)) % 2])
     assert got.shape == want.shape and np.array_equal(got, want.astype(np.uint8))
+    assert want.any()
+
+
+def test_skip_sampler_batch_and_shard_invariant(gpu):
+    """The skip sampler keys its words by the GLOBAL sample index: 64-sample batches (max_batch 64) and
+    two shards with an unaligned split draw exactly the samples one batch draws; high mechanism rates
+    (p = 0.3: several gaps per word) included."""
+    from qldpc_fault_tolerance_amd.engine import DeviceCircuit
+
+    sim, _ = _sim(4e-3, ALL_NOISE)
+    dem = sim.dem
+    S = 640
+    one = DeviceCircuit(dem).sample(sim.seed, 77, S)
+    small = DeviceCircuit(dem, max_batch=64).sample(sim.seed, 77, S)
+    d = DeviceCircuit(dem)
+    parts = np.vstack([d.sample(sim.seed, 77, 201), d.sample(sim.seed, 77 + 201, S - 201)])
+    assert np.array_equal(one, small) and np.array_equal(one, parts)
+
+
+def test_skip_sampler_rates(gpu):
+    """Statistics of the skip sampler on a synthetic DEM (one mechanism per detector, rates 1e-4 .. 0.5):
+    every detector's firing count within 5 sigma of Binomial(S, p)."""
+    from qldpc_fault_tolerance_amd.circuit import DetectorErrorModel
+    from qldpc_fault_tolerance_amd.engine import DeviceCircuit
+
+    probs = [1e-4, 1e-3, 0.01, 0.05, 0.2, 0.5]
+    dem = DetectorErrorModel(num_detectors=len(probs), num_observables=1, probs=list(probs),
+                             dets=[[j] for j in range(len(probs))], obs=[[] for _ in probs])
+    S = 1 << 18
+    x = DeviceCircuit(dem).sample(12345, 3, S)[:, :len(probs)].astype(np.int64).sum(0)
+    for k, p in zip(x, probs):
+        assert abs(k - S * p) <= 5 * np.sqrt(S * p * (1 - p)) + 1, (k, S * p)
 
 
 @pytest.mark.parametrize("osd,ratio,ctype", [(True, 10, "coloration"), (False, 3, "random"), (True, 2, "random")])

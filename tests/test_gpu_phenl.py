@@ -361,10 +361,12 @@ def test_firstmin_past_device_envelope_steps_the_engine(gpu, oracle):
     comparison does."""
     rng = np.random.default_rng(11)
     m, n = 12000, 24000
-    rows = np.concatenate([rng.choice(m, 3, replace=False) for _ in range(n)])
-    cols = np.repeat(np.arange(n), 3)
+    # column j on rows j, 7 j + 1 and 13 j + 5 (mod m): three distinct rows, every row of degree 6
+    j = np.arange(n)
     H = np.zeros((m, n), np.uint8)
-    H[rows, cols] = 1
+    for r in (j % m, (7 * j + 1) % m, (13 * j + 5) % m):
+        H[r, j] = 1
+    assert (H.sum(0) == 3).all() and (H.sum(1) == 6).all()
     probs = np.full(n, 0.01)
     fm = decoders.FirstMinBPDecoder(H, probs, 2.5, "minimum_sum", 0.625)
     assert fm._fm is None and fm._bp is not None
