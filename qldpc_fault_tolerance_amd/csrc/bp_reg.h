@@ -78,6 +78,22 @@
 #ifndef QLDPC_M2S_UNIL
 #define QLDPC_M2S_UNIL 1
 #endif
+// m2s on dword-scaled words (space-time family 111313): the V slot address unpacked for the
+// gather is carried to the store (one SDWA per edge and iteration fewer; the backend otherwise
+// unpacks it again at the store)
+#ifndef QLDPC_M2S_KEEPVA
+#define QLDPC_M2S_KEEPVA 1
+#endif
+// m2s check phase: explicit row / tail / F / CS pointers stepped per row
+#ifndef QLDPC_M2S_RPTR
+#define QLDPC_M2S_RPTR 1
+#endif
+// m2s families: each variable slot's previous decisions as a wave lane mask (SGPRs): the flip test
+// is a scalar xor of two masks instead of a bit extract and compare per variable and iteration
+// (not the dword-scaled 1024-thread space-time family: measured 1-2% slower with it, r06g)
+#ifndef QLDPC_M2S_XMASK
+#define QLDPC_M2S_XMASK 1
+#endif
 #include "bp_slot.h"
 
 namespace qldpc {
@@ -964,25 +980,41 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
 // v2c" marks the argmin and c2v = alpha * m2, else alpha * m1.  Same values as ldpc's "m2 if
 // |own| == m1 else m1": with a tie m1 == m2; a slot equal to the own word by chance has
 // m2 == m1 and the own sign == parity, i.e. the same c2v either way.
+constexpr bool m_xmask(int eng) { return QLDPC_M2S_XMASK && eng_sh(eng) != 2; }
+
+// the V slot address a gather computed is kept for the store (m_keepva): the sdwa unpack is an asm
+// statement, which the backend cannot rematerialize once the value passes through an opaque copy
+template <typename T, int DMAX, int VPL, int ENG>
+constexpr bool m_keepva() {
+  return QLDPC_M2S_KEEPVA && eng_m2s(ENG) && !eng_m2v(ENG) && !eng_c2s(ENG) && eng_sh(ENG) == 2 &&
+         RState<T, DMAX, VPL, ENG>::kAbs && !RState<T, DMAX, VPL, ENG>::kSplit && !RState<T, DMAX, VPL, ENG>::kPk;
+}
+
 template <typename T, int DMAX, int VPL, int ND, int ENG, int D3K = 0, int LB = 256>
 __device__ inline void m_gather(const RState<T, DMAX, VPL, ENG>& R, int k, typename FT<T>::U (&an)[DMAX],
-                                typename FT<T>::U (&vn)[DMAX]) {
+                                typename FT<T>::U (&vn)[DMAX], uint32_t (&va)[DMAX]) {
   using U = typename FT<T>::U;
 #pragma unroll
   for (int t = 0; t < ND; ++t) {
     if constexpr (!eng_c2s(ENG)) an[t] = lds_ld<U, true>(nullptr, r_csa(R, k, t));  // (c2s: ea = F word)
-    if constexpr (eng_m2v(ENG))
+    if constexpr (eng_m2v(ENG)) {
       vn[t] = lds_ld<U, true>(nullptr, m2v_va<T, DMAX, VPL, ENG, D3K, LB>(R, k, t));
-    else
+    } else if constexpr (m_keepva<T, DMAX, VPL, ENG>()) {
+      uint32_t a = r_va(R, k, t);
+      asm volatile("" : "+v"(a));
+      va[t] = a;
+      vn[t] = lds_ld<U, true>(nullptr, a);
+    } else {
       vn[t] = lds_ld<U, true>(nullptr, r_va(R, k, t));
+    }
   }
 }
 
 template <typename T, int DMAX, int VPL, int ND, int ENG, int D3K = 0, int LB = 256>
 __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, int k,
                                  const typename FT<T>::U (&an)[DMAX],
-                                 const typename FT<T>::U (&vn)[DMAX], uint32_t fdelta, T alpha, bool xprev,
-                                 double* post, const int32_t* perm) {
+                                 const typename FT<T>::U (&vn)[DMAX], const uint32_t (&va)[DMAX], uint32_t fdelta,
+                                 T alpha, bool xprev, uint64_t& xmk, double* post, const int32_t* perm) {
   using U = typename FT<T>::U;
   constexpr bool KV1 = RState<T, DMAX, VPL, ENG>::kKeepV;
   static_assert(sizeof(T) == 8 && RState<T, DMAX, VPL, ENG>::kAbs && (RState<T, DMAX, VPL, ENG>::kKeepV || eng_c2s(ENG)),
@@ -1031,11 +1063,21 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   for (int t = 0; t < ND; ++t) {
     if constexpr (eng_m2v(ENG))
       lds_st<U, true>(nullptr, m2v_va<T, DMAX, VPL, ENG, D3K, LB>(R, k, t), nv[t]);
+    else if constexpr (m_keepva<T, DMAX, VPL, ENG>())
+      lds_st<U, true>(nullptr, va[t], nv[t]);
     else
       lds_st<U, true>(nullptr, r_va(R, k, t), nv[t]);
     if constexpr (KV1) R.ov[k][t] = nv[t];
   }
-  if (x != xprev) {
+  bool flip;
+  if constexpr (m_xmask(ENG)) {  // (every lane active here: the variable phase is not divergent)
+    const uint64_t bx = __ballot(x);
+    flip = __builtin_amdgcn_inverse_ballot_w64(bx ^ xmk);
+    xmk = bx;
+  } else {
+    flip = x != xprev;
+  }
+  if (flip) {
 #pragma unroll
     for (int t = 0; t < ND; ++t) {
       if constexpr (eng_c2s(ENG))
@@ -1049,7 +1091,8 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
 
 template <typename T, int DMAX, int VPL, int D3K, int ENG, int LB = 256>
 __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, uint32_t fdelta, T alpha, uint32_t xprev,
-                                 bool last_live, double* post = nullptr, const int32_t* perm = nullptr, int TB = 0) {
+                                 uint64_t (&xm)[VPL], bool last_live, double* post = nullptr, const int32_t* perm = nullptr,
+                                 int TB = 0) {
   using U = typename FT<T>::U;
   constexpr int N3 = DMAX > 3 ? 3 : DMAX;
   // gathers one variable ahead: two ahead needs 32 more VGPRs than the 168 of 3 workgroups per
@@ -1060,32 +1103,35 @@ __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
   r_launder<T, DMAX, VPL, ENG, D3K>(R);
   uint32_t xbits = 0;
   U ab[PF][DMAX], vb[PF][DMAX];
-  auto gk = [&](int k, U (&an)[DMAX], U (&vn)[DMAX]) {
+  uint32_t vab[PF][DMAX];
+  auto gk = [&](int k, U (&an)[DMAX], U (&vn)[DMAX], uint32_t (&va)[DMAX]) {
     if (k < eng_d2k(ENG))  // (the space-time family's measurement variables: two edge slots)
-      m_gather<T, DMAX, VPL, 2, ENG, D3K, LB>(R, k, an, vn);
+      m_gather<T, DMAX, VPL, 2, ENG, D3K, LB>(R, k, an, vn, va);
     else if (k < D3K)
-      m_gather<T, DMAX, VPL, N3, ENG, D3K, LB>(R, k, an, vn);
+      m_gather<T, DMAX, VPL, N3, ENG, D3K, LB>(R, k, an, vn, va);
     else
-      m_gather<T, DMAX, VPL, DMAX, ENG, D3K, LB>(R, k, an, vn);
+      m_gather<T, DMAX, VPL, DMAX, ENG, D3K, LB>(R, k, an, vn, va);
   };
 #pragma unroll
-  for (int k = 0; k < PF; ++k) gk(k, ab[k], vb[k]);
+  for (int k = 0; k < PF; ++k) gk(k, ab[k], vb[k], vab[k]);
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     U an[DMAX], vn[DMAX];
+    uint32_t va[DMAX];
 #pragma unroll
     for (int t = 0; t < DMAX; ++t) {
       an[t] = ab[k % PF][t];
       vn[t] = vb[k % PF][t];
+      va[t] = vab[k % PF][t];
     }
-    if (k + PF < VPL) gk(k + PF, ab[k % PF], vb[k % PF]);
+    if (k + PF < VPL) gk(k + PF, ab[k % PF], vb[k % PF], vab[k % PF]);
     if (k == VPL - 1 && !last_live) break;
     const bool xp = ((xprev >> k) & 1u) != 0;
     const int32_t* pk = perm ? perm + k * TB : nullptr;
-    const bool x = k < eng_d2k(ENG) ? m_var_one<T, DMAX, VPL, 2, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk)
-                   : k < D3K        ? m_var_one<T, DMAX, VPL, N3, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk)
-                                    : m_var_one<T, DMAX, VPL, DMAX, ENG, D3K, LB>(smem, R, k, an, vn, fdelta, alpha, xp, post, pk);
-    xbits |= (x ? 1u : 0u) << k;
+    const bool x = k < eng_d2k(ENG) ? m_var_one<T, DMAX, VPL, 2, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk)
+                   : k < D3K        ? m_var_one<T, DMAX, VPL, N3, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk)
+                                    : m_var_one<T, DMAX, VPL, DMAX, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk);
+    if constexpr (!m_xmask(ENG)) xbits |= (x ? 1u : 0u) << k;
   }
   return xbits;
 }
@@ -1120,33 +1166,45 @@ __device__ inline int m_check(unsigned char* smem, const RLayout& Ly, int m, int
   uint32_t coff[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) coff[c] = kRot ? (((uint32_t)c + rot) & (uint32_t)(NCH - 1)) * 16u : (uint32_t)c * 16u;
+  // explicit absolute row pointers (QLDPC_M2S_RPTR): one row base stepped per row (opaque, so the
+  // backend neither splits it into one induction variable per chunk nor re-adds the region offset
+  // per row) plus the tail, F and CS pointers; the argmin is selected as an offset from the row base
+  constexpr bool AP = QLDPC_M2S_RPTR;
+  const uint32_t sb = AP ? lds_base(smem) : 0u;
+  uint32_t rb = sb + Ly.v + 16u + (uint32_t)tid * rstride;
+  uint32_t tp = sb + Ly.t + (uint32_t)tid * (uint32_t)sizeof(T);
+  uint32_t fp = sb + Ly.f + 4u * (uint32_t)(tid + 1);
+  uint32_t cp = sb + (uint32_t)(tid + 1) * (uint32_t)sizeof(T);
   for (int i = tid; i < m; i += TB, ++q) {
-    const uint32_t roff = Ly.v + 16u + (uint32_t)i * rstride;
+    if constexpr (AP) asm volatile("" : "+v"(rb));
+    const uint32_t roff = AP ? rb : Ly.v + 16u + (uint32_t)i * rstride;
+    const uint32_t toff = AP ? tp : Ly.t + (uint32_t)i * (uint32_t)sizeof(T);
+    const uint32_t fo = AP ? fp : Ly.f + 4u * (uint32_t)(i + 1);
+    const uint32_t co = AP ? cp : (uint32_t)(i + 1) * (uint32_t)sizeof(T);
     VT cur[NCH];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) cur[c] = *reinterpret_cast<const VT*>(smem + roff + coff[c]);
-    const uint32_t toff = Ly.t + (uint32_t)i * (uint32_t)sizeof(T);
+    for (int c = 0; c < NCH; ++c) cur[c] = lds_ld<VT, AP>(smem, roff + coff[c]);
     T tcur = (T)0;
-    if (TAIL) tcur = lds_at<T>(smem, toff);
-    const uint32_t fcur = lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1));
+    if (TAIL) tcur = lds_ld<T, AP>(smem, toff);
+    const uint32_t fcur = lds_ld<uint32_t, AP>(smem, fo);
     uint32_t s;
     if (FIRST) {
       s = ((fcur >> 1) ^ (fcur >> 2)) & 1u;
       sbits |= s << q;
-      lds_at<uint32_t>(smem, Ly.f + 4u * (uint32_t)(i + 1)) = (fcur & 4u) | ((fcur >> 2) & 1u);
+      lds_st<uint32_t, AP>(smem, fo, (fcur & 4u) | ((fcur >> 2) & 1u));
     } else {
       s = (sbits >> q) & 1u;
       mism |= (int)((fcur ^ s) & 1u);
     }
     double f1 = FT<T>::val(FT<T>::kSent), f2 = f1;
     uint32_t px = s ? 0x80000000u : 0u;
-    uint32_t amin = roff + coff[0];  // argmin slot (byte offset); any slot when no edge is below the sentinel
+    uint32_t aoff = coff[0];  // argmin slot (offset from the row base); any slot when no edge is below the sentinel
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         const double x = V16<T>::get(cur[c], k);
-        amin = __builtin_fabs(x) < f1 ? roff + coff[c] + 8u * (uint32_t)k : amin;
+        aoff = __builtin_fabs(x) < f1 ? coff[c] + 8u * (uint32_t)k : aoff;
         double t;
         asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x));
         asm("v_min_f64 %0, %1, %2" : "=v"(f2) : "v"(f2), "v"(t));
@@ -1158,6 +1216,7 @@ __device__ inline int m_check(unsigned char* smem, const RLayout& Ly, int m, int
           : "v"(px), "v"((uint32_t)(FT<T>::bits(cur[c].x) >> 32)), "v"((uint32_t)(FT<T>::bits(cur[c].y) >> 32)));
       px = p;
     }
+    uint32_t amin = roff + aoff;
     if (TAIL) {
       const double x = (double)tcur;
       amin = __builtin_fabs(x) < f1 ? toff : amin;
@@ -1168,8 +1227,12 @@ __device__ inline int m_check(unsigned char* smem, const RLayout& Ly, int m, int
       px ^= (uint32_t)(FT<T>::bits(tcur) >> 32);
     }
     const U par = (U)(px & 0x80000000u) << 32;
-    lds_at<U>(smem, (uint32_t)(i + 1) * (uint32_t)sizeof(T)) = FT<T>::bits(f1) | par;
-    lds_at<U>(smem, amin) = FT<T>::bits(f2) | par;
+    lds_st<U, AP>(smem, co, FT<T>::bits(f1) | par);
+    lds_st<U, AP>(smem, amin, FT<T>::bits(f2) | par);
+    rb += (uint32_t)TB * rstride;
+    tp += (uint32_t)TB * (uint32_t)sizeof(T);
+    fp += 4u * (uint32_t)TB;
+    cp += (uint32_t)TB * (uint32_t)sizeof(T);
   }
   return mism;
 }
@@ -1675,16 +1738,21 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
     int it = 1;
     bool conv = false;
     uint32_t xb = 0;
+    uint64_t xm[VPL];  // (m2s families, QLDPC_M2S_XMASK: decisions as wave lane masks)
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) xm[k] = 0;
     long long cslot = -1;  // BP+OSD capture slot of this decode (claimed at its last iteration)
     while (true) {
       int mism;
       double* cpost = nullptr;
       if constexpr (MC && eng_base(ENG) == 3) {
         if (A->c_n && A->c_post[q] && it >= S.max_iter) {  // uniform: the last iteration may end unconverged
-          __shared__ unsigned int s_cslot;
-          if (tid == 0) s_cslot = atomicAdd(&A->c_n[q], 1u);
+          // (lred word 11: no static LDS in these kernels, so the dynamic image starts at address 0
+          // and its offsets fold into the LDS instructions)
+          uint32_t* s_cslot = lred + 11;
+          if (tid == 0) *s_cslot = atomicAdd(&A->c_n[q], 1u);
           __syncthreads();
-          cslot = (long long)s_cslot;
+          cslot = (long long)*s_cslot;
           if (cslot < A->c_cap) cpost = A->c_post[q] + cslot * (long long)n;
         }
       }
@@ -1700,7 +1768,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         constexpr int kPV = (eng_tail(ENG) && !eng_m2x(ENG) && !eng_fb(ENG)) ? 0 : QLDPC_PRIO_V;
         if (kPV) __builtin_amdgcn_s_setprio(kPV);
         if constexpr (eng_m2x(ENG))
-          xb = m_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
+          xb = m_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, xm, last_live, cpost, S.perm + tidl, TB);
         else
           xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
         if (kPV) __builtin_amdgcn_s_setprio(0);
@@ -1748,6 +1816,11 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       conv = any == 0;
       if (conv || it >= S.max_iter) break;
       ++it;
+    }
+    if constexpr (eng_m2x(ENG) && eng_base(ENG) != 4 && m_xmask(ENG)) {
+      xb = 0;
+#pragma unroll
+      for (int k = 0; k < VPL; ++k) xb |= (__builtin_amdgcn_inverse_ballot_w64(xm[k]) ? 1u : 0u) << k;
     }
     const long long sl = c0 + sh;
     if (MC && cslot >= 0 && cslot < A->c_cap) {
@@ -1839,12 +1912,13 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rmc_kernel(SMcArgs
   const int nchunks = (int)((A.shot_count + CH - 1) / CH);
   // chunks come from a queue (A.work): a workgroup that drew short decodes takes more
   // chunks, so the launch does not wait on the unluckiest static share
-  __shared__ int s_next;
+  // the chunk queue's next index in lred word 10 (r_pass clears words 0-9 only; no static LDS)
+  int* s_next = reinterpret_cast<int*>(smem + Ly.lred + 40);
   int ch = blockIdx.x;
   if (A.work) {
-    if (tid == 0) s_next = (int)atomicAdd(A.work, 1u);
+    if (tid == 0) *s_next = (int)atomicAdd(A.work, 1u);
     __syncthreads();
-    ch = s_next;
+    ch = *s_next;
   }
   for (; ch < nchunks;) {
     const long long c0 = (long long)((unsigned long long)(unsigned)ch * (unsigned)CH);
@@ -1872,10 +1946,10 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rmc_kernel(SMcArgs
     if (nf) atomicAdd(&cnt[kCntFail], nf);
     if (tid == 0) {
       cnt[kCntShots] += (unsigned long long)cn;
-      if (A.work) s_next = (int)atomicAdd(A.work, 1u);
+      if (A.work) *s_next = (int)atomicAdd(A.work, 1u);
     }
     __syncthreads();
-    ch = A.work ? s_next : ch + (int)gridDim.x;
+    ch = A.work ? *s_next : ch + (int)gridDim.x;
   }
   __syncthreads();
   if (tid < kCntHist && cnt[tid]) atomicAdd(&A.counters[tid], cnt[tid]);
@@ -1888,12 +1962,13 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rdec_kernel(SDecAr
   const int CH = D.chunk;
   const RLayout Ly = r_layout(eng_base(ENG), D.vslots, D.mmax, (int)sizeof(T), eng_tail(ENG), eng_m2s(ENG) ? 1 : eng_c2s(ENG) ? 2 : 0, eng_fb(ENG));
   const long long nchunks = (D.B + CH - 1) / CH;
-  __shared__ long long s_next;
+  // the chunk queue's next index in lred words 10-11 (r_pass clears words 0-9 only; no static LDS)
+  long long* s_next = reinterpret_cast<long long*>(smem + Ly.lred + 40);
   long long ch = blockIdx.x;
   if (D.work) {
-    if (tid == 0) s_next = (long long)atomicAdd(D.work, 1u);
+    if (tid == 0) *s_next = (long long)atomicAdd(D.work, 1u);
     __syncthreads();
-    ch = s_next;
+    ch = *s_next;
   }
   while (ch < nchunks) {
     const long long c0 = ch * CH;
@@ -1901,9 +1976,9 @@ __global__ __launch_bounds__(LB, (lb_waves<T, ENG>(LB))) void rdec_kernel(SDecAr
     r_pass<T, DMAX, VPL, false, ENG, D3K, NCH>(D.sec, 0, c0, cn, smem, Ly, D.vslots, D.mmax, nullptr, nullptr, nullptr, &D, tid,
                                 TB);
     if (D.work) {  // r_pass ends with a barrier: every thread has read s_next
-      if (tid == 0) s_next = (long long)atomicAdd(D.work, 1u);
+      if (tid == 0) *s_next = (long long)atomicAdd(D.work, 1u);
       __syncthreads();
-      ch = s_next;
+      ch = *s_next;
     } else {
       ch += gridDim.x;
     }

@@ -46,6 +46,26 @@ def counts(lines):
     return c
 
 
+def split_conditional(lines):
+    """VALU of the unconditional path vs the blocks behind `s_cbranch_execz` (decision-flip F-word
+    xors, BP+OSD posterior capture): those run only in waves where some lane takes them."""
+    main, cond, inside = collections.Counter(), collections.Counter(), False
+    for t in lines:
+        t = t.strip()
+        if t.startswith("s_cbranch_execz"):
+            inside = True
+            continue
+        if t.startswith(".LBB"):
+            inside = False
+            continue
+        if not t or t.startswith((";", ".")) or t.endswith(":"):
+            continue
+        op = t.split()[0]
+        if op.startswith("v_"):
+            (cond if inside else main)[op] += 1
+    return main, cond
+
+
 def role_of(op):
     for pat, r in ROLE:
         if re.match(pat, op):
@@ -67,6 +87,7 @@ def main():
     p2 = next(i for i, l in enumerate(K) if "s_setprio 2" in l)
     p0 = next(i for i in range(p2, len(K)) if "s_setprio 0" in K[i])
     var = counts(K[p2:p0])
+    var_main, var_cond = split_conditional(K[p2:p0])
     # the check phase's row loop: the first backward branch after the variable phase's barrier
     b = next(i for i in range(p0, len(K)) if "s_barrier" in K[i])
     loop_end = next(i for i in range(b, len(K)) if re.search(r"s_cbranch_\w+ \.LBB", K[i]) and
@@ -90,8 +111,11 @@ def main():
         by[role_of(op)] += k
     for r, k in by.most_common():
         out.append(f"  {k:4d}  {k / 7:5.2f}/edge  {r}")
-    out.append(f"static total ~ {nv / 24 + nc / 7:.1f} VALU per edge-iteration (measured by SQ_INSTS_VALU: 18.8, "
-               "profiles/r05/headline_sq/)")
+    nm, ncd = sum(var_main.values()), sum(var_cond.values())
+    out.append(f"variable phase, unconditional path: {nm} VALU = {nm / 24:.2f} per edge slot; behind execz branches "
+               f"(decision-flip F-word xors, posterior capture): {ncd}")
+    out.append(f"static total ~ {nv / 24 + nc / 7:.1f} VALU per edge-iteration; unconditional path "
+               f"{nm / 24 + nc / 7:.1f} (SQ_INSTS_VALU per edge-iteration: profiles/r06/headline_sq/)")
     out.append("by opcode, variable phase: " + ", ".join(f"{k} {v}" for k, v in var.most_common()))
     out.append("by opcode, check row: " + ", ".join(f"{k} {v}" for k, v in chk.most_common()))
     text = "\n".join(out) + "\n"
