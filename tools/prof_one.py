@@ -39,4 +39,4 @@ torch.cuda.synchronize()
 w = cnt.cpu().numpy()
 dec = max(1, int(w[2] + w[3]))
 print(f"{name} p={p} shots={S} logical={logical} precision={prec} geometry={(dx or dz).geometry()} "
-      f"iters/decode={(w[4] + w[5]) / dec:.1f}")
+      f"decodes={dec} iters/decode={(w[4] + w[5]) / dec:.3f}")
