@@ -142,6 +142,16 @@ constexpr bool eng_c2s(int E) { return (E / 10000) % 10 == 3; }
 // + 100000 * D2K (byte-F family): slots k < D2K hold variables of column degree <= 2 (the
 // space-time graphs' measurement variables, host-sorted first): no third edge slot kept
 constexpr int eng_d2k(int E) { return (E / 100000) % 10; }
+// narrow waves (round 6): in the fp64 space-time m2s family the waves 0..W_k-1 of variable slot
+// k < kNwSlots (W_k from SSector::nw, host-planned by qldpc_hip.hip st_plan) hold variables of one
+// degree fewer than the slot's compile-time width and compute that slot with one edge slot fewer (no
+// c2v, sum, v2c store or flip xor for it; one wave-uniform branch per such slot): no private dummy
+// edges for the measurement columns of config 5.  The gathers stay full width (the missing edge reads
+// CS[0] / the shared V dummy, unused): branches around them too split the variable phase into basic
+// blocks the scheduler cannot overlap (+2.7 % instead of the edge count's 7.7 %, twice the SALU, 3x
+// the branches; one variable phase compiled per narrow mask instead spills, profiles/r06/config5/)
+constexpr bool eng_nw(int E) { return eng_m2s(E) && !eng_m2v(E) && eng_tail(E) && eng_sh(E) == 2; }
+constexpr int kNwSlots = 2;
 // edge slot t of variable slot k is compile-time absent (m2s / c2s / byte-F kernels)
 template <int ENG, int D3K>
 __device__ constexpr bool no_edge(int k, int t) {
@@ -1092,7 +1102,7 @@ __device__ inline bool m_var_one(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
 template <typename T, int DMAX, int VPL, int D3K, int ENG, int LB = 256>
 __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>& R, uint32_t fdelta, T alpha, uint32_t xprev,
                                  uint64_t (&xm)[VPL], bool last_live, double* post = nullptr, const int32_t* perm = nullptr,
-                                 int TB = 0) {
+                                 int TB = 0, uint32_t nwm = 0) {
   using U = typename FT<T>::U;
   constexpr int N3 = DMAX > 3 ? 3 : DMAX;
   // gathers one variable ahead: two ahead needs 32 more VGPRs than the 168 of 3 workgroups per
@@ -1128,9 +1138,16 @@ __device__ inline uint32_t m_var(unsigned char* smem, RState<T, DMAX, VPL, ENG>&
     if (k == VPL - 1 && !last_live) break;
     const bool xp = ((xprev >> k) & 1u) != 0;
     const int32_t* pk = perm ? perm + k * TB : nullptr;
-    const bool x = k < eng_d2k(ENG) ? m_var_one<T, DMAX, VPL, 2, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk)
-                   : k < D3K        ? m_var_one<T, DMAX, VPL, N3, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk)
-                                    : m_var_one<T, DMAX, VPL, DMAX, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk);
+    bool x;
+    // (narrow waves: bit k of the wave-uniform nwm = this wave computes slot k one edge slot narrower)
+    if (eng_nw(ENG) && k < kNwSlots && ((nwm >> k) & 1u))
+      x = k < eng_d2k(ENG) ? m_var_one<T, DMAX, VPL, 1, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk)
+          : k < D3K        ? m_var_one<T, DMAX, VPL, (N3 > 1 ? N3 - 1 : 1), ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk)
+                           : m_var_one<T, DMAX, VPL, (DMAX > 1 ? DMAX - 1 : 1), ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk);
+    else
+      x = k < eng_d2k(ENG) ? m_var_one<T, DMAX, VPL, 2, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk)
+          : k < D3K        ? m_var_one<T, DMAX, VPL, N3, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk)
+                           : m_var_one<T, DMAX, VPL, DMAX, ENG, D3K, LB>(smem, R, k, an, vn, va, fdelta, alpha, xp, xm[k], post, pk);
     if constexpr (!m_xmask(ENG)) xbits |= (x ? 1u : 0u) << k;
   }
   return xbits;
@@ -1589,6 +1606,14 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   const uint32_t fdelta = eng_base(ENG) == 4 ? Ly.f : M.fbase;
   // waves whose lanes all hold padding variables skip the last variable (engine 4)
   const bool last_live = uni((VPL - 1) * TB + (tid & ~63) < S.npos ? 1 : 0) != 0;
+  // narrow-wave mask of this wave (eng_nw: bit k = slot k one edge slot narrower), scalar
+  uint32_t nwm = 0;
+  if constexpr (eng_nw(ENG)) {
+    const uint32_t wv = (uint32_t)wbase >> 6;
+#pragma unroll
+    for (int k = 0; k < kNwSlots && k < VPL; ++k) nwm |= (wv < ((S.nw >> (5 * k)) & 31u) ? 1u : 0u) << k;
+    nwm = __builtin_amdgcn_readfirstlane(nwm);
+  }
   uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);
   uint32_t* flags = lred + 8;
   const bool adaptive = S.alpha == 0.0;
@@ -1768,7 +1793,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         constexpr int kPV = (eng_tail(ENG) && !eng_m2x(ENG) && !eng_fb(ENG)) ? 0 : QLDPC_PRIO_V;
         if (kPV) __builtin_amdgcn_s_setprio(kPV);
         if constexpr (eng_m2x(ENG))
-          xb = m_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, xm, last_live, cpost, S.perm + tidl, TB);
+          xb = m_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, xm, last_live, cpost, S.perm + tidl, TB, nwm);
         else
           xb = r_var<T, DMAX, VPL, D3K, ENG>(smem, R, fdelta, alpha, xb, last_live, cpost, S.perm + tidl, TB);
         if (kPV) __builtin_amdgcn_s_setprio(0);

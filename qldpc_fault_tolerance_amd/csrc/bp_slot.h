@@ -55,6 +55,8 @@ struct SSector {
   int vlast, vnl;
   int npos;                         // 1 + the last slot position holding a variable (= n unless the
                                     // slot map pads a degree class to whole variable slots)
+  uint32_t nw;                      // narrow waves (the fp64 space-time m2s family): 5 bits per variable
+                                    // slot k, W_k = waves 0..W_k-1 of slot k take one edge slot fewer
 };
 
 struct SMcArgs {

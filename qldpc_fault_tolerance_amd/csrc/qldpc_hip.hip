@@ -399,11 +399,62 @@ static int upload_llr(qldpc_bp* bp) {
 // its CS entry at lab[i] + 1 and its row at position lab[i] of V (see
 // label_checks below).  The F words and the check phase follow the labels; the
 // decode path maps syndromes through the inverse permutation (bp->rperm).
+// Slot plan of the fp64 space-time m2s family (engine id 111313, kern_r_f64_m2st.hip): the
+// variable order, its D2K / D3K, the private dummy count and (narrow) the narrow-wave thresholds.
+// Round 6: the degree classes 1 / 2 / 3 / 4 in column order (config 5: 588 degree-1 and 1,176
+// degree-2 measurement columns, 2,352 degree-3 and 1,323 degree-4 data columns) and, per variable
+// slot k of compile-time width w_k (2 below D2K, 3 below D3K, else DM), the waves 0..W_k-1 whose
+// variables all have degree <= w_k - 1 take one edge slot fewer (a wave-uniform branch, SSector::nw):
+// config 5 executes 15,360 edge slots per iteration for 15,288 edges instead of 16,640, with 68
+// private dummies instead of 1,348.  !narrow: the round-6 classes <= 2 / 3 / 4, W_k = 0.
+struct StPlan {
+  std::vector<int32_t> order;
+  int d2 = 0, d3 = 0, nd = 0;
+  uint32_t nw = 0;
+};
+static StPlan st_plan(const qldpc_graph* g, int tb, int vpl, int DM, bool narrow) {
+  StPlan P;
+  auto cls = [&](int d) { return narrow ? std::min(std::max(d, 1), 4) - 1 : (d <= 2 ? 0 : d <= 3 ? 1 : 2); };
+  P.order.reserve(g->n);
+  for (int c = 0; c < (narrow ? 4 : 3); ++c)
+    for (int j = 0; j < g->n; ++j)
+      if (cls((int)g->col_rows[j].size()) == c) P.order.push_back(j);
+  std::vector<int> deg((size_t)vpl * tb, -1);
+  for (int p = 0; p < g->n && p < vpl * tb; ++p) deg[p] = (int)g->col_rows[P.order[p]].size();
+  auto whole = [&](int lim) {  // leading variable slots whose variables all have degree <= lim
+    int kk = 0;
+    for (; kk < vpl; ++kk) {
+      bool ok = true;
+      for (int t = 0; t < tb && ok; ++t) ok = deg[(size_t)kk * tb + t] <= lim;
+      if (!ok) break;
+    }
+    return kk;
+  };
+  P.d2 = whole(2);
+  P.d3 = whole(3);
+  for (int k = 0; k < vpl; ++k) {
+    const int w = k < P.d2 ? 2 : k < P.d3 ? 3 : DM;
+    int W = 0;
+    if (narrow && k < kNwSlots && 5 * vpl <= 32)
+      for (; W < std::min(tb / 64, 31); ++W) {
+        bool ok = true;
+        for (int t = W * 64; t < W * 64 + 64 && t < tb && ok; ++t) ok = deg[(size_t)k * tb + t] <= w - 1;
+        if (!ok) break;
+      }
+    P.nw |= (uint32_t)W << (5 * k);
+    for (int t = 0; t < tb; ++t) {
+      const int d = deg[(size_t)k * tb + t];
+      if (d >= 0) P.nd += w - ((t >> 6) < W ? 1 : 0) - d;
+    }
+  }
+  return P;
+}
+
 static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int tsize, int nch,
                              const std::vector<int32_t>& slot_var, std::vector<uint32_t>& out, int vbase_dw = -1,
                              const std::vector<int>& lab = {}, int tail = 0, int m2s = 0, int d3k = 0,
                              int dummy0 = -1, int* ndummy = nullptr, int anneal = 0, int anneal_iters = -1,
-                             int tail_base = -1, int d2k = 0) {
+                             int tail_base = -1, int d2k = 0, uint32_t nw = 0) {
   const int nv = 16 / tsize;  // messages per 16-byte chunk
   const int rw = nch * nv;
   const int rwt = rw + (tail ? 1 : 0);  // tail layouts: logical slot rw = the row's tail slot
@@ -623,15 +674,17 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
       }
     }
   // m2s rows of 8 / space-time rows: the missing edges of real variables (slots k >= d3k hold DM
-  // edge slots, d2k <= k < d3k three, k < d2k two) get private V slots from dummy0 on,
-  // lane-consecutive per (k, d) (conflict-free reads and stores), and the dummy CS entry 0
+  // edge slots, d2k <= k < d3k three, k < d2k two; one fewer in the narrow waves of `nw`) get private
+  // V slots from dummy0 on, lane-consecutive per (k, d) (conflict-free reads and stores), and the
+  // dummy CS entry 0
   int nd = 0;
   if (dummy0 >= 0)
     for (int k = 0; k < VPL; ++k)
       for (int d = 0; d < DM; ++d)
         for (int t = 0; t < TB; ++t) {
           const int j = slot_var[(size_t)k * TB + t];
-          if (j >= 0 && d >= (int)g->col_rows[j].size() && d < (k < d2k ? 2 : k < d3k ? 3 : DM))
+          const int w = (k < d2k ? 2 : k < d3k ? 3 : DM) - ((t >> 6) < (int)((nw >> (5 * k)) & 31u) ? 1 : 0);
+          if (j >= 0 && d >= (int)g->col_rows[j].size() && d < w)
             out[((size_t)k * DM + d) * TB + t] = (uint32_t)(dummy0 + nd++) << 16;
         }
   if (ndummy) *ndummy = nd;
@@ -1154,38 +1207,18 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       bool uni = true;
       for (int j = 1; j < g->n && QLDPC_M2S_UNIL; ++j) uni = uni && channel_probs[j] == channel_probs[0];
       if (uni && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb > 512) {
-        // the slot map the build below makes (sort2: degree <= 2, 3, 4 in column order), its D2K / D3K
-        // and the private dummies of build_slot_edges
-        std::vector<int> deg;
-        deg.reserve((size_t)vpl * tb);
-        for (int c = 0; c < 3; ++c)
-          for (int j = 0; j < g->n; ++j) {
-            const int d = (int)g->col_rows[j].size();
-            if ((d <= 2 ? 0 : d <= 3 ? 1 : 2) == c) deg.push_back(d);
-          }
-        deg.resize((size_t)vpl * tb, -1);
-        auto whole = [&](int lim) {  // leading variable slots whose variables all have degree <= lim
-          int kk = 0;
-          for (; kk < vpl; ++kk) {
-            bool ok = true;
-            for (int t = 0; t < tb && ok; ++t) ok = deg[(size_t)kk * tb + t] <= lim;
-            if (!ok) break;
-          }
-          return kk;
-        };
-        const int d2 = whole(2), d3 = whole(3);
-        int nd = 0, dmax = 0;
-        for (int k = 0; k < vpl; ++k)
-          for (int t = 0; t < tb; ++t) {
-            const int d = deg[(size_t)k * tb + t];
-            dmax = std::max(dmax, d);
-            if (d >= 0) nd += (k < d2 ? 2 : k < d3 ? 3 : DM) - d;
-          }
+        // the slot map the build below makes (st_plan), its D2K / D3K and the private dummies of
+        // build_slot_edges
+        const StPlan P = st_plan(g, tb, vpl, DM, env_int("QLDPC_NW", 1) != 0);
+        const int d2 = P.d2, d3 = P.d3, nd = P.nd;
+        int dmax = 0;
+        for (int j = 0; j < g->n; ++j) dmax = std::max(dmax, (int)g->col_rows[j].size());
         const int vs = (1 + g->m * 4) * 2 + nd;
         if (dmax <= DM && d2 >= 1 && vs < 0x3FFFF && get_rvariant_f64_m2st(vpl, d3, d2).dec_k &&
             r_fits(3, vs, g->m, 8, 2, 1, 1)) {
           bp->m2s = 1;
           bp->vslots_dummy = nd;
+          bp->nw = P.nw;
         }
       }
     }
@@ -1285,9 +1318,14 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       const int d = (int)g->col_rows[j].size();
       return sort2 ? (d <= 2 ? 0 : d <= 3 ? 1 : 2) : (d <= 3 ? 0 : 1);
     };
-    for (int pass = 0; pass < (sort2 ? 3 : sort3 ? 2 : 1); ++pass)
-      for (int j = 0; j < g->n; ++j)
-        if (!sort3 || cls(j) == pass) order.push_back(j);
+    // (the fp64 space-time m2s family: st_plan's order, degree classes 1 / 2 / 3 / 4 with narrow waves)
+    const bool stm2s = bp->engine == 3 && precision == 64 && bp->tail && bp->m2s == 1 && bp->nch == 4;
+    if (stm2s)
+      order = st_plan(g, bp->TB, bp->VPL, DM, env_int("QLDPC_NW", 1) != 0).order;
+    else
+      for (int pass = 0; pass < (sort2 ? 3 : sort3 ? 2 : 1); ++pass)
+        for (int j = 0; j < g->n; ++j)
+          if (!sort3 || cls(j) == pass) order.push_back(j);
     bp->slot_var.assign((size_t)VPL * TB, -1);
     for (int j = 0; j < g->n; ++j) bp->slot_var[j] = order[j];
     bp->npos = g->n;
@@ -1396,7 +1434,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
                          : 0,
                      -1,
                      (bp->tail && bp->vslots_dummy) ? (int)(r_layout(3, vslots2, g->m, tsize, 1, bp->m2s).t - r_layout(3, vslots2, g->m, tsize, 1, bp->m2s).v) / tsize : -1,
-                     bp->d2k);
+                     bp->d2k, bp->nw);
     if (ndummy != bp->vslots_dummy) return fail(set_err(QLDPC_EINVAL, "m2s private dummy slot count mismatch"));
     if (bp->engine == 3 && precision == 64 && bp->m2s != 3 && bp->ea_shift == 0)
       lds_model_var_phase(vchk, bp->TB, bp->VPL, DM, bp->d3k,
@@ -1667,6 +1705,7 @@ static SSector ssector_of(const qldpc_bp* bp, const unsigned long long* lmask, i
   s.vlast = bp->m2v_vlast;
   s.vnl = bp->m2v_nl;
   s.npos = bp->npos > 0 ? bp->npos : bp->g->n;
+  s.nw = bp->nw;
   return s;
 }
 
