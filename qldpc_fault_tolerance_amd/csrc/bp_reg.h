@@ -1914,9 +1914,12 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
       st_a = t;
     }
   }
-  if (QLDPC_STAMPS && MC && A->stamps && (tid & 63) == 0) {
+  if (QLDPC_STAMPS && (tid & 63) == 0) {
+    unsigned long long* stp = MC ? A->stamps : D->stamps;
+    if (stp) {
 #pragma unroll
-    for (int k = 0; k < 10; ++k) atomicAdd(&A->stamps[k], st_acc[k]);
+      for (int k = 0; k < 10; ++k) atomicAdd(&stp[k], st_acc[k]);
+    }
   }
   __syncthreads();  // image reused by the next pass
 }

@@ -95,6 +95,7 @@ struct SDecArgs {
   long long B;
   int mmax, vslots, img_bytes, chunk;
   unsigned int* work;  // engine 3: chunk queue head (zeroed per launch), NULL = static chunk striding
+  unsigned long long* stamps;  // diagnostic builds (QLDPC_STAMPS): per-segment cycle sums, else NULL
 };
 
 template <typename T> struct V16;

@@ -1775,6 +1775,11 @@ static int decode_batch(qldpc_bp* bp, const uint8_t* d_synd, uint8_t* d_corr, in
     a.img_bytes = (int)slot_img_bytes(a.vslots, a.mmax, tsize);
     a.chunk = chunk_for(B, cap, bp->NS);
     a.work = nullptr;
+#if QLDPC_STAMPS
+    a.stamps = debug_stamps_buffer();
+#else
+    a.stamps = nullptr;
+#endif
     if (bp->engine >= 3 && env_int("QLDPC_DYN", 1) != 0) {  // chunk queue, ~64 chunks per workgroup
       if (!bp->work.p && bp->work.alloc(16)) return QLDPC_ENOMEM;
       // at most kMaxQueuePops pops of the one queue counter per launch: small graphs run many

@@ -1,4 +1,5 @@
-"""Phase shares of the fused MC kernel from a QLDPC_STAMPS diagnostic build.
+"""Phase shares of the fused MC kernel (or, --st, config 5's space-time decode_batch) from a
+QLDPC_STAMPS diagnostic build.
 
     python tools/build_variant.py libqldpc_hip_stamps.so QLDPC_STAMPS=1
     QLDPC_LIB=$PWD/qldpc_fault_tolerance_amd/libqldpc_hip_stamps.so python tools/stamps.py [prof_one args]
@@ -13,7 +14,9 @@ import runpy
 import sys
 
 here = os.path.dirname(os.path.abspath(__file__))
-sys.argv = [os.path.join(here, "prof_one.py")] + sys.argv[1:]
+# --st: one space-time decode_batch launch of config 5 (tools/prof_st.py args) instead of the fused MC
+st = len(sys.argv) > 1 and sys.argv[1] == "--st"
+sys.argv = [os.path.join(here, "prof_st.py" if st else "prof_one.py")] + sys.argv[(2 if st else 1):]
 runpy.run_path(sys.argv[0], run_name="__main__")
 from qldpc_fault_tolerance_amd import _native  # noqa: E402
 
