@@ -654,22 +654,34 @@ def native_comm_check(torch, dist, world, rank, dev, local, reduced):
     with torch.distributed's result.  Never fatal: a failure is reported in the JSON line."""
     if os.environ.get("QLDPC_NATIVE_COMM_CHECK", "1") == "0" or os.environ.get("QLDPC_DIST_BACKEND", "nccl") != "nccl":
         return None
-    try:
-        from qldpc_fault_tolerance_amd.parallel import NativeComm
+    # every rank takes part in the broadcast and the final all-reduce whatever fails in between, so a
+    # local failure cannot leave the other ranks waiting in a torch collective
+    from qldpc_fault_tolerance_amd.parallel import NativeComm
 
-        uid = [NativeComm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = NativeComm(dev.index, world, rank, uid[0])
-        comm.allreduce_counters(local)
-        torch.cuda.synchronize(dev)
-        same = bool(torch.equal(local, reduced))
-        comm.close()
-        ok = torch.tensor([1 if same else 0], dtype=torch.int64, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        return {"native_allreduce_equals_torch": bool(ok.item()), "ranks": world,
-                "how": "qldpc_comm_init_rank + qldpc_comm_allreduce_counters (C ABI, RCCL) on each rank's counters"}
-    except Exception as e:  # noqa: BLE001
-        return {"native_allreduce_equals_torch": None, "error": repr(e)[:300]}
+    err, same = None, False
+    uid = [None]
+    if rank == 0:
+        try:
+            uid[0] = NativeComm.unique_id()
+        except Exception as e:  # noqa: BLE001
+            err = e
+    dist.broadcast_object_list(uid, src=0)
+    if uid[0] is not None:
+        try:
+            comm = NativeComm(dev.index, world, rank, uid[0])
+            comm.allreduce_counters(local)
+            torch.cuda.synchronize(dev)
+            same = bool(torch.equal(local, reduced))
+            comm.close()
+        except Exception as e:  # noqa: BLE001
+            err = e
+    ok = torch.tensor([1 if same else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    out = {"native_allreduce_equals_torch": bool(ok.item()) if uid[0] is not None else None, "ranks": world,
+           "how": "qldpc_comm_init_rank + qldpc_comm_allreduce_counters (C ABI, RCCL) on each rank's counters"}
+    if err is not None:
+        out["error"] = repr(err)[:300]
+    return out
 
 
 def native_comm_main(a, torch):
