@@ -143,7 +143,7 @@ constexpr bool eng_c2s(int E) { return (E / 10000) % 10 == 3; }
 // space-time graphs' measurement variables, host-sorted first): no third edge slot kept
 constexpr int eng_d2k(int E) { return (E / 100000) % 10; }
 // narrow waves (round 6): in the fp64 space-time m2s family the waves 0..W_k-1 of variable slot
-// k < kNwSlots (W_k from SSector::nw, host-planned by qldpc_hip.hip st_plan) hold variables of one
+// k < kNwSlots (a wave mask per slot in SSector::nw, host-planned by qldpc_hip.hip st_plan) hold variables of one
 // degree fewer than the slot's compile-time width and compute that slot with one edge slot fewer (no
 // c2v, sum, v2c store or flip xor for it; one wave-uniform branch per such slot): no private dummy
 // edges for the measurement columns of config 5.  The gathers stay full width (the missing edge reads
@@ -1605,13 +1605,15 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
   if (AB) M.fbase = Ly.f - (sbase >> (eng_fb(ENG) ? 3 : (sizeof(T) == 4 || eng_m2s(ENG)) ? 1 : 2));
   const uint32_t fdelta = eng_base(ENG) == 4 ? Ly.f : M.fbase;
   // waves whose lanes all hold padding variables skip the last variable (engine 4)
-  const bool last_live = uni((VPL - 1) * TB + (tid & ~63) < S.npos ? 1 : 0) != 0;
+  // (the fp64 space-time m2s family places its waves over the SIMDs: a mask, not a prefix)
+  const bool last_live = eng_nw(ENG) ? ((S.live_last >> ((uint32_t)wbase >> 6)) & 1u) != 0
+                                     : uni((VPL - 1) * TB + (tid & ~63) < S.npos ? 1 : 0) != 0;
   // narrow-wave mask of this wave (eng_nw: bit k = slot k one edge slot narrower), scalar
   uint32_t nwm = 0;
   if constexpr (eng_nw(ENG)) {
     const uint32_t wv = (uint32_t)wbase >> 6;
 #pragma unroll
-    for (int k = 0; k < kNwSlots && k < VPL; ++k) nwm |= (wv < ((S.nw >> (5 * k)) & 31u) ? 1u : 0u) << k;
+    for (int k = 0; k < kNwSlots && k < VPL; ++k) nwm |= ((S.nw >> (16 * k + wv)) & 1u) << k;
     nwm = __builtin_amdgcn_readfirstlane(nwm);
   }
   uint32_t* lred = reinterpret_cast<uint32_t*>(smem + Ly.lred);

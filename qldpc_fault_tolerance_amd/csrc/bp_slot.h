@@ -55,8 +55,9 @@ struct SSector {
   int vlast, vnl;
   int npos;                         // 1 + the last slot position holding a variable (= n unless the
                                     // slot map pads a degree class to whole variable slots)
-  uint32_t nw;                      // narrow waves (the fp64 space-time m2s family): 5 bits per variable
-                                    // slot k, W_k = waves 0..W_k-1 of slot k take one edge slot fewer
+  uint32_t nw;                      // narrow waves (the fp64 space-time m2s family): bit 16 k + w = wave w
+                                    // computes variable slot k (< kNwSlots) one edge slot narrower
+  uint32_t live_last;               // (the same family) bit w = wave w holds variables in the last slot
 };
 
 struct SMcArgs {

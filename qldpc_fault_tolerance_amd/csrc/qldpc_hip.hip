@@ -399,28 +399,33 @@ static int upload_llr(qldpc_bp* bp) {
 // its CS entry at lab[i] + 1 and its row at position lab[i] of V (see
 // label_checks below).  The F words and the check phase follow the labels; the
 // decode path maps syndromes through the inverse permutation (bp->rperm).
-// Slot plan of the fp64 space-time m2s family (engine id 111313, kern_r_f64_m2st.hip): the
-// variable order, its D2K / D3K, the private dummy count and (narrow) the narrow-wave thresholds.
-// Round 6: the degree classes 1 / 2 / 3 / 4 in column order (config 5: 588 degree-1 and 1,176
-// degree-2 measurement columns, 2,352 degree-3 and 1,323 degree-4 data columns) and, per variable
-// slot k of compile-time width w_k (2 below D2K, 3 below D3K, else DM), the waves 0..W_k-1 whose
-// variables all have degree <= w_k - 1 take one edge slot fewer (a wave-uniform branch, SSector::nw):
-// config 5 executes 15,360 edge slots per iteration for 15,288 edges instead of 16,640, with 68
-// private dummies instead of 1,348.  !narrow: the round-6 classes <= 2 / 3 / 4, W_k = 0.
+// Slot plan of the fp64 space-time m2s family (engine id 111313, kern_r_f64_m2st.hip): the slot map
+// (variable of every physical position k * tb + t, -1 = padding), its D2K / D3K, the private dummy
+// count, the narrow-wave masks and the waves live in the last variable slot.  Round 6: the degree
+// classes 1 / 2 / 3 / 4 in column order fill the LOGICAL positions slot-major; per variable slot k <
+// kNwSlots of compile-time width w_k (2 below D2K, 3 below D3K, else DM) the leading logical waves whose
+// variables all have degree <= w_k - 1 compute that slot one edge slot narrower (a wave-uniform branch,
+// SSector::nw bit 16 k + physical wave): config 5 executes 15,360 edge slots per iteration for 15,288
+// edges instead of 16,640, with 68 private dummies instead of 1,348.  Then (balance) the logical waves
+// are placed on physical waves so that the four SIMDs (wave w on SIMD w mod 4) carry equal edge slots
+// per iteration: config 5's logical waves execute 13-17 edge slots per thread (the five holding the
+// sixth variable slot 17), 62 / 59 / 59 / 60 per SIMD in wave order, 60 on every SIMD placed (longest
+// first onto the least loaded SIMD).  !narrow: the classes <= 2 / 3 / 4, no narrow waves.
 struct StPlan {
-  std::vector<int32_t> order;
+  std::vector<int32_t> slots;
   int d2 = 0, d3 = 0, nd = 0;
-  uint32_t nw = 0;
+  uint32_t nw = 0, live_last = 0;
 };
-static StPlan st_plan(const qldpc_graph* g, int tb, int vpl, int DM, bool narrow) {
+static StPlan st_plan(const qldpc_graph* g, int tb, int vpl, int DM, bool narrow, bool balance) {
   StPlan P;
   auto cls = [&](int d) { return narrow ? std::min(std::max(d, 1), 4) - 1 : (d <= 2 ? 0 : d <= 3 ? 1 : 2); };
-  P.order.reserve(g->n);
+  std::vector<int32_t> order;
+  order.reserve(g->n);
   for (int c = 0; c < (narrow ? 4 : 3); ++c)
     for (int j = 0; j < g->n; ++j)
-      if (cls((int)g->col_rows[j].size()) == c) P.order.push_back(j);
+      if (cls((int)g->col_rows[j].size()) == c) order.push_back(j);
   std::vector<int> deg((size_t)vpl * tb, -1);
-  for (int p = 0; p < g->n && p < vpl * tb; ++p) deg[p] = (int)g->col_rows[P.order[p]].size();
+  for (int p = 0; p < g->n && p < vpl * tb; ++p) deg[p] = (int)g->col_rows[order[p]].size();
   auto whole = [&](int lim) {  // leading variable slots whose variables all have degree <= lim
     int kk = 0;
     for (; kk < vpl; ++kk) {
@@ -432,20 +437,53 @@ static StPlan st_plan(const qldpc_graph* g, int tb, int vpl, int DM, bool narrow
   };
   P.d2 = whole(2);
   P.d3 = whole(3);
+  const int nwv = (tb + 63) / 64;
+  std::vector<int> W(vpl, 0), units(nwv, 0);
   for (int k = 0; k < vpl; ++k) {
     const int w = k < P.d2 ? 2 : k < P.d3 ? 3 : DM;
-    int W = 0;
-    if (narrow && k < kNwSlots && 5 * vpl <= 32)
-      for (; W < std::min(tb / 64, 31); ++W) {
+    if (narrow && k < kNwSlots && nwv <= 16)
+      for (; W[k] < nwv; ++W[k]) {
         bool ok = true;
-        for (int t = W * 64; t < W * 64 + 64 && t < tb && ok; ++t) ok = deg[(size_t)k * tb + t] <= w - 1;
+        for (int t = W[k] * 64; t < W[k] * 64 + 64 && t < tb && ok; ++t) ok = deg[(size_t)k * tb + t] <= w - 1;
         if (!ok) break;
       }
-    P.nw |= (uint32_t)W << (5 * k);
+    for (int v = 0; v < nwv; ++v) {
+      bool live = k < vpl - 1;
+      for (int t = v * 64; t < v * 64 + 64 && t < tb && !live; ++t) live = deg[(size_t)k * tb + t] >= 0;
+      if (live) units[v] += w - (v < W[k] ? 1 : 0);
+    }
     for (int t = 0; t < tb; ++t) {
       const int d = deg[(size_t)k * tb + t];
-      if (d >= 0) P.nd += w - ((t >> 6) < W ? 1 : 0) - d;
+      if (d >= 0) P.nd += w - ((t >> 6) < W[k] ? 1 : 0) - d;
     }
+  }
+  // logical wave -> physical wave (identity, or balanced over the 4 SIMDs: longest first, least loaded)
+  std::vector<int> phys(nwv);
+  for (int v = 0; v < nwv; ++v) phys[v] = v;
+  if (balance && nwv % 4 == 0 && nwv <= 16) {
+    std::vector<int> byu(nwv);
+    for (int v = 0; v < nwv; ++v) byu[v] = v;
+    std::stable_sort(byu.begin(), byu.end(), [&](int a, int b) { return units[a] > units[b]; });
+    int load[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
+    for (int v : byu) {
+      int best = -1;
+      for (int q = 0; q < 4; ++q)
+        if (cnt[q] < nwv / 4 && (best < 0 || load[q] < load[best])) best = q;
+      phys[v] = best + 4 * cnt[best]++;
+      load[best] += units[v];
+    }
+  }
+  P.slots.assign((size_t)vpl * tb, -1);
+  for (int p = 0; p < g->n && p < vpl * tb; ++p) {
+    const int k = p / tb, t = p % tb;
+    P.slots[(size_t)k * tb + phys[t >> 6] * 64 + (t & 63)] = order[p];
+  }
+  for (int v = 0; v < nwv && v < 32; ++v) {
+    bool live = false;
+    for (int t = v * 64; t < v * 64 + 64 && t < tb && !live; ++t) live = deg[(size_t)(vpl - 1) * tb + t] >= 0;
+    if (live) P.live_last |= 1u << phys[v];
+    for (int k = 0; k < kNwSlots && k < vpl; ++k)
+      if (v < W[k]) P.nw |= 1u << (16 * k + phys[v]);
   }
   return P;
 }
@@ -683,7 +721,7 @@ static void build_slot_edges(const qldpc_graph* g, int TB, int VPL, int DM, int 
       for (int d = 0; d < DM; ++d)
         for (int t = 0; t < TB; ++t) {
           const int j = slot_var[(size_t)k * TB + t];
-          const int w = (k < d2k ? 2 : k < d3k ? 3 : DM) - ((t >> 6) < (int)((nw >> (5 * k)) & 31u) ? 1 : 0);
+          const int w = (k < d2k ? 2 : k < d3k ? 3 : DM) - (k < kNwSlots && ((nw >> (16 * k + (t >> 6))) & 1u) ? 1 : 0);
           if (j >= 0 && d >= (int)g->col_rows[j].size() && d < w)
             out[((size_t)k * DM + d) * TB + t] = (uint32_t)(dummy0 + nd++) << 16;
         }
@@ -1209,7 +1247,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       if (uni && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb > 512) {
         // the slot map the build below makes (st_plan), its D2K / D3K and the private dummies of
         // build_slot_edges
-        const StPlan P = st_plan(g, tb, vpl, DM, env_int("QLDPC_NW", 1) != 0);
+        const StPlan P = st_plan(g, tb, vpl, DM, env_int("QLDPC_NW", 1) != 0, env_int("QLDPC_NW_BAL", 1) != 0);
         const int d2 = P.d2, d3 = P.d3, nd = P.nd;
         int dmax = 0;
         for (int j = 0; j < g->n; ++j) dmax = std::max(dmax, (int)g->col_rows[j].size());
@@ -1219,6 +1257,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
           bp->m2s = 1;
           bp->vslots_dummy = nd;
           bp->nw = P.nw;
+          bp->live_last = P.live_last;
         }
       }
     }
@@ -1320,14 +1359,15 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     };
     // (the fp64 space-time m2s family: st_plan's order, degree classes 1 / 2 / 3 / 4 with narrow waves)
     const bool stm2s = bp->engine == 3 && precision == 64 && bp->tail && bp->m2s == 1 && bp->nch == 4;
-    if (stm2s)
-      order = st_plan(g, bp->TB, bp->VPL, DM, env_int("QLDPC_NW", 1) != 0).order;
-    else
+    if (stm2s) {
+      bp->slot_var = st_plan(g, bp->TB, bp->VPL, DM, env_int("QLDPC_NW", 1) != 0, env_int("QLDPC_NW_BAL", 1) != 0).slots;
+    } else {
       for (int pass = 0; pass < (sort2 ? 3 : sort3 ? 2 : 1); ++pass)
         for (int j = 0; j < g->n; ++j)
           if (!sort3 || cls(j) == pass) order.push_back(j);
-    bp->slot_var.assign((size_t)VPL * TB, -1);
-    for (int j = 0; j < g->n; ++j) bp->slot_var[j] = order[j];
+      bp->slot_var.assign((size_t)VPL * TB, -1);
+      for (int j = 0; j < g->n; ++j) bp->slot_var[j] = order[j];
+    }
     bp->npos = g->n;
     bp->d3k = 0;
     if (sort3)
@@ -1706,6 +1746,7 @@ static SSector ssector_of(const qldpc_bp* bp, const unsigned long long* lmask, i
   s.vnl = bp->m2v_nl;
   s.npos = bp->npos > 0 ? bp->npos : bp->g->n;
   s.nw = bp->nw;
+  s.live_last = bp->live_last;
   return s;
 }
 

@@ -79,6 +79,7 @@ struct qldpc_bp {
   int m2s_pk = 0;        // m2s rows of 8 with packed absolute edge addresses (engine id 10203)
   int vslots_dummy = 0;  // m2s rows of 8 (engine id 10103): private V slots of real variables' missing edges
   uint32_t nw = 0;       // narrow waves of the fp64 space-time m2s family (SSector::nw)
+  uint32_t live_last = 0;  // its waves live in the last variable slot (SSector::live_last)
   int npos = 0;       // 1 + the last slot position holding a variable (SSector::npos)
   qldpc_rt::DevBuf work;       // engine 3 decode_batch: chunk-queue head
   // engines 3/4: variable of each (k, t) slot (-1 = padding).  Engine 3 sorts
