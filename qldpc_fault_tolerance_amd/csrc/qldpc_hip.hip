@@ -1159,9 +1159,11 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     // rows one message wider than whole chunks (space-time graphs: rows of 9 = 4 fp64 / 2 fp32
     // chunks + 1): chunk rows + a tail slot per row, dword-scaled addresses, 1024-thread
     // workgroups.  fp64: the image fits LDS at all (162.7 KB instead of 176 KB); fp32: the check
-    // phase reads 36 instead of 48 bytes per row through the compile-time-width loop.
+    // phase reads 36 instead of 48 bytes per row through the compile-time-width loop.  fp64 images
+    // past the 16-bit layout's 64 KiB take it too (round 6: e.g. hgp_34_n1600 over two rounds, 1536 x
+    // 4736, 117 KB, which ran on engine 2 before: fp64 engine 3 has no dword-scaled plain layout)
     if (bp->engine == 3 && DM == 4 && g->max_row == 9 && env_int("QLDPC_E3_TAIL", 1) != 0 &&
-        (precision == 32 || !r_fits(3, vslots, g->m, tsize, 2))) {
+        (precision == 32 || !r_fits(3, vslots, g->m, tsize, 0))) {
       const int nch_t = 8 * tsize / 16;
       const int vst = (1 + g->m * nch_t) * (16 / tsize);
       int tb = 0, vpl = 0;

@@ -6,8 +6,10 @@ degree, runs the leading waves of the first two variable slots one edge slot nar
 places the logical waves on the SIMDs.  Config 5 (hgp_34_n1225_q3, three rounds: 6 variable slots) is
 replayed against the reference's histories in ``test_gpu_golden.py``; here a second graph with another
 slot structure (hgp_34_n1600 over two rounds: 1536 x 4736, 5 variable slots, 768 degree-1 and 768
-degree-2 measurement columns) and config 5's graph decode i.i.d. syndromes bit-exactly against the
-oracle, and every plan switch (narrow waves, SIMD placement) leaves the outputs unchanged.
+degree-2 measurement columns; an fp64 image of 117 KB that ran on engine 2 before round 6) and config
+5's graph decode i.i.d. syndromes bit-exactly against the oracle, and every plan switch (narrow waves,
+SIMD placement) leaves the outputs unchanged.  hgp_34_n1225_q3 over two rounds (4 variable slots) takes
+the two-word tail family (engine id 1013; the one-word family is built for 5 and 6 slots).
 """
 import numpy as np
 import pytest
@@ -25,8 +27,9 @@ def _synd(H, p, B, seed):
     return (e @ Hd.T % 2).astype(np.uint8), Hd.astype(np.uint8)
 
 
-@pytest.mark.parametrize("name,t0,vpl", [("hgp_34_n1600", 2, 5), ("hgp_34_n1225_q3", 3, 6)])
-def test_space_time_one_word_family_matches_oracle(gpu, oracle, monkeypatch, name, t0, vpl):
+@pytest.mark.parametrize("name,t0,kid,vpl", [("hgp_34_n1600", 2, 111313, 5), ("hgp_34_n1225_q3", 3, 111313, 6),
+                                              ("hgp_34_n1225_q3", 2, 1013, 4)])
+def test_space_time_one_word_family_matches_oracle(gpu, oracle, monkeypatch, name, t0, kid, vpl):
     from qldpc_fault_tolerance_amd.engine import DeviceBP
 
     code = codes.get_code(name)
@@ -38,7 +41,7 @@ def test_space_time_one_word_family_matches_oracle(gpu, oracle, monkeypatch, nam
         probs = np.hstack([p * np.ones(n), p * np.ones(code.hz.shape[0])] * t0)
         dec = DeviceBP(Hst, probs, max_iter=mi, precision=64)
         g = dec.geometry()
-        assert (g["engine"], g["kernel_id"], g["threads"], g["vars_per_thread"]) == (3, 111313, 1024, vpl), g
+        assert (g["engine"], g["kernel_id"], g["threads"], g["vars_per_thread"]) == (3, kid, 1024, vpl), g
         c, i, v = dec.decode_batch(synd)
         oc, oi, ov = oracle.bp_decode_batch(Hd, probs, mi, "minimum_sum", 0.625, synd, 64)
         assert np.array_equal(i, oi) and np.array_equal(v, ov), (name, p)
@@ -48,7 +51,7 @@ def test_space_time_one_word_family_matches_oracle(gpu, oracle, monkeypatch, nam
             for k, val in env.items():
                 monkeypatch.setenv(k, val)
             d2 = DeviceBP(Hst, probs, max_iter=mi, precision=64)
-            assert d2.geometry()["kernel_id"] == 111313
+            assert d2.geometry()["kernel_id"] == kid
             c2, i2, v2 = d2.decode_batch(synd)
             for k in env:
                 monkeypatch.delenv(k)
