@@ -111,7 +111,7 @@ SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int 
   if (m2s) {
     // the fp64 space-time graphs: rows of 4 chunks + a tail slot, dword-scaled addresses, 1024
     // threads (engine id 111313, round 6)
-    if (m2s == 1 && engine == 3 && precision == 64 && dmax == 4 && ea_shift == 2 && nch == 4 && tail && tb > 512)
+    if (m2s == 1 && engine == 3 && precision == 64 && dmax == 4 && ea_shift == 2 && nch == 4 && tail && tb >= 512)
       return get_rvariant_f64_m2st(vpl, d3k, d2k);
     // rows of 8 (4 chunks, no tail array), column degree 5, 256 threads: engine id 10103
     if (m2s == 1 && engine == 3 && precision == 64 && dmax == 5 && ea_shift == 0 && nch == 4 && !tail && tb == 256)
@@ -125,7 +125,8 @@ SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int 
   }
   // fp64 tail layout (rows of 4 chunks + a tail slot, dword-scaled addresses, 1024 threads)
   if (tail) {
-    const bool ok = engine == 3 && dmax == 4 && ea_shift == 2 && nch == (precision == 64 ? 4 : 2) && tb > 512;
+    const bool ok = engine == 3 && dmax == 4 && ea_shift == 2 && nch == (precision == 64 ? 4 : 2) &&
+                    (tb > 512 || (precision == 64 && tb == 512));
     if (!ok) return SVariant{nullptr, nullptr, nullptr, nullptr};
     return precision == 64 ? get_rvariant_f64_st(vpl, d3k, d2k) : get_rvariant_f32_st(vpl, d3k);
   }
@@ -1161,9 +1162,12 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
     // workgroups.  fp64: the image fits LDS at all (162.7 KB instead of 176 KB); fp32: the check
     // phase reads 36 instead of 48 bytes per row through the compile-time-width loop.  fp64 images
     // past the 16-bit layout's 64 KiB take it too (round 6: e.g. hgp_34_n1600 over two rounds, 1536 x
-    // 4736, 117 KB, which ran on engine 2 before: fp64 engine 3 has no dword-scaled plain layout)
-    if (bp->engine == 3 && DM == 4 && g->max_row == 9 && env_int("QLDPC_E3_TAIL", 1) != 0 &&
-        (precision == 32 || !r_fits(3, vslots, g->m, tsize, 0))) {
+    // 4736, 117 KB, which ran on engine 2 before: fp64 engine 3 has no dword-scaled plain layout), and
+    // so do fp64 rows of 8 (the tail slot stays empty: GenBicycleA3 / A4 over 2-5 rounds) and graphs
+    // whose geometry is 512 threads (hgp_34_n625 over three rounds, 900 x 2775: two decodes per CU)
+    const bool f64t = precision == 64 && env_int("QLDPC_E3_TAIL64", 1) != 0;
+    if (bp->engine == 3 && DM == 4 && (g->max_row == 9 || (f64t && g->max_row == 8)) && env_int("QLDPC_E3_TAIL", 1) != 0 &&
+        (precision == 32 || !r_fits(3, vslots, g->m, tsize, f64t ? 0 : 2))) {
       const int nch_t = 8 * tsize / 16;
       const int vst = (1 + g->m * nch_t) * (16 / tsize);
       int tb = 0, vpl = 0;
@@ -1180,7 +1184,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         bp->TB = 512;
         bp->VPL = vpl_fb;
       } else if (r_fits(3, vst, g->m, tsize, 2, 1) && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) &&
-                 tb > 512 && vpl >= 4 && vpl <= 8) {
+                 (tb > 512 || (f64t && tb == 512)) && vpl >= 4 && vpl <= 8) {
         bp->tail = 1;
         bp->nch = nch_t;
         bp->ea_shift = 2;
@@ -1246,7 +1250,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       int tb = 0, vpl = 0;
       bool uni = true;
       for (int j = 1; j < g->n && QLDPC_M2S_UNIL; ++j) uni = uni && channel_probs[j] == channel_probs[0];
-      if (uni && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb > 512) {
+      if (uni && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl) && tb >= 512) {
         // the slot map the build below makes (st_plan), its D2K / D3K and the private dummies of
         // build_slot_edges
         const StPlan P = st_plan(g, tb, vpl, DM, env_int("QLDPC_NW", 1) != 0, env_int("QLDPC_NW_BAL", 1) != 0);

@@ -9,7 +9,9 @@ slot structure (hgp_34_n1600 over two rounds: 1536 x 4736, 5 variable slots, 768
 degree-2 measurement columns; an fp64 image of 117 KB that ran on engine 2 before round 6) and config
 5's graph decode i.i.d. syndromes bit-exactly against the oracle, and every plan switch (narrow waves,
 SIMD placement) leaves the outputs unchanged.  hgp_34_n1225_q3 over two rounds (4 variable slots) takes
-the two-word tail family (engine id 1013; the one-word family is built for 5 and 6 slots).
+the two-word tail family (engine id 1013; the one-word family is built for 5 and 6 slots); hgp_34_n625
+over three rounds and GenBicycleA4 over two (rows of 8: an empty tail slot) run 512-thread workgroups,
+two decodes per CU; GenBicycleA3 over five rounds (rows of 8) the two-word tail family.
 """
 import numpy as np
 import pytest
@@ -27,9 +29,11 @@ def _synd(H, p, B, seed):
     return (e @ Hd.T % 2).astype(np.uint8), Hd.astype(np.uint8)
 
 
-@pytest.mark.parametrize("name,t0,kid,vpl", [("hgp_34_n1600", 2, 111313, 5), ("hgp_34_n1225_q3", 3, 111313, 6),
-                                              ("hgp_34_n1225_q3", 2, 1013, 4)])
-def test_space_time_one_word_family_matches_oracle(gpu, oracle, monkeypatch, name, t0, kid, vpl):
+@pytest.mark.parametrize("name,t0,kid,tb,vpl", [
+    ("hgp_34_n1600", 2, 111313, 1024, 5), ("hgp_34_n1225_q3", 3, 111313, 1024, 6), ("hgp_34_n1225_q3", 2, 1013, 1024, 4),
+    # 512-thread geometries (two decodes per CU) and rows of 8 (an empty tail slot per row)
+    ("hgp_34_n625", 3, 111313, 512, 6), ("GenBicycleA4", 2, 111313, 512, 6), ("GenBicycleA3", 5, 1013, 1024, 4)])
+def test_space_time_one_word_family_matches_oracle(gpu, oracle, monkeypatch, name, t0, kid, tb, vpl):
     from qldpc_fault_tolerance_amd.engine import DeviceBP
 
     code = codes.get_code(name)
@@ -41,7 +45,7 @@ def test_space_time_one_word_family_matches_oracle(gpu, oracle, monkeypatch, nam
         probs = np.hstack([p * np.ones(n), p * np.ones(code.hz.shape[0])] * t0)
         dec = DeviceBP(Hst, probs, max_iter=mi, precision=64)
         g = dec.geometry()
-        assert (g["engine"], g["kernel_id"], g["threads"], g["vars_per_thread"]) == (3, kid, 1024, vpl), g
+        assert (g["engine"], g["kernel_id"], g["threads"], g["vars_per_thread"]) == (3, kid, tb, vpl), g
         c, i, v = dec.decode_batch(synd)
         oc, oi, ov = oracle.bp_decode_batch(Hd, probs, mi, "minimum_sum", 0.625, synd, 64)
         assert np.array_equal(i, oi) and np.array_equal(v, ov), (name, p)
