@@ -113,8 +113,8 @@ SVariant slot_variant(int engine, int precision, int dmax, int ns, int vpl, int 
     // threads (engine id 111313, round 6)
     if (m2s == 1 && engine == 3 && precision == 64 && dmax == 4 && ea_shift == 2 && nch == 4 && tail && tb >= 512)
       return get_rvariant_f64_m2st(vpl, d3k, d2k);
-    // rows of 8 (4 chunks, no tail array), column degree 5, 256 threads: engine id 10103
-    if (m2s == 1 && engine == 3 && precision == 64 && dmax == 5 && ea_shift == 0 && nch == 4 && !tail && tb == 256)
+    // rows of 8 (4 chunks, no tail array), column degree 5, 256 threads (128 / 192 for small graphs): engine id 10103
+    if (m2s == 1 && engine == 3 && precision == 64 && dmax == 5 && ea_shift == 0 && nch == 4 && !tail && tb <= 256)
       return pk ? get_rvariant_f64_m2s8pk(vpl, d3k) : get_rvariant_f64_m2s8(vpl, d3k);
     const bool ok = engine == 3 && precision == 64 && dmax == 4 && ea_shift == 0 && nch == 3 && tail && tb <= 256;
     if (m2s == 3)  // variable-major V slots: no tail array, 256 threads
@@ -1267,6 +1267,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         }
       }
     }
+    int m2s8_vpt = 0;  // (the rows-of-8 family's 128-thread geometry for small graphs, below)
     // the same family for rows of 8 and column degree 5 (kern_r_f64_m2s8.hip, engine id 10103): the
     // lifted-product codes (LP_Matg8_L30: 750 degree-3 and 270 degree-5 columns, rows of 8).  Rows of
     // 4 chunks, no tail array.  Slots k >= D3K hold 5 edge slots; a real variable with fewer edges
@@ -1281,8 +1282,22 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       for (int j = 0; j < g->n; ++j) n3 += g->col_rows[j].size() <= 3;
       bool uni = true;
       for (int j = 1; j < g->n && QLDPC_M2S_UNIL; ++j) uni = uni && channel_probs[j] == channel_probs[0];
-      if (uni && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl, pref, vmax) && tb == 256 && vpl >= 4 &&
-          vpl <= 6) {
+      bool ok = uni && !choose_rgeometry(g->n, g->m, vars_per_thread, tb, vpl, pref, vmax);
+      // smaller graphs (LP_Matg8_L16 / L21, the Threshold notebook's codes: 544 / 714 columns) come out
+      // at 256 threads x 3 variables, below the family's 4-6: run them at the most variables per thread
+      // (<= 5 for degree 5) whose workgroup is smaller, 128 x 5 / 192 x 5 (round 6; they ran on engine 2
+      // before).  The geometry call below then takes this VPL.
+      if (ok && tb == 256 && vpl < 4 && vars_per_thread <= 0 && env_int("QLDPC_TB", 0) <= 0 &&
+          env_int("QLDPC_M2S8_SMALL", 1) != 0)
+        for (int v = std::min(6, vmax); v >= 4 && !m2s8_vpt; --v) {
+          int tb2 = 0, vpl2 = 0;
+          if (!choose_rgeometry(g->n, g->m, v, tb2, vpl2, pref, vmax) && tb2 < 256 && vpl2 == v) {
+            tb = tb2;
+            vpl = vpl2;
+            m2s8_vpt = v;
+          }
+        }
+      if (ok && (tb == 256 || (tb < 256 && m2s8_vpt > 0)) && vpl >= 4 && vpl <= 6) {
         // the slot map below: degree <= 3 first, so slots k < n3 / tb (whole) hold degree <= 3 only
         const int d3 = n3 == g->n ? vpl : n3 / tb;
         int nd = 0;
@@ -1299,6 +1314,7 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
           bp->nch = 4;
           bp->ea_shift = 0;
           bp->vslots_dummy = nd;
+          if (m2s8_vpt > 0) vars_per_thread = m2s8_vpt;
           // packed absolute addresses, 4 workgroups per CU: LP L30 fp64 4.08 M vs 3.67 M shots/s
           // (0.622 vs 0.561 of the LDS roofline, profiles/r04/passd/); QLDPC_M2S8_PK=0 keeps 10103
           bp->m2s_pk = env_int("QLDPC_M2S8_PK", 1) != 0 && vpl <= 5 &&

@@ -146,3 +146,29 @@ def test_m2s8_fused_mc_matches_oracle_per_shot(gpu, oracle, pk):
         assert np.array_equal(getattr(res, k), ref[k]), k
     assert res.failures == ref["failures"] and res.sector_iters == ref["sector_iters"]
     assert 0 < res.failures < S
+
+
+@pytest.mark.parametrize("name,tb,vpl", [("LP_Matg8_L16_Dmin12", 128, 5), ("LP_Matg8_L21_Dmin16", 192, 5)])
+def test_m2s8_small_lp_codes_at_fewer_threads_match_oracle(gpu, oracle, monkeypatch, name, tb, vpl):
+    """The Threshold notebook's smaller lifted-product codes (544 / 714 columns; they came out at 256
+    threads x 3 variables, below the family's 4-6, and ran on engine 2 before round 6) run the rows-of-8
+    family with packed addresses at 128 / 192 threads x 5 variables: bit-exact against the oracle and
+    against their old route (QLDPC_M2S8_SMALL=0)."""
+    code = codes.get_code(name)
+    for sector in ("hz", "hx"):
+        H = getattr(code, sector)
+        for p, seed in ((0.03, 1), (0.08, 2)):
+            synd = _synd(H, p, 384, seed)
+            dec = _dec(H, p, 54, pk=True)
+            g = dec.geometry()
+            assert (g["engine"], g["kernel_id"], g["threads"], g["vars_per_thread"]) == \
+                (3, FAM[vpl <= 5], tb, vpl), g
+            c, i, v = dec.decode_batch(synd)
+            oc, oi, ov = oracle.bp_decode_batch(H, p, 54, "minimum_sum", 0.625, synd, 64)
+            assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64)), p
+            monkeypatch.setenv("QLDPC_M2S8_SMALL", "0")
+            d0 = _dec(H, p, 54, pk=True)
+            monkeypatch.delenv("QLDPC_M2S8_SMALL")
+            assert d0.geometry()["engine"] == 2
+            c0, i0, v0 = d0.decode_batch(synd)
+            assert np.array_equal(c, c0) and np.array_equal(i, i0) and np.array_equal(v, v0), p

@@ -1,6 +1,6 @@
 """Time one fp64 space-time decode_batch on a given code / round count (round-6 routing A/B).
 
-    QLDPC_E3_TAIL=0|1 python tools/st_route_ab.py [code] [t0] [p] [syndromes]
+    QLDPC_E3_TAIL=0|1 python tools/st_route_ab.py [code] [t0] [p] [syndromes]     (t0 = 0: hz itself)
 
 Builds the hz space-time decoder as bench.py --workload phenl does (min-sum alpha 0.625, max_iter
 int(n/10), fp64), decodes i.i.d.-error syndromes generated on the GPU, one warm-up launch then three
@@ -23,8 +23,10 @@ p = float(sys.argv[3]) if len(sys.argv) > 3 else 0.01
 B = int(sys.argv[4]) if len(sys.argv) > 4 else 32768
 code = codes.get_code(name)
 n = code.N
-Hst = codes.space_time_csr(code.hz, t0)
-dec = DeviceBP(Hst, np.hstack([p * np.ones(n), p * np.ones(code.hz.shape[0])] * t0), max_iter=int(n / 10), precision=64)
+# t0 = 0: hz itself (the data-error / BP+OSD decoders)
+Hst = codes.space_time_csr(code.hz, t0) if t0 > 0 else codes.CSR.from_dense(code.hz)
+probs = np.hstack([p * np.ones(n), p * np.ones(code.hz.shape[0])] * t0) if t0 > 0 else p * np.ones(n)
+dec = DeviceBP(Hst, probs, max_iter=int(n / 10), precision=64)
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev)
 g.manual_seed(7)
@@ -47,7 +49,7 @@ e1.record()
 torch.cuda.synchronize(dev)
 geo = dec.geometry()
 print(json.dumps({"code": name, "t0": t0, "p": p, "syndromes": B, "shape": [Hst.m, Hst.n],
-                  "E3_TAIL": os.environ.get("QLDPC_E3_TAIL", "1"), "engine": geo["engine"],
+                  "E3_TAIL": os.environ.get("QLDPC_E3_TAIL", "1"), "env": {k: v for k, v in os.environ.items() if k.startswith("QLDPC_")}, "engine": geo["engine"],
                   "kernel_id": geo["kernel_id"], "threads": geo["threads"], "vpl": geo["vars_per_thread"],
                   "lds_bytes": geo["lds_bytes"], "ms": e0.elapsed_time(e1) / 3,
                   "mean_iters": float(iters.float().mean())}))
