@@ -1595,6 +1595,16 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
         return fail(set_err(QLDPC_EHIP, "upload row degrees"));
     }
   }
+  if (!kern && (bp->engine == 3 || bp->engine == 4) && env_int("QLDPC_HBM_FALLBACK", 1) != 0) {
+    // no kernel compiled for this engine-3/4 geometry (e.g. fp32 images past 64 KiB at 8 variables per
+    // thread, GenBicycleA4 over five rounds): the HBM-resident engine serves any graph
+    bp->tail = bp->m2s = bp->fb = bp->m2s_pk = bp->vslots_dummy = bp->d3k = bp->d2k = 0;
+    bp->nw = bp->live_last = 0;
+    bp->rperm.release();
+    bp->rowtab.release();
+    bp->rdeg.release();
+    return setup_hbm();
+  }
   if (!kern) return fail(set_err(QLDPC_ENOTSUP, "no kernel variant"));
   if ((rc = bp->vchk.alloc(vchk.size() * 4)) || (rc = bp->llr.alloc((size_t)bp->VPL * bp->TB * tsize))) return fail(rc);
   if (hipMemcpy(bp->vchk.p, vchk.data(), vchk.size() * 4, hipMemcpyHostToDevice) != hipSuccess)

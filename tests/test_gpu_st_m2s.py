@@ -60,3 +60,22 @@ def test_space_time_one_word_family_matches_oracle(gpu, oracle, monkeypatch, nam
             for k in env:
                 monkeypatch.delenv(k)
             assert np.array_equal(c2, c) and np.array_equal(i2, i) and np.array_equal(v2, v), (name, p, env)
+
+
+def test_graph_without_a_compiled_engine3_variant_falls_back_to_hbm(gpu, oracle):
+    """GenBicycleA4 over five rounds in fp32 (2555 x 7665, rows of 8): engine 3's dword-scaled fp32
+    family is compiled for 3-7 variables per thread and this geometry needs 8 (round 6: creation failed
+    with "no kernel variant"); the decoder now falls back to the HBM-resident engine, bit-exact against
+    the oracle's fp32 restatement."""
+    from qldpc_fault_tolerance_amd.engine import DeviceBP
+
+    code = codes.get_code("GenBicycleA4")
+    Hst = codes.space_time_csr(code.hz, 5)
+    n, p = code.N, 0.01
+    probs = np.hstack([p * np.ones(n), p * np.ones(code.hz.shape[0])] * 5)
+    dec = DeviceBP(Hst, probs, max_iter=int(n / 10), precision=32)
+    assert dec.geometry()["engine"] == 6, dec.geometry()
+    synd, Hd = _synd(Hst, p, 64, seed=9)
+    c, i, v = dec.decode_batch(synd)
+    oc, oi, ov = oracle.bp_decode_batch(Hd, probs, int(n / 10), "minimum_sum", 0.625, synd, 32)
+    assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64))
