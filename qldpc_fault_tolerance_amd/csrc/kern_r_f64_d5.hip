@@ -14,6 +14,8 @@ static SVariant pick_d5(int vpl, int d3k) {
   }
 }
 SVariant get_rvariant_f64_w_d5(int vpl, int d3k, int nch) {
-  return nch == 4 ? pick_d5<4>(vpl, d3k) : nch == 3 ? pick_d5<3>(vpl, d3k) : SVariant{nullptr, nullptr, nullptr, nullptr};
+  // (nch 5: rows of 9-10, the lifted-product [h | I] graphs of CodeSimulator_Phenon's decoder1, round 6)
+  return nch == 4 ? pick_d5<4>(vpl, d3k) : nch == 3 ? pick_d5<3>(vpl, d3k) : nch == 5 ? pick_d5<5>(vpl, d3k)
+                                                                           : SVariant{nullptr, nullptr, nullptr, nullptr};
 }
 }  // namespace qldpc

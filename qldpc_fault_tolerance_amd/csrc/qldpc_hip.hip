@@ -72,8 +72,9 @@ SVariant get_rvariant(int engine, int precision, int vpl, int d3k, int dmax) {
 // 256-VGPR budget, own v2c in VGPRs, compile-time D3K); QLDPC_F64W=0 disables.
 bool use_f64w(int engine, int precision, int dmax, int tb, int vpl, int ea_shift, int nch) {
   // column degree 5 (kern_r_f64_d5.hip): VPL 4-5 only
+  // (column degree 5 also with rows of 9-10 = 5 chunks: the lifted-product [h | I] graphs, round 6)
   return engine == 3 && precision == 64 && (dmax == 4 || (dmax == 5 && vpl <= 5)) && ea_shift == 0 && tb <= 256 &&
-         vpl >= 4 && vpl <= 8 && (nch == 3 || nch == 4) && env_int("QLDPC_F64W", 1) != 0;
+         vpl >= 4 && vpl <= 8 && (nch == 3 || nch == 4 || (dmax == 5 && nch == 5)) && env_int("QLDPC_F64W", 1) != 0;
 }
 
 // fp32 engine-3 kernels with the compile-time 2-chunk check phase (rows of <= 8 edges);
@@ -1268,6 +1269,16 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       }
     }
     int m2s8_vpt = 0;  // (the rows-of-8 family's 128-thread geometry for small graphs, below)
+    // fp64 column degree 5 graphs that come out at 512 threads x <= 3 variables (LP_Matg8_L21's [h | I],
+    // 315 x 1029): the two-word degree-5 family at 256 threads x 5 variables instead of engine 2
+    // (round 6; QLDPC_D5_256=0 keeps the old geometry)
+    if (bp->engine == 3 && precision == 64 && DM == 5 && vars_per_thread <= 0 && env_int("QLDPC_TB", 0) <= 0 &&
+        env_int("QLDPC_D5_256", 1) != 0 && g->max_row > 8) {
+      int tb = 0, vpl = 0, tb5 = 0, vpl5 = 0;
+      if (!choose_rgeometry(g->n, g->m, 0, tb, vpl, pref, vmax) && tb > 256 &&
+          !choose_rgeometry(g->n, g->m, 5, tb5, vpl5, pref, vmax) && tb5 <= 256)
+        vars_per_thread = 5;
+    }
     // the same family for rows of 8 and column degree 5 (kern_r_f64_m2s8.hip, engine id 10103): the
     // lifted-product codes (LP_Matg8_L30: 750 degree-3 and 270 degree-5 columns, rows of 8).  Rows of
     // 4 chunks, no tail array.  Slots k >= D3K hold 5 edge slots; a real variable with fewer edges

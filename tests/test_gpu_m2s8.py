@@ -172,3 +172,33 @@ def test_m2s8_small_lp_codes_at_fewer_threads_match_oracle(gpu, oracle, monkeypa
             assert d0.geometry()["engine"] == 2
             c0, i0, v0 = d0.decode_batch(synd)
             assert np.array_equal(c, c0) and np.array_equal(i, i0) and np.array_equal(v, v0), p
+
+
+@pytest.mark.parametrize("name,vpl", [("LP_Matg8_L16_Dmin12", 4), ("LP_Matg8_L21_Dmin16", 5)])
+def test_lp_h_identity_graphs_on_the_degree5_family_match_oracle(gpu, oracle, monkeypatch, name, vpl):
+    """[h | I] of the Threshold notebook's lifted-product codes (CodeSimulator_Phenon's decoder1 graph,
+    ``src/Simulators.py:189-250``: rows of 9, columns of degree 1 / 3 / 5) on the two-word degree-5
+    family with 5-chunk rows at 256 threads (round 6; engine 2 before): bit-exact against the oracle and
+    the old route (QLDPC_F64W=0)."""
+    from qldpc_fault_tolerance_amd.engine import DeviceBP
+
+    h = codes.get_code(name).hz
+    H = np.hstack([h, np.eye(h.shape[0], dtype=np.uint8)])
+    mi = int(h.shape[1] / 30)
+    for p, seed in ((0.02, 3), (0.06, 4)):
+        synd = _synd(H, p, 384, seed)
+        dec = DeviceBP(H, p * np.ones(H.shape[1]), max_iter=mi, precision=64)
+        g = dec.geometry()
+        assert (g["engine"], g["kernel_id"], g["threads"], g["vars_per_thread"], g["row_chunks"]) == \
+            (3, 103, 256, vpl, 5), g
+        c, i, v = dec.decode_batch(synd)
+        oc, oi, ov = oracle.bp_decode_batch(H, p, mi, "minimum_sum", 0.625, synd, 64)
+        assert np.array_equal(i, oi) and np.array_equal(v, ov) and np.array_equal(c, oc.astype(np.int64)), p
+        monkeypatch.setenv("QLDPC_F64W", "0")
+        monkeypatch.setenv("QLDPC_D5_256", "0")
+        d0 = DeviceBP(H, p * np.ones(H.shape[1]), max_iter=mi, precision=64)
+        monkeypatch.delenv("QLDPC_F64W")
+        monkeypatch.delenv("QLDPC_D5_256")
+        assert d0.geometry()["engine"] == 2
+        c0, i0, v0 = d0.decode_batch(synd)
+        assert np.array_equal(c, c0) and np.array_equal(i, i0) and np.array_equal(v, v0), p
