@@ -10,6 +10,10 @@ static SVariant pick_d5(int vpl, int d3k) {
   switch (vpl) {
     case 4: return pick_rd3k<double, 4, 103, 5, 256, NCH>(d3k);
     case 5: return pick_rd3k<double, 5, 103, 5, 256, NCH>(d3k);
+    // 6 variables (rows of 9-10 only: LP_Matg8_L30's [h | I], 1470 columns at 256 threads; <= 212 VGPRs)
+    case 6:
+      if constexpr (NCH == 5) return pick_rd3k<double, 6, 103, 5, 256, NCH>(d3k);
+      return SVariant{nullptr, nullptr, nullptr, nullptr};
     default: return SVariant{nullptr, nullptr, nullptr, nullptr};
   }
 }

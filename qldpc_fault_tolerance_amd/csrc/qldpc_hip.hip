@@ -73,8 +73,9 @@ SVariant get_rvariant(int engine, int precision, int vpl, int d3k, int dmax) {
 bool use_f64w(int engine, int precision, int dmax, int tb, int vpl, int ea_shift, int nch) {
   // column degree 5 (kern_r_f64_d5.hip): VPL 4-5 only
   // (column degree 5 also with rows of 9-10 = 5 chunks: the lifted-product [h | I] graphs, round 6)
-  return engine == 3 && precision == 64 && (dmax == 4 || (dmax == 5 && vpl <= 5)) && ea_shift == 0 && tb <= 256 &&
-         vpl >= 4 && vpl <= 8 && (nch == 3 || nch == 4 || (dmax == 5 && nch == 5)) && env_int("QLDPC_F64W", 1) != 0;
+  return engine == 3 && precision == 64 && (dmax == 4 || (dmax == 5 && (vpl <= 5 || (vpl == 6 && nch == 5)))) &&
+         ea_shift == 0 && tb <= 256 && vpl >= 4 && vpl <= 8 && (nch == 3 || nch == 4 || (dmax == 5 && nch == 5)) &&
+         env_int("QLDPC_F64W", 1) != 0;
 }
 
 // fp32 engine-3 kernels with the compile-time 2-chunk check phase (rows of <= 8 edges);
@@ -1153,7 +1154,8 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       return setup_hbm();
     }
     // degree-5/6 variables hold 2.5x the registers of degree-4 ones: fewer per thread
-    const int pref = DM == 4 ? kPrefVplR : 4, vmax = DM == 4 ? kMaxVplR : 5;
+    const int pref = DM == 4 ? kPrefVplR : 4;
+    int vmax = DM == 4 ? kMaxVplR : 5;
     // images of 64-256 KiB (space-time graphs): engine 3 with dword-scaled addresses (fp32, 4 slots)
     if (bp->engine == 3 && precision == 32 && DM == 4 && !r_fits(3, vslots, g->m, tsize) &&
         r_fits(3, vslots, g->m, tsize, 2) && env_int("QLDPC_E3_BIG", 1) != 0)
@@ -1269,15 +1271,20 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
       }
     }
     int m2s8_vpt = 0;  // (the rows-of-8 family's 128-thread geometry for small graphs, below)
-    // fp64 column degree 5 graphs that come out at 512 threads x <= 3 variables (LP_Matg8_L21's [h | I],
-    // 315 x 1029): the two-word degree-5 family at 256 threads x 5 variables instead of engine 2
-    // (round 6; QLDPC_D5_256=0 keeps the old geometry)
+    // fp64 column degree 5 graphs that come out at 512 threads x <= 3 variables (LP_Matg8_L21 / L30's
+    // [h | I], 315 x 1029 / 450 x 1470): the two-word degree-5 family at 256 threads x 5 / 6 variables
+    // instead of engine 2 (round 6; QLDPC_D5_256=0 keeps the old geometry)
     if (bp->engine == 3 && precision == 64 && DM == 5 && vars_per_thread <= 0 && env_int("QLDPC_TB", 0) <= 0 &&
-        env_int("QLDPC_D5_256", 1) != 0 && g->max_row > 8) {
-      int tb = 0, vpl = 0, tb5 = 0, vpl5 = 0;
-      if (!choose_rgeometry(g->n, g->m, 0, tb, vpl, pref, vmax) && tb > 256 &&
-          !choose_rgeometry(g->n, g->m, 5, tb5, vpl5, pref, vmax) && tb5 <= 256)
-        vars_per_thread = 5;
+        env_int("QLDPC_D5_256", 1) != 0 && g->max_row > 8 && g->max_row <= 10) {
+      int tb = 0, vpl = 0;
+      if (!choose_rgeometry(g->n, g->m, 0, tb, vpl, pref, vmax) && tb > 256)
+        for (int v = 5; v <= 6 && vars_per_thread <= 0; ++v) {
+          int tb5 = 0, vpl5 = 0;
+          if (!choose_rgeometry(g->n, g->m, v, tb5, vpl5, pref, 6) && tb5 <= 256) {
+            vars_per_thread = v;
+            vmax = std::max(vmax, v);
+          }
+        }
     }
     // the same family for rows of 8 and column degree 5 (kern_r_f64_m2s8.hip, engine id 10103): the
     // lifted-product codes (LP_Matg8_L30: 750 degree-3 and 270 degree-5 columns, rows of 8).  Rows of

@@ -174,7 +174,7 @@ def test_m2s8_small_lp_codes_at_fewer_threads_match_oracle(gpu, oracle, monkeypa
             assert np.array_equal(c, c0) and np.array_equal(i, i0) and np.array_equal(v, v0), p
 
 
-@pytest.mark.parametrize("name,vpl", [("LP_Matg8_L16_Dmin12", 4), ("LP_Matg8_L21_Dmin16", 5)])
+@pytest.mark.parametrize("name,vpl", [("LP_Matg8_L16_Dmin12", 4), ("LP_Matg8_L21_Dmin16", 5), ("LP_Matg8_L30_Dmin20", 6)])
 def test_lp_h_identity_graphs_on_the_degree5_family_match_oracle(gpu, oracle, monkeypatch, name, vpl):
     """[h | I] of the Threshold notebook's lifted-product codes (CodeSimulator_Phenon's decoder1 graph,
     ``src/Simulators.py:189-250``: rows of 9, columns of degree 1 / 3 / 5) on the two-word degree-5

@@ -8,7 +8,7 @@ mkdir -p "$O"
 timeout -k 10 900 python -u -m pytest -q -x --timeout 400 --timeout-method thread tests/test_gpu_m2s8.py tests/test_gpu_parity.py tests/test_gpu_phenl.py \
   > "$O/pytest.out" 2>&1 || { echo "pytest failed"; tail -40 "$O/pytest.out"; exit 1; }
 tail -2 "$O/pytest.out"
-for spec in "LP_Matg8_L16_Dmin12 1" "LP_Matg8_L21_Dmin16 1"; do
+for spec in "LP_Matg8_L30_Dmin20 1" "LP_Matg8_L16_Dmin12 1" "LP_Matg8_L21_Dmin16 1"; do
   for T in 1 0; do
     for P in 0.02 0.06; do
       # shellcheck disable=SC2086
