@@ -1267,6 +1267,11 @@ static int create_min_sum(qldpc_graph* g, const double* channel_probs, int32_t m
           bp->vslots_dummy = nd;
           bp->nw = P.nw;
           bp->live_last = P.live_last;
+#if QLDPC_DIAG_NOLAST
+          // diagnostic builds only (results invalid): no wave runs the last variable slot, to time the
+          // cost of the waves that hold it
+          bp->live_last = 0;
+#endif
         }
       }
     }
