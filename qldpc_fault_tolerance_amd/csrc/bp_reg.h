@@ -88,6 +88,13 @@
 #ifndef QLDPC_M2S_RPTR
 #define QLDPC_M2S_RPTR 1
 #endif
+// m2s check phase of the space-time family: rows in pairs, the second row's first QLDPC_M2S_ROWPAIR
+// chunks loaded before the first row is reduced (A/B build; 4 = the whole row spills).  Measured slower:
+// config 5 kernel 94.5 ms with one row at a time against 96.1-96.6 ms with 1-3 chunks ahead
+// (profiles/r06/config5/rowpair/), so 0 (one row at a time) is the product
+#ifndef QLDPC_M2S_ROWPAIR
+#define QLDPC_M2S_ROWPAIR 0
+#endif
 // m2s families: each variable slot's previous decisions as a wave lane mask (SGPRs): the flip test
 // is a scalar xor of two masks instead of a bit extract and compare per variable and iteration
 // (not the dword-scaled 1024-thread space-time family: measured 1-2% slower with it, r06g)
@@ -1192,26 +1199,36 @@ __device__ inline int m_check(unsigned char* smem, const RLayout& Ly, int m, int
   uint32_t tp = sb + Ly.t + (uint32_t)tid * (uint32_t)sizeof(T);
   uint32_t fp = sb + Ly.f + 4u * (uint32_t)(tid + 1);
   uint32_t cp = sb + (uint32_t)(tid + 1) * (uint32_t)sizeof(T);
-  for (int i = tid; i < m; i += TB, ++q) {
-    if constexpr (AP) asm volatile("" : "+v"(rb));
-    const uint32_t roff = AP ? rb : Ly.v + 16u + (uint32_t)i * rstride;
-    const uint32_t toff = AP ? tp : Ly.t + (uint32_t)i * (uint32_t)sizeof(T);
-    const uint32_t fo = AP ? fp : Ly.f + 4u * (uint32_t)(i + 1);
-    const uint32_t co = AP ? cp : (uint32_t)(i + 1) * (uint32_t)sizeof(T);
+  // one row: its loads, then its reduction and stores (kept apart so that rows can be loaded in pairs)
+  struct RowIn {
     VT cur[NCH];
+    T tcur;
+    uint32_t fcur, roff, toff, fo, co;
+  };
+  // (c0..c1: the chunks to load; the tail and F word with the last chunk)
+  auto load_row = [&](RowIn& r, int i, uint32_t rb_, uint32_t tp_, uint32_t fp_, uint32_t cp_, int c0 = 0, int c1 = NCH) {
+    r.roff = AP ? rb_ : Ly.v + 16u + (uint32_t)i * rstride;
+    r.toff = AP ? tp_ : Ly.t + (uint32_t)i * (uint32_t)sizeof(T);
+    r.fo = AP ? fp_ : Ly.f + 4u * (uint32_t)(i + 1);
+    r.co = AP ? cp_ : (uint32_t)(i + 1) * (uint32_t)sizeof(T);
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) cur[c] = lds_ld<VT, AP>(smem, roff + coff[c]);
-    T tcur = (T)0;
-    if (TAIL) tcur = lds_ld<T, AP>(smem, toff);
-    const uint32_t fcur = lds_ld<uint32_t, AP>(smem, fo);
+    for (int c = 0; c < NCH; ++c)
+      if (c >= c0 && c < c1) r.cur[c] = lds_ld<VT, AP>(smem, r.roff + coff[c]);
+    if (c1 == NCH) {
+      r.tcur = (T)0;
+      if (TAIL) r.tcur = lds_ld<T, AP>(smem, r.toff);
+      r.fcur = lds_ld<uint32_t, AP>(smem, r.fo);
+    }
+  };
+  auto reduce_row = [&](const RowIn& r, int qq) {
     uint32_t s;
     if (FIRST) {
-      s = ((fcur >> 1) ^ (fcur >> 2)) & 1u;
-      sbits |= s << q;
-      lds_st<uint32_t, AP>(smem, fo, (fcur & 4u) | ((fcur >> 2) & 1u));
+      s = ((r.fcur >> 1) ^ (r.fcur >> 2)) & 1u;
+      sbits |= s << qq;
+      lds_st<uint32_t, AP>(smem, r.fo, (r.fcur & 4u) | ((r.fcur >> 2) & 1u));
     } else {
-      s = (sbits >> q) & 1u;
-      mism |= (int)((fcur ^ s) & 1u);
+      s = (sbits >> qq) & 1u;
+      mism |= (int)((r.fcur ^ s) & 1u);
     }
     double f1 = FT<T>::val(FT<T>::kSent), f2 = f1;
     uint32_t px = s ? 0x80000000u : 0u;
@@ -1220,7 +1237,7 @@ __device__ inline int m_check(unsigned char* smem, const RLayout& Ly, int m, int
     for (int c = 0; c < NCH; ++c) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        const double x = V16<T>::get(cur[c], k);
+        const double x = V16<T>::get(r.cur[c], k);
         aoff = __builtin_fabs(x) < f1 ? coff[c] + 8u * (uint32_t)k : aoff;
         double t;
         asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x));
@@ -1230,26 +1247,58 @@ __device__ inline int m_check(unsigned char* smem, const RLayout& Ly, int m, int
       uint32_t p;
       asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96"
           : "=v"(p)
-          : "v"(px), "v"((uint32_t)(FT<T>::bits(cur[c].x) >> 32)), "v"((uint32_t)(FT<T>::bits(cur[c].y) >> 32)));
+          : "v"(px), "v"((uint32_t)(FT<T>::bits(r.cur[c].x) >> 32)), "v"((uint32_t)(FT<T>::bits(r.cur[c].y) >> 32)));
       px = p;
     }
-    uint32_t amin = roff + aoff;
+    uint32_t amin = r.roff + aoff;
     if (TAIL) {
-      const double x = (double)tcur;
-      amin = __builtin_fabs(x) < f1 ? toff : amin;
+      const double x = (double)r.tcur;
+      amin = __builtin_fabs(x) < f1 ? r.toff : amin;
       double t;
       asm("v_max_f64 %0, %1, |%2|" : "=v"(t) : "v"(f1), "v"(x));
       asm("v_min_f64 %0, %1, %2" : "=v"(f2) : "v"(f2), "v"(t));
       asm("v_min_f64 %0, %1, |%2|" : "=v"(f1) : "v"(f1), "v"(x));
-      px ^= (uint32_t)(FT<T>::bits(tcur) >> 32);
+      px ^= (uint32_t)(FT<T>::bits(r.tcur) >> 32);
     }
     const U par = (U)(px & 0x80000000u) << 32;
-    lds_st<U, AP>(smem, co, FT<T>::bits(f1) | par);
+    lds_st<U, AP>(smem, r.co, FT<T>::bits(f1) | par);
     lds_st<U, AP>(smem, amin, FT<T>::bits(f2) | par);
-    rb += (uint32_t)TB * rstride;
-    tp += (uint32_t)TB * (uint32_t)sizeof(T);
-    fp += 4u * (uint32_t)TB;
-    cp += (uint32_t)TB * (uint32_t)sizeof(T);
+  };
+  const uint32_t drb = (uint32_t)TB * rstride, dtp = (uint32_t)TB * (uint32_t)sizeof(T), dfp = 4u * (uint32_t)TB,
+                 dcp = (uint32_t)TB * (uint32_t)sizeof(T);
+  // QLDPC_M2S_ROWPAIR (the space-time family: one decode per CU, 1-2 rows per thread): both rows' loads
+  // are issued before the first row is reduced (their addresses never alias: distinct rows, tails, F
+  // words and CS entries), so the second row's LDS latency hides under the first row's arithmetic
+  if constexpr (QLDPC_M2S_ROWPAIR > 0 && TAIL && NCH == 4) {
+    for (int i = tid; i < m; i += 2 * TB, q += 2) {
+      if constexpr (AP) asm volatile("" : "+v"(rb));
+      RowIn a, b;
+      load_row(a, i, rb, tp, fp, cp);
+      const bool hb = i + TB < m;
+      // the second row's first QLDPC_M2S_ROWPAIR chunks ahead, the rest after the first row (VGPRs)
+      constexpr int PC = QLDPC_M2S_ROWPAIR < NCH ? QLDPC_M2S_ROWPAIR : NCH;
+      if (hb) load_row(b, i + TB, rb + drb, tp + dtp, fp + dfp, cp + dcp, 0, PC);
+      reduce_row(a, q);
+      if (hb) {
+        if constexpr (PC < NCH) load_row(b, i + TB, rb + drb, tp + dtp, fp + dfp, cp + dcp, PC, NCH);
+        reduce_row(b, q + 1);
+      }
+      rb += 2 * drb;
+      tp += 2 * dtp;
+      fp += 2 * dfp;
+      cp += 2 * dcp;
+    }
+  } else {
+    for (int i = tid; i < m; i += TB, ++q) {
+      if constexpr (AP) asm volatile("" : "+v"(rb));
+      RowIn a;
+      load_row(a, i, rb, tp, fp, cp);
+      reduce_row(a, q);
+      rb += drb;
+      tp += dtp;
+      fp += dfp;
+      cp += dcp;
+    }
   }
   return mism;
 }
