@@ -88,6 +88,10 @@
 #ifndef QLDPC_M2S_RPTR
 #define QLDPC_M2S_RPTR 1
 #endif
+// two-word check phase (r_check_c): absolute LDS addresses for the rows, tails and CS stores
+#ifndef QLDPC_RC_RPTR
+#define QLDPC_RC_RPTR 1
+#endif
 // m2s check phase of the space-time family: rows in pairs, the second row's first QLDPC_M2S_ROWPAIR
 // chunks loaded before the first row is reduced (A/B build; 4 = the whole row spills).  Measured slower:
 // config 5 kernel 94.5 ms with one row at a time against 96.1-96.6 ms with 1-3 chunks ahead
@@ -882,12 +886,23 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
 #pragma unroll
   for (int c = 0; c < NCH; ++c) coff[c] = kRot ? (((uint32_t)c + rot) & (uint32_t)(NCH - 1)) * 16u : (uint32_t)c * 16u;
   // rows are loaded PFC (1 or 2) rows ahead of the one being reduced
+  // (QLDPC_RC_RPTR: absolute LDS row / tail / CS addresses, as the m2s check phase's pointers; fp64
+  // only: the two-word tail family +1.5 %, the fp32 families -0.6 %, profiles/r06/rc_rptr/)
+  constexpr bool RP = QLDPC_RC_RPTR != 0 && sizeof(T) == 8;
+  const uint32_t sbase = RP ? lds_base(smem) : 0u;
   auto load = [&](int r, VT (&v)[NCH], T& tv, uint32_t& fv) {
     if (r < m) {
-      const unsigned char* row = smem + Ly.v + 16 + (uint32_t)r * rstride;
+      if constexpr (RP) {
+        const uint32_t row = sbase + Ly.v + 16u + (uint32_t)r * rstride;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) v[c] = *reinterpret_cast<const VT*>(row + coff[c]);
-      if (TAIL) tv = lds_at<T>(smem, Ly.t + (uint32_t)r * (uint32_t)sizeof(T));
+        for (int c = 0; c < NCH; ++c) v[c] = lds_ld<VT, true>(nullptr, row + coff[c]);
+        if (TAIL) tv = lds_ld<T, true>(nullptr, sbase + Ly.t + (uint32_t)r * (uint32_t)sizeof(T));
+      } else {
+        const unsigned char* row = smem + Ly.v + 16 + (uint32_t)r * rstride;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) v[c] = *reinterpret_cast<const VT*>(row + coff[c]);
+        if (TAIL) tv = lds_at<T>(smem, Ly.t + (uint32_t)r * (uint32_t)sizeof(T));
+      }
       fv = f_ld<ENG>(smem, f_off<ENG>(Ly, r + 1));
     }
   };
@@ -969,7 +984,11 @@ __device__ inline int r_check_c(unsigned char* smem, const RLayout& Ly, int m, i
       st.a = FT<T>::bits(f1) | (px & kS);
       st.b = FT<T>::bits(f2) | (QLDPC_F32_C2V4 ? (px & kS) : 0u);  // m2 | parity (r_var_one's 4-VALU c2v)
     }
-    lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
+    if constexpr (RP) {
+      lds_st<typename CSEntry<T>::type, true>(nullptr, sbase + (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T)), st);
+    } else {
+      lds_at<typename CSEntry<T>::type>(smem, (uint32_t)(i + 1) * (uint32_t)(2 * sizeof(T))) = st;
+    }
     if (PFC == 2) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
