@@ -1730,6 +1730,17 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
         int jv[VPL];
 #pragma unroll
         for (int k = 0; k < VPL; ++k) jv[k] = S.perm[k * TB + tidl];
+        // the per-shot class cache (SMcArgs::cls_cache, both sectors with Philox draws): the first
+        // sector's pass stores this thread's classes, the second reads them back (same thread, same
+        // address: program order) instead of drawing again
+        uint16_t* cc = nullptr;
+        bool cc_read = false;
+        uint32_t cw = 0;
+        if (A->cls_cache && !A->uniforms && VPL <= 8) {
+          cc = A->cls_cache + ((long long)blockIdx.x * A->chunk + sh) * TB + tidl;
+          cc_read = q == A->sec_id1;
+          if (cc_read) cw = *cc;
+        }
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
           const int j = jv[k];
@@ -1738,9 +1749,12 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
             if (A->uniforms) {
               const double u = A->uniforms[sl * (long long)n + j];
               cls = (u < A->t1) ? 2u : (A->t1 <= u && u < A->t2) ? 1u : (A->t2 <= u && u < A->t3) ? 3u : 0u;
+            } else if (cc_read) {
+              cls = (cw >> (2 * k)) & 3u;
             } else {
               const unsigned long long kk = philox_k53(A->seed, gshot, (uint32_t)j);
               cls = (kk < A->K1) ? 2u : (kk < A->K2) ? 1u : (kk < A->K3) ? 3u : 0u;
+              cw |= cls << (2 * k);
             }
             const uint32_t e = (q == 0) ? (cls & 1u) : (cls >> 1);
             eb |= e << k;
@@ -1759,6 +1773,7 @@ __device__ void r_pass(const SSector& S, int q, long long c0, int cn, unsigned c
             }
           }
         }
+        if (cc && !cc_read) *cc = (uint16_t)cw;
       } else {
         const uint8_t* srow = D->synd + (c0 + sh) * (long long)m;
         for (int i = tidl; i < m; i += TB) {  // i = check label (engine 3: S.rperm maps it to the check)

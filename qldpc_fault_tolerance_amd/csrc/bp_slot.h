@@ -85,6 +85,9 @@ struct SMcArgs {
   long long* c_shot[2];   // [cap] launch-relative shot, -1 = converged at max_iter (no OSD)
   long long c_cap;
   unsigned long long* stamps;  // diagnostic builds (QLDPC_STAMPS): per-segment cycle sums, else NULL
+  // both sectors: the first sector's pass leaves each shot's sampled 3-way classes (2 bits per variable
+  // slot, [grid][chunk][TB]) for the second's, which then skips its Philox draws; NULL = both draw
+  uint16_t* cls_cache;
 };
 
 struct SDecArgs {

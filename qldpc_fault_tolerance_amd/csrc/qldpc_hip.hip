@@ -2059,6 +2059,7 @@ int qldpc_mc_destroy(qldpc_mc* mc) {
   mc->lmask[1].release();
   mc->counters.release();
   mc->work.release();
+  mc->cls_cache.release();
   staged_mc_release(mc);
   delete mc;
   return 0;
@@ -2176,6 +2177,19 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     const long long nchunks = (shot_count + a.chunk - 1) / a.chunk;
     if (nchunks > 0x7fffffffLL) return set_err(QLDPC_EINVAL, "too many shots for one launch (chunk count >= 2^31)");
     const long long grid = std::max<long long>(1, std::min<long long>(nchunks, want));
+    // both sectors drawing Philox errors: the first sector's pass caches each shot's classes for the
+    // second (SMcArgs::cls_cache; [grid][chunk][TB] u16, one Philox draw per (shot, variable) instead of
+    // two; QLDPC_CLS_CACHE=0 draws in both passes)
+    a.cls_cache = nullptr;
+    if (a.nsec == 2 && !d_uniforms && mc->VPL <= 8 && env_int("QLDPC_CLS_CACHE", 1) != 0) {
+      const size_t need = (size_t)grid * (size_t)a.chunk * (size_t)mc->TB * 2;
+      if (mc->cls_cache.bytes < need) {
+        mc->cls_cache.release();
+        int rc = mc->cls_cache.alloc(need);
+        if (rc) return rc;
+      }
+      a.cls_cache = static_cast<uint16_t*>(mc->cls_cache.p);
+    }
     // BP+OSD: capture buffers with one slot per shot of this launch (<= the budgeted slots)
     hipStream_t st = (hipStream_t)stream;
     if (bposd) {

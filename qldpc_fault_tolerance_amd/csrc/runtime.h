@@ -112,6 +112,7 @@ struct qldpc_mc {
   qldpc_rt::DevBuf lmask[2];
   qldpc_rt::DevBuf counters;
   qldpc_rt::DevBuf work;  // engine 3: chunk-queue head
+  qldpc_rt::DevBuf cls_cache;  // engine 3, both sectors: sampled classes of the first sector's pass (SMcArgs)
   int engine = 2, TB = 0, VPL = 0, DMAX = 0, NS = 1, precision = 64, lds_bytes = 0, blocks_per_cu = 0, cus = 0;
   int mmax = 0, vslots = 0, img_bytes = 0;
   int d3k = 0;  // engine 3: compile-time degree-3 slot count of the kernel (min over sectors)
