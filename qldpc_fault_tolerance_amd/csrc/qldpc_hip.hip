@@ -2181,8 +2181,11 @@ int qldpc_mc_launch(qldpc_mc* mc, double px, double py, double pz, uint64_t seed
     // second (SMcArgs::cls_cache; [grid][chunk][TB] u16, one Philox draw per (shot, variable) instead of
     // two; QLDPC_CLS_CACHE=0 draws in both passes)
     a.cls_cache = nullptr;
-    if (a.nsec == 2 && !d_uniforms && mc->VPL <= 8 && env_int("QLDPC_CLS_CACHE", 1) != 0) {
-      const size_t need = (size_t)grid * (size_t)a.chunk * (size_t)mc->TB * 2;
+    const size_t cc_need = (size_t)grid * (size_t)a.chunk * (size_t)mc->TB * 2;
+    // (bounded: 256 MiB covers every bundled code at the bench's launch sizes; huge launches of small
+    // codes, e.g. 10^9 shots of GenBicycleA1 at 1024-shot chunks, would need ~0.7 GB: they draw twice)
+    if (a.nsec == 2 && !d_uniforms && mc->VPL <= 8 && env_int("QLDPC_CLS_CACHE", 1) != 0 && cc_need <= (256u << 20)) {
+      const size_t need = cc_need;
       if (mc->cls_cache.bytes < need) {
         mc->cls_cache.release();
         int rc = mc->cls_cache.alloc(need);
